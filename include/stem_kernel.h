@@ -1,0 +1,202 @@
+/*
+ * stem_kernel.h -- C ABI of the MI355X stem-kernel Gram engine.
+ *
+ * Drop-in boundary for the reference's hot path (keio-bioinformatics/stem_kernel
+ * rev 296): the per-pair kernel DP evaluated for every (i,j) cell of the Gram
+ * matrix by KernelMatrix::calculate (common/kernel_matrix.h:67-105,
+ * common/kernel_matrix.cpp:485-575).  Each entry point below names the
+ * reference interface it replaces.  Plain pointers and sizes only; every call
+ * returns SK_OK (0) or a negative sk_status and never throws.  Host buffers are
+ * caller-owned; device buffers (sk_*_device) are addresses in the context's HIP
+ * device.
+ *
+ * Semantics kept from the reference:
+ *   - K(x,y) is evaluated with x = row example, y = column example, only for
+ *     i <= j, and mirrored (kernel_matrix.cpp:44-55): the DAG kernel is not
+ *     symmetric;
+ *   - normalisation K_ij / sqrt(K_ii K_jj), diagonal := 1, only when asked
+ *     (kernel_matrix.cpp:560-571); NaN from non-positive diagonals propagates;
+ *   - libsvm precomputed-kernel text layout (kernel_matrix.cpp:756-770).
+ */
+#ifndef STEM_KERNEL_H
+#define STEM_KERNEL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SK_ABI_VERSION 1
+
+typedef enum {
+  SK_OK = 0,
+  SK_ERR_INVALID = -1,    /* bad argument (the reference threw const char*) */
+  SK_ERR_HIP = -2,        /* HIP runtime error */
+  SK_ERR_NO_DEVICE = -3,  /* no gfx950 device / HIP unavailable */
+  SK_ERR_ALLOC = -4,      /* host or device allocation failed */
+  SK_ERR_RANGE = -5,      /* index out of range */
+  SK_ERR_UNSUPPORTED = -6 /* kernel kind / size not supported */
+} sk_status;
+
+/* Kernel kinds: the instantiations stem_kernel_lite/main.cpp:180-215 dispatches
+ * to, plus their components (stem_kernel_lite/def_kernel.h, ss_kernel.h). */
+typedef enum {
+  SK_SU_STEM = 0,      /* SuStemKernel(loop_gap, beta, band)        --no-string     */
+  SK_SI_STEM = 1,      /* SiStemKernel(loop_gap, stack, covar, band) --no-string --no-ribosum */
+  SK_SU_STR = 2,       /* StringKernel(gap, alpha)                                  */
+  SK_SI_STR = 3,       /* StringKernel(gap, match, mismatch)                        */
+  SK_SU_STEM_STR = 4,  /* SuStemStrKernel == StemStrKernel (ss_kernel.h)  default   */
+  SK_SI_STEM_STR = 5,  /* SiStemStrKernel                                --no-ribosum */
+  SK_LSU_STEM = 6,     /* LSuStemKernel: beta*log(K_stem)                --log --no-string */
+  SK_LSU_STEM_STR = 7  /* LSuStemStrKernel: beta*log K_stem + alpha*log K_str  --log */
+} sk_kernel_kind;
+
+/* Kernel parameters; defaults are stem_kernel_lite/main.cpp:103-149
+ * (sk_kernel_params_default). */
+typedef struct {
+  int32_t kind;       /* sk_kernel_kind */
+  uint32_t len_band;  /* --length-band (0 = off), default 10 */
+  double beta;        /* -b   0.3 */
+  double loop_gap;    /* -g   0.2 */
+  double stack;       /* -s   1.3 */
+  double covar;       /* -v   0.8 */
+  double alpha;       /* -a   0.2 */
+  double gap;         /* -G   0.8 */
+  double match;       /* --match 1.0 */
+  double mismatch;    /* --mismatch 0.8 */
+} sk_kernel_params;
+
+void sk_kernel_params_default(sk_kernel_params *p, int32_t kind);
+
+/* ---------------------------------------------------------------- context */
+typedef struct sk_context sk_context;
+
+/* One context per GPU (HIP device ordinal).  hip_stream may be NULL (the
+ * context creates its own) or a hipStream_t owned by the caller. */
+int sk_open(int device, void *hip_stream, sk_context **ctx);
+int sk_close(sk_context *ctx);
+const char *sk_strerror(int status);
+/* Last error message recorded on this context (static storage). */
+const char *sk_last_error(const sk_context *ctx);
+
+/* ---------------------------------------------------------------- examples */
+/* An example set: the reference's ExampleSet of (label, MData)
+ * (common/framework.h:308-353), built host-side and uploaded once. */
+typedef struct sk_dataset sk_dataset;
+
+int sk_dataset_create(sk_dataset **ds);
+int sk_dataset_free(sk_dataset *ds);
+
+/* Append one example = one alignment of n_rows rows of equal length.
+ * bpp_rows[r]: base-pairing probabilities of row r after erase_gap (length
+ * n_r = number of non-'-' characters), strict upper triangle packed row-major:
+ * p(i,j), 0<=i<j<n_r, at i*n_r - i*(i+1)/2 + (j-i-1).  This is the matrix
+ * Vienna pf_fold would give the reference (common/bpmatrix.cpp:151-177).
+ * th = --basepair.  use_bp = 0 builds MData(ma) (no DAG; string kernels only).
+ * Replaces: new MData(ma, th, pf_scale, opts)  stem_kernel_lite/data.cpp:466-487
+ * and DataLoader<MData>::get()  stem_kernel_lite/data.cpp:689-728. */
+int sk_dataset_add(sk_dataset *ds, const char *label, int n_rows,
+                   const char *const *rows, const double *const *bpp_rows,
+                   float th, int use_bp);
+int sk_dataset_size(const sk_dataset *ds);
+/* label of example i (pointer valid while ds lives) */
+const char *sk_dataset_label(const sk_dataset *ds, int i);
+/* DAG shape of example i: nodes, edges, bp_freq entries, roots, length */
+int sk_dataset_shape(const sk_dataset *ds, int i, int32_t *n_nodes,
+                     int32_t *n_edges, int32_t *n_bpfreq, int32_t *n_roots,
+                     int32_t *seq_len);
+/* DAG arrays of example i (packer-parity introspection; any pointer may be
+ * NULL).  Node arrays have n_nodes entries, edge arrays n_edges (node-major,
+ * reference list order), bp arrays n_bpfreq. */
+int sk_dataset_dag(const sk_dataset *ds, int i, uint32_t *first, uint32_t *last,
+                   uint32_t *n_edges, uint32_t *n_bpfreq, float *weight,
+                   uint32_t *max_pa, uint32_t *edge_to, uint32_t *edge_gaps,
+                   uint32_t *bp_code, float *bp_p, uint32_t *roots,
+                   float *pos_weight);
+
+/* Upload the packed example set to the context's device (idempotent).
+ * Must be called after the last sk_dataset_add and before any compute. */
+int sk_dataset_upload(sk_context *ctx, sk_dataset *ds);
+
+/* ---------------------------------------------------------------- compute */
+/* Train Gram matrix: K(train[i], train[j]) for i<=j, mirrored, optional
+ * normalisation.  out: n*n doubles, row-major, host memory.
+ * Replaces: KernelMatrix<double>::calculate(train, kernel, normalize, n_th)
+ *           common/kernel_matrix.cpp:485-575. */
+int sk_gram(sk_context *ctx, sk_dataset *ds, const sk_kernel_params *kp,
+            int normalize, double *out);
+
+/* Arbitrary (x,y) pair list, results to a DEVICE buffer out_dev[k] =
+ * K(ds[x[k]], ds[y[k]]).  No normalisation.  Asynchronous on the context's
+ * stream; host arrays are read before return.  Used by row-block shards
+ * (multi-GPU) and by the benchmark.
+ * Replaces: the inner loop CalcTrainMatrix::operator() kernel_matrix.cpp:42-56
+ * (and the MPI variant's per-rank share, kernel_matrix.cpp:186-261). */
+int sk_pairs_device(sk_context *ctx, sk_dataset *ds, const sk_kernel_params *kp,
+                    const int32_t *x, const int32_t *y, int64_t n_pairs,
+                    double *out_dev);
+/* Same, host output (synchronous). */
+int sk_pairs(sk_context *ctx, sk_dataset *ds, const sk_kernel_params *kp,
+             const int32_t *x, const int32_t *y, int64_t n_pairs, double *out);
+
+/* Test row: out[i] = K(train[i], test[t]) for i in sv_index[0..n_sv) (all i
+ * when sv_index == NULL); out has n_train entries and entries outside
+ * sv_index are left untouched (the reference indexes by train position).
+ * *self = K(test[t], test[t]) when self != NULL.  test and train may be the
+ * same dataset.
+ * Replaces: KernelMatrix::calculate(vec, data, train, sv_index, kernel, n_th,
+ * data_self)  common/kernel_matrix.cpp:112-182, 635-697. */
+int sk_test_row(sk_context *ctx, sk_dataset *test, int t, sk_dataset *train,
+                const int32_t *sv_index, int32_t n_sv,
+                const sk_kernel_params *kp, double *out, double *self);
+
+/* Diagonal: out[i] = K(train[i], train[i]) for i in sv_index (or all i);
+ * out has n_train entries.
+ * Replaces: KernelMatrix::diagonal  common/kernel_matrix.cpp:59-110, 577-633. */
+int sk_diagonal(sk_context *ctx, sk_dataset *ds, const int32_t *sv_index,
+                int32_t n_sv, const sk_kernel_params *kp, double *out);
+
+/* Test x train matrix: out[i*n_train + j] = K(train[j], test[i]).  When
+ * norm_test || normalize, self_out[i] = K(test[i], test[i]) (self_out may be
+ * NULL otherwise); when normalize, out[i][j] /= sqrt(self[i] * diag[j]).
+ * Replaces: KernelMatrix::calculate(test, train, kernel, norm_test,
+ * normalize, n_th)  common/kernel_matrix.cpp:699-754. */
+int sk_test_matrix(sk_context *ctx, sk_dataset *test, sk_dataset *train,
+                   const sk_kernel_params *kp, int norm_test, int normalize,
+                   double *out, double *self_out);
+
+/* ---------------------------------------------------------------- output */
+/* libsvm precomputed-kernel text: "label 0:(i+1) 1:K_i1 ... n:K_in \n" with
+ * ostream default formatting (6 significant digits).  Writes into buf (NUL
+ * terminated) if buf_size is large enough; *needed receives the byte count
+ * including the NUL.  Replaces: KernelMatrix::print common/kernel_matrix.cpp:756-770. */
+int sk_format_libsvm(const double *matrix, int32_t rows, int32_t cols,
+                     const char *const *labels, char *buf, size_t buf_size,
+                     size_t *needed);
+
+/* ---------------------------------------------------------------- inputs */
+/* Synthetic base-pairing probabilities: Boltzmann-weighted Nussinov partition
+ * function (GC 1.5, AU 1.0, GU 0.5 in kT units, hairpin >= 3).  Stand-in for
+ * Vienna pf_fold; out gets n*(n-1)/2 doubles in the packed layout above. */
+int sk_fold_synthetic(const char *seq, int32_t n, int32_t no_gu, double *out);
+/* splitmix64 sequences over ACGU: n_seqs strings of length len written to
+ * out (n_seqs*(len+1) bytes, NUL separated); *state advances. */
+int sk_random_sequences(uint64_t *state, int32_t n_seqs, int32_t len, char *out);
+
+/* ---------------------------------------------------------------- diagnostics */
+/* Milliseconds spent in the last compute call's dominant kernel (DAG stem
+ * DP), measured with HIP events on the context's stream, and its launch
+ * count.  Algorithmic work of that launch: *cells = sum |Vx|*|Vy| over the
+ * pairs (non-leaf nodes). */
+int sk_last_timing(const sk_context *ctx, double *stem_ms, double *string_ms,
+                   double *cells, int32_t *launches);
+/* RIBOSUM85-60 tables as compiled into the library (pinning tests). */
+void sk_ribosum_tables(float *s16, float *p256);
+int sk_char2rna(int c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STEM_KERNEL_H */

@@ -1,0 +1,171 @@
+"""ctypes loader for the CPU ORACLE (oracle/liboracle.so) and the partial
+reference build (oracle/_ref/libskref.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, always as the checker, never as the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libskref.so")
+
+_o = None
+_r = None
+
+_D = C.POINTER(C.c_double)
+_U = C.POINTER(C.c_uint32)
+_F = C.POINTER(C.c_float)
+
+
+def oracle():
+    global _o
+    if _o is None:
+        if not os.path.exists(ORACLE_SO):
+            raise RuntimeError(f"{ORACLE_SO} not built (make -C oracle)")
+        L = C.CDLL(ORACLE_SO)
+        L.orc_mdata_new.restype = C.c_void_p
+        L.orc_mdata_new.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(_D), C.c_float, C.c_int]
+        L.orc_mdata_free.argtypes = [C.c_void_p]
+        for n in ("orc_mdata_n_nodes", "orc_mdata_n_edges", "orc_mdata_n_bpfreq",
+                  "orc_mdata_seq_len", "orc_mdata_n_roots"):
+            getattr(L, n).argtypes = [C.c_void_p]
+            getattr(L, n).restype = C.c_int
+        L.orc_mdata_nodes.argtypes = [C.c_void_p, _U, _U, _U, _U, _F, _U]
+        L.orc_mdata_edges.argtypes = [C.c_void_p, _U, _U]
+        L.orc_mdata_bpfreq.argtypes = [C.c_void_p, _U, _F]
+        L.orc_mdata_roots.argtypes = [C.c_void_p, _U]
+        L.orc_mdata_weight.argtypes = [C.c_void_p, _F]
+        L.orc_mdata_profile.argtypes = [C.c_void_p, _F, _F]
+        L.orc_mdata_bpp.argtypes = [C.c_void_p, _D]
+        for n in ("orc_su_stem",):
+            getattr(L, n).restype = C.c_double
+            getattr(L, n).argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_double, C.c_uint]
+        L.orc_si_stem.restype = C.c_double
+        L.orc_si_stem.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_double, C.c_double, C.c_uint]
+        L.orc_profile_string.restype = C.c_double
+        L.orc_profile_string.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_int, C.c_double,
+                                         C.c_double, C.c_double]
+        L.orc_ribosum_tables.argtypes = [_F, _F]
+        L.orc_char2rna.argtypes = [C.c_int]
+        L.orc_char2rna.restype = C.c_int
+        L.orc_naive_string.restype = C.c_double
+        L.orc_naive_string.argtypes = [C.c_char_p, C.c_char_p, C.c_double]
+        _o = L
+    return _o
+
+
+def reference_partial():
+    """The reference's own rna.cpp/profile.cpp/ribosum.cpp (None if absent)."""
+    global _r
+    if _r is None:
+        if not os.path.exists(REF_SO):
+            return None
+        L = C.CDLL(REF_SO)
+        L.skref_char2rna.argtypes = [C.c_int]
+        L.skref_char2rna.restype = C.c_int
+        L.skref_profile.argtypes = [C.c_int, C.POINTER(C.c_char_p), _F, _F]
+        L.skref_profile.restype = C.c_int
+        L.skref_ribosum.argtypes = [_F, _F]
+        _r = L
+    return _r
+
+
+class OMData:
+    """Oracle MData (one example)."""
+
+    def __init__(self, rows: Sequence[str], bpp_rows: Optional[Sequence[np.ndarray]], th=0.01,
+                 use_bp=True):
+        L = oracle()
+        n = len(rows)
+        self._rows = (C.c_char_p * n)(*[r.encode() for r in rows])
+        self._keep = []
+        barr = (_D * n)()
+        if use_bp:
+            for k, b in enumerate(bpp_rows):
+                b = np.ascontiguousarray(b, dtype=np.float64)
+                if b.size == 0:
+                    b = np.zeros(1)
+                self._keep.append(b)
+                barr[k] = b.ctypes.data_as(_D)
+        self.h = C.c_void_p(L.orc_mdata_new(n, self._rows, barr, C.c_float(th), int(use_bp)))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _o is not None:
+            _o.orc_mdata_free(self.h)
+            self.h = None
+
+    def dag(self) -> dict:
+        L = oracle()
+        nn = L.orc_mdata_n_nodes(self.h)
+        ne = L.orc_mdata_n_edges(self.h)
+        nb = L.orc_mdata_n_bpfreq(self.h)
+        nr = L.orc_mdata_n_roots(self.h)
+        sl = L.orc_mdata_seq_len(self.h)
+        u = lambda k: np.zeros(max(k, 1), np.uint32)
+        f = lambda k: np.zeros(max(k, 1), np.float32)
+        first, last, ned, nbf, mp = u(nn), u(nn), u(nn), u(nn), u(nn)
+        w = f(nn)
+        L.orc_mdata_nodes(self.h, *(a.ctypes.data_as(_U) for a in (first, last, ned, nbf)),
+                          w.ctypes.data_as(_F), mp.ctypes.data_as(_U))
+        to, gaps = u(ne), u(ne)
+        L.orc_mdata_edges(self.h, to.ctypes.data_as(_U), gaps.ctypes.data_as(_U))
+        code, p = u(nb), f(nb)
+        L.orc_mdata_bpfreq(self.h, code.ctypes.data_as(_U), p.ctypes.data_as(_F))
+        roots = u(nr)
+        L.orc_mdata_roots(self.h, roots.ctypes.data_as(_U))
+        pw = f(sl)
+        L.orc_mdata_weight(self.h, pw.ctypes.data_as(_F))
+        return dict(first=first[:nn], last=last[:nn], n_edges=ned[:nn], n_bpfreq=nbf[:nn],
+                    weight=w[:nn], max_pa=mp[:nn], edge_to=to[:ne], edge_gaps=gaps[:ne],
+                    bp_code=code[:nb], bp_p=p[:nb], roots=roots[:nr], pos_weight=pw[:sl])
+
+
+def su_stem(x: OMData, y: OMData, loop_gap=0.2, beta=0.3, band=10) -> float:
+    return oracle().orc_su_stem(x.h, y.h, loop_gap, beta, band)
+
+
+def si_stem(x: OMData, y: OMData, loop_gap=0.2, stack=1.3, covar=0.8, band=10) -> float:
+    return oracle().orc_si_stem(x.h, y.h, loop_gap, stack, covar, band)
+
+
+def su_str(x: OMData, y: OMData, gap=0.8, alpha=0.2) -> float:
+    return oracle().orc_profile_string(x.h, y.h, gap, 1, alpha, 0.0, 0.0)
+
+
+def si_str(x: OMData, y: OMData, gap=0.8, match=1.0, mismatch=0.8) -> float:
+    return oracle().orc_profile_string(x.h, y.h, gap, 0, 0.0, match, mismatch)
+
+
+def kernel_value(kind: int, x: OMData, y: OMData, p) -> float:
+    """Composite kernels of def_kernel.h / conv_kernel.h from the components;
+    p is a KernelParams-like object (attribute access)."""
+    import math
+    stem = lambda: su_stem(x, y, p.loop_gap, p.beta, p.len_band)
+    if kind == 0:
+        return stem()
+    if kind == 1:
+        return si_stem(x, y, p.loop_gap, p.stack, p.covar, p.len_band)
+    if kind == 2:
+        return su_str(x, y, p.gap, p.alpha)
+    if kind == 3:
+        return si_str(x, y, p.gap, p.match, p.mismatch)
+    if kind == 4:
+        return stem() + su_str(x, y, p.gap, p.alpha)
+    if kind == 5:
+        return si_stem(x, y, p.loop_gap, p.stack, p.covar, p.len_band) + si_str(x, y, p.gap, p.match, p.mismatch)
+    if kind == 6:
+        return p.beta * math.log(stem()) + 0.0
+    if kind == 7:
+        return (p.beta * math.log(stem()) + 0.0) + (p.alpha * math.log(su_str(x, y, p.gap, p.alpha)) + 0.0)
+    raise ValueError(kind)
+
+
+def naive_string(x: str, y: str, gap=0.8) -> float:
+    return oracle().orc_naive_string(x.encode(), y.encode(), gap)

@@ -1,0 +1,796 @@
+/*
+ * sk_oracle.c -- CPU ORACLE (test infrastructure only; see sk_oracle.h).
+ *
+ * Plain-C restatement of the reference stem_kernel_lite path:
+ *   ProfileSequence            common/profile.cpp:9-89
+ *   char2rna                   common/rna.cpp:173-231
+ *   BPMatrix averaging         common/bpmatrix.cpp:292-342, 399-417
+ *   Profiler                   stem_kernel_lite/data.cpp:175-274
+ *   DAGBuilder                 stem_kernel_lite/data.cpp:283-449
+ *   find_root/find_max_parent  stem_kernel_lite/data.cpp:538-577
+ *   fill_weight                stem_kernel_lite/data.cpp:579-595
+ *   StemKernel::operator()     stem_kernel_lite/stem_kernel.cpp:49-130
+ *   Simple/SubstNodeScore      stem_kernel_lite/score_table.cpp:193-232, 297-380
+ *   SimpleEdgeScore            stem_kernel_lite/score_table.cpp:235-280
+ *   StringKernel (profile)     stem_kernel_lite/string_kernel.cpp:46-168
+ *   StringKernel (naive)       string_kernel/string_kernel.cpp:11-50
+ * Loop orders and float/double intermediates follow the reference so that the
+ * oracle reproduces its rounding; build with -ffp-contract=off.
+ */
+#include "sk_oracle.h"
+
+#include <assert.h>
+#include <ctype.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../stem_kernel_amd/csrc/ribosum85_60.inc"
+
+#define NONE 0xffffffffu
+enum { N_RNA = 4, RNA_GAP = 4 };
+
+/* ------------------------------------------------------------------ */
+/* alphabet: common/rna.cpp:173-231 (lower-case table search, default GAP) */
+static const char kCharTab[17] = {'a', 'c', 'g', 'u', 't', '-', 'r', 'y', 'm',
+                                  'k', 's', 'w', 'b', 'd', 'h', 'v', 'n'};
+static const unsigned char kRnaTab[17] = {0, 1, 2, 3, 3, 4, 5,  6,  7,
+                                          8, 9, 10, 11, 12, 13, 14, 15};
+
+int orc_char2rna(int c) {
+  char r = (char)tolower(c);
+  for (int i = 0; i != 17; ++i)
+    if (r == kCharTab[i]) return kRnaTab[i];
+  return RNA_GAP;
+}
+
+/* IUPAC weights: common/profile.cpp:9-29 */
+static const float kIupac[16][4] = {
+    {1.0f, 0.0f, 0.0f, 0.0f},          {0.0f, 1.0f, 0.0f, 0.0f},
+    {0.0f, 0.0f, 1.0f, 0.0f},          {0.0f, 0.0f, 0.0f, 1.0f},
+    {0.0f, 0.0f, 0.0f, 0.0f},          {1.0 / 2, 0.0f, 1.0 / 2, 0.0f},
+    {0.0f, 1.0 / 2, 0.0f, 1.0 / 2},    {1.0 / 2, 1.0 / 2, 0.0f, 0.0f},
+    {0.0f, 0.0f, 1.0 / 2, 1.0 / 2},    {0.0f, 1.0 / 2, 1.0 / 2, 0.0f},
+    {1.0 / 2, 0.0f, 0.0f, 1.0 / 2},    {0.0f, 1.0 / 3, 1.0 / 3, 1.0 / 3},
+    {1.0 / 3, 0.0f, 1.0 / 3, 1.0 / 3}, {1.0 / 3, 1.0 / 3, 0.0f, 1.0 / 3},
+    {1.0 / 3, 1.0 / 3, 1.0 / 3, 0.0f}, {1.0 / 4, 1.0 / 4, 1.0 / 4, 1.0 / 4},
+};
+
+void orc_ribosum_tables(float *s16, float *p256) {
+  memcpy(s16, SK_RIBOSUM_S, sizeof(SK_RIBOSUM_S));
+  memcpy(p256, SK_RIBOSUM_P, sizeof(SK_RIBOSUM_P));
+}
+
+/* ProfileSequence::add_sequence(string, w=1) (profile.cpp:647-665) */
+static void profile_add(float *prof5, int len, const char *s, float *n_seqs) {
+  for (int i = 0; i != len; ++i) {
+    int r = orc_char2rna((unsigned char)s[i]);
+    if (r != RNA_GAP) {
+      for (int j = 0; j != N_RNA; ++j) prof5[i * 5 + j] += kIupac[r][j] * 1.0f;
+    } else {
+      prof5[i * 5 + RNA_GAP] += 1.0f;
+    }
+  }
+  *n_seqs += 1.0f;
+}
+
+/* ------------------------------------------------------------------ */
+/* bp matrices: 1-based p(i,j), i<j, packed strict upper triangle */
+typedef struct {
+  const double *p;
+  int n;
+} bpmat;
+
+static size_t tri_index(int n, int i, int j) { /* 0-based i<j */
+  return (size_t)i * n - (size_t)i * (i + 1) / 2 + (size_t)(j - i - 1);
+}
+static double bpm_get(const bpmat *m, int i1, int j1) {
+  assert(i1 < j1 && j1 <= m->n);
+  return m->p[tri_index(m->n, i1 - 1, j1 - 1)];
+}
+
+/* ------------------------------------------------------------------ */
+/* Profiler: stem_kernel_lite/data.cpp:175-274 */
+typedef struct {
+  const char *seq;
+  int len;           /* aligned length (seq_.size()) */
+  const bpmat *bpm;  /* per-row (gap-erased) or averaged matrix */
+  float w;
+  float *pr;  /* single-row profile [len][5] */
+  uint32_t *idx;
+  float *nbp;
+} profiler;
+
+static void profiler_init(profiler *P, const char *seq, int len,
+                          const bpmat *bpm, float w) {
+  P->seq = seq;
+  P->len = len;
+  P->bpm = bpm;
+  P->w = w;
+  P->pr = (float *)calloc((size_t)len * 5, sizeof(float));
+  float ns = 0.0f;
+  profile_add(P->pr, len, seq, &ns);
+  P->idx = (uint32_t *)malloc(sizeof(uint32_t) * len);
+  P->nbp = (float *)malloc(sizeof(float) * len);
+  for (int i = 0; i != len; ++i) {
+    P->idx[i] = NONE;
+    P->nbp[i] = 1.0f;
+  }
+  /* make_idxmap (data.cpp:226-234): GAP is '-' for std::string */
+  uint32_t j = 0;
+  for (int i = 0; i != len; ++i)
+    if (seq[i] != '-') P->idx[i] = j++;
+  /* non_bp_profile (data.cpp:236-265) */
+  if (bpm->n != len) {
+    for (int i = 0; i != len; ++i) {
+      if (P->idx[i] != NONE) {
+        for (int k = 0; k != i; ++k)
+          if (P->idx[k] != NONE)
+            P->nbp[i] -= bpm_get(bpm, P->idx[k] + 1, P->idx[i] + 1);
+        for (int k = i + 1; k != len; ++k)
+          if (P->idx[k] != NONE)
+            P->nbp[i] -= bpm_get(bpm, P->idx[i] + 1, P->idx[k] + 1);
+        if (P->nbp[i] < 0.0) P->nbp[i] = 0.0f;
+      }
+    }
+  } else {
+    for (int i = 0; i != len; ++i) {
+      if (P->idx[i] != NONE) {
+        for (int k = 0; k != i; ++k)
+          if (P->idx[k] != NONE) P->nbp[i] -= bpm_get(bpm, k + 1, i + 1);
+        for (int k = i + 1; k != len; ++k)
+          if (P->idx[k] != NONE) P->nbp[i] -= bpm_get(bpm, i + 1, k + 1);
+        if (P->nbp[i] < 0.0) P->nbp[i] = 0.0f;
+      }
+    }
+  }
+}
+
+static void profiler_free(profiler *P) {
+  free(P->pr);
+  free(P->idx);
+  free(P->nbp);
+}
+
+static float profiler_loop(const profiler *P, int i) {
+  assert(P->idx[i] != NONE);
+  return P->w * P->nbp[i];
+}
+
+/* std::map<bp_t,float> restated as a 16-slot ordered table (keys (a,b) with
+ * a,b<4 iterate in the same lexicographic order as the std::map). */
+typedef struct {
+  int present[16];
+  float val[16];
+} bpmap;
+
+static void profiler_bp(const profiler *P, int i, int j, bpmap *v) {
+  if (P->idx[i] != NONE && P->idx[j] != NONE) {
+    float p = (float)(P->bpm->n != P->len
+                          ? bpm_get(P->bpm, P->idx[i] + 1, P->idx[j] + 1)
+                          : bpm_get(P->bpm, i + 1, j + 1));
+    for (int a = 0; a != N_RNA; ++a) {
+      if (P->pr[i * 5 + a] == 0.0) continue;
+      for (int b = 0; b != N_RNA; ++b) {
+        if (P->pr[j * 5 + b] == 0.0) continue;
+        int k = a * 4 + b;
+        float add = P->w * p * P->pr[i * 5 + a] * P->pr[j * 5 + b];
+        if (!v->present[k]) {
+          v->present[k] = 1;
+          v->val[k] = add;
+        } else {
+          v->val[k] += add;
+        }
+      }
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* DAG storage: stem_kernel_lite/dag.h:17-157 */
+typedef struct {
+  uint32_t to, gaps;
+} oedge;
+typedef struct {
+  uint32_t code;
+  float p;
+} obpf;
+typedef struct {
+  uint32_t first, last;
+  float weight;
+  oedge *edges;
+  int n_edges;
+  obpf *bpf;
+  int n_bpf;
+} onode;
+
+struct orc_mdata {
+  int len;      /* aligned length */
+  int n_rows;
+  onode *tree;
+  int n_nodes, cap_nodes;
+  uint32_t *root;
+  int n_root;
+  uint32_t *max_pa;
+  float *weight; /* per position; NULL if !use_bp */
+  float *prof5;  /* ProfileSequence of all rows [len][5] */
+  float n_seqs;
+  double *bpp;   /* averaged matrix, packed over len (NULL if !use_bp) */
+};
+
+/* growable Pos list (std::list<Pos> in the reference) */
+typedef struct {
+  uint32_t *a, *b;
+  int n, cap;
+} plist;
+
+static void plist_push(plist *l, uint32_t a, uint32_t b) {
+  if (l->n == l->cap) {
+    l->cap = l->cap ? l->cap * 2 : 4;
+    l->a = (uint32_t *)realloc(l->a, sizeof(uint32_t) * l->cap);
+    l->b = (uint32_t *)realloc(l->b, sizeof(uint32_t) * l->cap);
+  }
+  l->a[l->n] = a;
+  l->b[l->n] = b;
+  l->n++;
+}
+static void plist_free(plist *l) {
+  free(l->a);
+  free(l->b);
+  l->a = l->b = NULL;
+  l->n = l->cap = 0;
+}
+
+/* CYKTable cell (i<=j) index for a size-sz table */
+static size_t cyk(int i, int j) { return (size_t)j * (j + 1) / 2 + (size_t)i; }
+
+typedef struct {
+  const profiler *prof;
+  int n_prof;
+  const bpmat *bpm;
+  float th;
+  int sz;
+  plist *bp;    /* CYKTable<list<Pos>> bp_ */
+  plist *head;  /* vector<list<Pos>> head_ */
+  uint32_t *vt; /* CYKTable<uint> vt_ */
+  orc_mdata *d;
+} dagbuilder;
+
+/* DAGBuilder::initialize (data.cpp:307-333) */
+static void dag_initialize(dagbuilder *B) {
+  int sz = B->sz;
+  size_t ncell = (size_t)sz * (sz + 1) / 2;
+  plist *ch = (plist *)calloc(ncell ? ncell : 1, sizeof(plist));
+  for (int j = 1; j < sz; ++j) {
+    for (int i = j - 1;; --i) {
+      if (bpm_get(B->bpm, i + 1, j + 1) >= (double)B->th) {
+        /* std::swap(bp_(i,j), ch(i+1,j-1)); bp_(i,j) is empty here, so this
+         * moves the candidate list.  For j==i+1 the reference's CYKTable read
+         * of (i+1,j-1) aliases a still-empty cell: the list is empty. */
+        if (i + 1 <= j - 1) {
+          plist t = B->bp[cyk(i, j)];
+          B->bp[cyk(i, j)] = ch[cyk(i + 1, j - 1)];
+          ch[cyk(i + 1, j - 1)] = t;
+        }
+        plist_push(&ch[cyk(i, j)], (uint32_t)i, (uint32_t)j);
+        plist_push(&B->head[i], (uint32_t)i, (uint32_t)j);
+      } else {
+        /* remove_copy_if(ch(i+1,j), bind1st(is_child(), head_[i].back()))
+         * then copy head_[i].  head_[i].back() on an empty libstdc++ list
+         * reads the node header's size word: Pos(0,0) (SURVEY App.A #2). */
+        uint32_t hb = B->head[i].n ? B->head[i].b[B->head[i].n - 1] : 0u;
+        plist *src = &ch[cyk(i + 1, j)];
+        plist *dst = &ch[cyk(i, j)];
+        for (int k = 0; k != src->n; ++k)
+          if (!(hb > src->b[k])) plist_push(dst, src->a[k], src->b[k]);
+        for (int k = 0; k != B->head[i].n; ++k)
+          plist_push(dst, B->head[i].a[k], B->head[i].b[k]);
+      }
+      if (i == 0) break;
+    }
+  }
+  for (size_t c = 0; c != ncell; ++c) plist_free(&ch[c]);
+  free(ch);
+  for (size_t c = 0; c != ncell; ++c) B->vt[c] = NONE;
+}
+
+static float dag_loop_profile(const dagbuilder *B, int i) {
+  float v = 0.0f, t = 0.0f;
+  for (int p = 0; p != B->n_prof; ++p) {
+    if (B->prof[p].idx[i] != NONE) v += profiler_loop(&B->prof[p], i);
+    t += B->prof[p].w;
+  }
+  return v / t;
+}
+
+static void dag_bp_profile(const dagbuilder *B, int i, int j, onode *nd) {
+  bpmap v;
+  memset(&v, 0, sizeof(v));
+  float t = 0.0f;
+  for (int p = 0; p != B->n_prof; ++p) {
+    if (B->prof[p].idx[i] != NONE && B->prof[p].idx[j] != NONE)
+      profiler_bp(&B->prof[p], i, j, &v);
+    t += B->prof[p].w;
+  }
+  int n = 0;
+  for (int k = 0; k != 16; ++k) n += v.present[k];
+  nd->bpf = (obpf *)malloc(sizeof(obpf) * (n ? n : 1));
+  nd->n_bpf = 0;
+  for (int k = 0; k != 16; ++k)
+    if (v.present[k]) {
+      nd->bpf[nd->n_bpf].code = (uint32_t)k;
+      nd->bpf[nd->n_bpf].p = v.val[k] / t;
+      nd->n_bpf++;
+    }
+}
+
+static uint32_t tree_push(orc_mdata *d, const onode *n) {
+  if (d->n_nodes == d->cap_nodes) {
+    d->cap_nodes = d->cap_nodes ? d->cap_nodes * 2 : 64;
+    d->tree = (onode *)realloc(d->tree, sizeof(onode) * d->cap_nodes);
+  }
+  d->tree[d->n_nodes] = *n;
+  return (uint32_t)d->n_nodes++;
+}
+
+static uint32_t dag_build_helper(dagbuilder *B, uint32_t a, uint32_t b);
+
+/* make_loop (data.cpp:342-353) */
+static void dag_make_loop(dagbuilder *B, uint32_t a, uint32_t b) {
+  onode nd;
+  memset(&nd, 0, sizeof(nd));
+  nd.first = a;
+  nd.last = b;
+  dag_bp_profile(B, (int)a, (int)b, &nd);
+  nd.weight = dag_loop_profile(B, (int)a) * dag_loop_profile(B, (int)b);
+  uint32_t ret = dag_build_helper(B, a, a);
+  nd.edges = (oedge *)malloc(sizeof(oedge));
+  nd.n_edges = 1;
+  nd.edges[0].to = ret;
+  nd.edges[0].gaps = b - a - 1; /* Edge(to, p_pos): dag.h:183-187 */
+  B->vt[cyk((int)a, (int)b)] = tree_push(B->d, &nd);
+}
+
+/* make_stem (data.cpp:355-371) */
+static void dag_make_stem(dagbuilder *B, uint32_t a, uint32_t b) {
+  const plist cur = B->bp[cyk((int)a, (int)b)];
+  onode nd;
+  memset(&nd, 0, sizeof(nd));
+  nd.first = a;
+  nd.last = b;
+  dag_bp_profile(B, (int)a, (int)b, &nd);
+  nd.weight = dag_loop_profile(B, (int)a) * dag_loop_profile(B, (int)b);
+  nd.edges = (oedge *)malloc(sizeof(oedge) * cur.n);
+  nd.n_edges = cur.n;
+  for (int k = 0; k != cur.n; ++k) {
+    uint32_t ret = dag_build_helper(B, cur.a[k], cur.b[k]);
+    nd.edges[k].to = ret;
+    /* Edge(to, p_pos, c_pos): dag.h:176-181 */
+    nd.edges[k].gaps = (cur.a[k] - a - 1) + (b - cur.b[k] - 1);
+  }
+  B->vt[cyk((int)a, (int)b)] = tree_push(B->d, &nd);
+}
+
+/* build_helper (data.cpp:373-386) */
+static uint32_t dag_build_helper(dagbuilder *B, uint32_t a, uint32_t b) {
+  if (B->vt[cyk((int)a, (int)b)] == NONE) {
+    if (a == b) {
+      onode leaf;
+      memset(&leaf, 0, sizeof(leaf));
+      leaf.first = a;
+      leaf.last = b;
+      leaf.weight = 1.0f;
+      B->vt[cyk((int)a, (int)b)] = tree_push(B->d, &leaf);
+    } else if (B->bp[cyk((int)a, (int)b)].n == 0) {
+      dag_make_loop(B, a, b);
+    } else {
+      dag_make_stem(B, a, b);
+    }
+  }
+  return B->vt[cyk((int)a, (int)b)];
+}
+
+/* ------------------------------------------------------------------ */
+orc_mdata *orc_mdata_new(int n_rows, const char *const *rows,
+                         const double *const *bpp_rows, float th, int use_bp) {
+  orc_mdata *d = (orc_mdata *)calloc(1, sizeof(orc_mdata));
+  int L = (int)strlen(rows[0]);
+  d->len = L;
+  d->n_rows = n_rows;
+  for (int r = 0; r != n_rows; ++r) assert((int)strlen(rows[r]) == L);
+  d->prof5 = (float *)calloc((size_t)L * 5, sizeof(float));
+  d->n_seqs = 0.0f;
+  for (int r = 0; r != n_rows; ++r) profile_add(d->prof5, L, rows[r], &d->n_seqs);
+  if (!use_bp) return d;
+
+  /* BPMatrix(list<string>) FOLD path: per-row fold of erase_gap(lowercase(row))
+   * then average_matrix (bpmatrix.cpp:306-342, 399-417). */
+  size_t npk = L > 1 ? (size_t)L * (L - 1) / 2 : 1;
+  d->bpp = (double *)calloc(npk, sizeof(double));
+  bpmat *rowm = (bpmat *)malloc(sizeof(bpmat) * n_rows);
+  for (int r = 0; r != n_rows; ++r) {
+    int *idxmap = (int *)malloc(sizeof(int) * L);
+    int nr = 0;
+    for (int i = 0; i != L; ++i) idxmap[i] = (rows[r][i] != '-') ? nr++ : -1;
+    rowm[r].p = bpp_rows[r];
+    rowm[r].n = nr;
+    for (int j = 1; j < L; ++j) {
+      if (idxmap[j] < 0) continue;
+      for (int i = j - 1;; --i) {
+        if (idxmap[i] >= 0)
+          d->bpp[tri_index(L, i, j)] += bpm_get(&rowm[r], idxmap[i] + 1, idxmap[j] + 1);
+        if (i == 0) break;
+      }
+    }
+    free(idxmap);
+  }
+  for (size_t k = 0; k != npk; ++k) d->bpp[k] = d->bpp[k] / n_rows;
+  bpmat avg = {d->bpp, L};
+
+  /* MData ctor: per-row matrices when n_matrices()>1, else the averaged one */
+  profiler *prof = (profiler *)malloc(sizeof(profiler) * n_rows);
+  for (int r = 0; r != n_rows; ++r)
+    profiler_init(&prof[r], rows[r], L, n_rows > 1 ? &rowm[r] : &avg, 1.0f);
+
+  dagbuilder B;
+  memset(&B, 0, sizeof(B));
+  B.prof = prof;
+  B.n_prof = n_rows;
+  B.bpm = &avg;
+  B.th = th;
+  B.sz = L;
+  size_t ncell = (size_t)L * (L + 1) / 2;
+  B.bp = (plist *)calloc(ncell ? ncell : 1, sizeof(plist));
+  B.head = (plist *)calloc(L ? L : 1, sizeof(plist));
+  B.vt = (uint32_t *)malloc(sizeof(uint32_t) * (ncell ? ncell : 1));
+  B.d = d;
+  dag_initialize(&B);
+  /* build (data.cpp:293-302): heads of each i in reverse push order */
+  for (int i = 0; i != L; ++i)
+    for (int k = B.head[i].n - 1; k >= 0; --k)
+      dag_build_helper(&B, B.head[i].a[k], B.head[i].b[k]);
+
+  /* find_root (data.cpp:538-560) */
+  char *is_root = (char *)malloc(d->n_nodes ? d->n_nodes : 1);
+  memset(is_root, 1, d->n_nodes);
+  for (int i = 0; i != d->n_nodes; ++i)
+    for (int e = 0; e != d->tree[i].n_edges; ++e) is_root[d->tree[i].edges[e].to] = 0;
+  d->n_root = 0;
+  for (int i = 0; i != d->n_nodes; ++i) d->n_root += is_root[i];
+  d->root = (uint32_t *)malloc(sizeof(uint32_t) * (d->n_root ? d->n_root : 1));
+  int c = 0;
+  for (int i = 0; i != d->n_nodes; ++i)
+    if (is_root[i]) d->root[c++] = (uint32_t)i;
+  free(is_root);
+  /* find_max_parent (data.cpp:562-577) */
+  d->max_pa = (uint32_t *)malloc(sizeof(uint32_t) * (d->n_nodes ? d->n_nodes : 1));
+  for (int i = 0; i != d->n_nodes; ++i) d->max_pa[i] = NONE;
+  for (int i = 0; i != d->n_nodes; ++i)
+    for (int e = 0; e != d->tree[i].n_edges; ++e) {
+      uint32_t t = d->tree[i].edges[e].to;
+      if (d->max_pa[t] == NONE || d->max_pa[t] < (uint32_t)i) d->max_pa[t] = (uint32_t)i;
+    }
+  /* fill_weight (data.cpp:579-595) */
+  d->weight = (float *)malloc(sizeof(float) * (L ? L : 1));
+  for (int i = 0; i != L; ++i) {
+    float v = 0.0f, t = 0.0f;
+    for (int p = 0; p != n_rows; ++p) {
+      if (prof[p].idx[i] != NONE) v += profiler_loop(&prof[p], i);
+      t += prof[p].w;
+    }
+    d->weight[i] = v / t;
+  }
+
+  for (size_t k = 0; k != ncell; ++k) plist_free(&B.bp[k]);
+  for (int i = 0; i != L; ++i) plist_free(&B.head[i]);
+  free(B.bp);
+  free(B.head);
+  free(B.vt);
+  for (int r = 0; r != n_rows; ++r) profiler_free(&prof[r]);
+  free(prof);
+  free(rowm);
+  return d;
+}
+
+void orc_mdata_free(orc_mdata *d) {
+  if (!d) return;
+  for (int i = 0; i != d->n_nodes; ++i) {
+    free(d->tree[i].edges);
+    free(d->tree[i].bpf);
+  }
+  free(d->tree);
+  free(d->root);
+  free(d->max_pa);
+  free(d->weight);
+  free(d->prof5);
+  free(d->bpp);
+  free(d);
+}
+
+int orc_mdata_n_nodes(const orc_mdata *d) { return d->n_nodes; }
+int orc_mdata_seq_len(const orc_mdata *d) { return d->len; }
+int orc_mdata_n_edges(const orc_mdata *d) {
+  int n = 0;
+  for (int i = 0; i != d->n_nodes; ++i) n += d->tree[i].n_edges;
+  return n;
+}
+int orc_mdata_n_bpfreq(const orc_mdata *d) {
+  int n = 0;
+  for (int i = 0; i != d->n_nodes; ++i) n += d->tree[i].n_bpf;
+  return n;
+}
+void orc_mdata_nodes(const orc_mdata *d, uint32_t *first, uint32_t *last,
+                     uint32_t *n_edges, uint32_t *n_bpfreq, float *weight,
+                     uint32_t *max_pa) {
+  for (int i = 0; i != d->n_nodes; ++i) {
+    first[i] = d->tree[i].first;
+    last[i] = d->tree[i].last;
+    n_edges[i] = (uint32_t)d->tree[i].n_edges;
+    n_bpfreq[i] = (uint32_t)d->tree[i].n_bpf;
+    weight[i] = d->tree[i].weight;
+    max_pa[i] = d->max_pa[i];
+  }
+}
+void orc_mdata_edges(const orc_mdata *d, uint32_t *to, uint32_t *gaps) {
+  int k = 0;
+  for (int i = 0; i != d->n_nodes; ++i)
+    for (int e = 0; e != d->tree[i].n_edges; ++e, ++k) {
+      to[k] = d->tree[i].edges[e].to;
+      gaps[k] = d->tree[i].edges[e].gaps;
+    }
+}
+void orc_mdata_bpfreq(const orc_mdata *d, uint32_t *code, float *p) {
+  int k = 0;
+  for (int i = 0; i != d->n_nodes; ++i)
+    for (int e = 0; e != d->tree[i].n_bpf; ++e, ++k) {
+      code[k] = d->tree[i].bpf[e].code;
+      p[k] = d->tree[i].bpf[e].p;
+    }
+}
+int orc_mdata_n_roots(const orc_mdata *d) { return d->n_root; }
+void orc_mdata_roots(const orc_mdata *d, uint32_t *roots) {
+  memcpy(roots, d->root, sizeof(uint32_t) * d->n_root);
+}
+void orc_mdata_weight(const orc_mdata *d, float *w) {
+  if (d->weight) memcpy(w, d->weight, sizeof(float) * d->len);
+}
+void orc_mdata_profile(const orc_mdata *d, float *prof5, float *n_seqs) {
+  memcpy(prof5, d->prof5, sizeof(float) * 5 * d->len);
+  *n_seqs = d->n_seqs;
+}
+void orc_mdata_bpp(const orc_mdata *d, double *packed) {
+  if (d->bpp && d->len > 1)
+    memcpy(packed, d->bpp, sizeof(double) * (size_t)d->len * (d->len - 1) / 2);
+}
+
+/* ------------------------------------------------------------------ */
+/* StemKernel<ST,MData>::operator() (stem_kernel_lite/stem_kernel.cpp:49-130)
+ * with SubstScoreTable (subst=1) or SimpleScoreTable (subst=0). */
+typedef struct {
+  int subst;
+  double gap; /* loop_gap: SimpleEdgeScore gap_ and node gap_ */
+  double co_subst[256];
+  double match, mismatch;
+  unsigned band;
+} stem_params;
+
+static double *gap_powers(double gap, int n) {
+  /* SimpleEdgeScore::initialize (score_table.cpp:239-256): g[k]=g[k-1]*gap */
+  double *g = (double *)malloc(sizeof(double) * (n > 1 ? n : 1));
+  g[0] = 1.0;
+  for (int k = 1; k < n; ++k) g[k] = g[k - 1] * gap;
+  return g;
+}
+
+static double node_gap_score(const stem_params *S, const orc_mdata *d, int i) {
+  return S->gap * S->gap * d->tree[i].weight; /* score_table.h:26-29, 51-54 */
+}
+
+static double node_match_score(const stem_params *S, const orc_mdata *x,
+                               const orc_mdata *y, int i, int j) {
+  const onode *ni = &x->tree[i], *nj = &y->tree[j];
+  double v_c = 0.0;
+  for (int a = 0; a != ni->n_bpf; ++a) {
+    double cx = ni->bpf[a].p;
+    for (int b = 0; b != nj->n_bpf; ++b) {
+      double cy = nj->bpf[b].p;
+      double v;
+      if (S->subst) {
+        v = S->co_subst[ni->bpf[a].code * 16 + nj->bpf[b].code];
+      } else {
+        v = (ni->bpf[a].code != nj->bpf[b].code) ? S->mismatch : S->match;
+      }
+      v_c += v * cx * cy;
+    }
+  }
+  double nbp_x = x->prof5[ni->first * 5 + RNA_GAP];
+  v_c += node_gap_score(S, y, j) * nbp_x / (double)x->n_seqs;
+  double nbp_y = y->prof5[nj->first * 5 + RNA_GAP];
+  v_c += node_gap_score(S, x, i) * nbp_y / (double)y->n_seqs;
+  return v_c;
+}
+
+static double stem_dp(const stem_params *S, const orc_mdata *x, const orc_mdata *y) {
+  int nx = x->n_nodes, ny = y->n_nodes;
+  int glen = 2 * (x->len > y->len ? x->len : y->len);
+  double *g = gap_powers(S->gap, glen + 2);
+  size_t cells = (size_t)(nx ? nx : 1) * (ny ? ny : 1);
+  double *K0 = (double *)malloc(sizeof(double) * cells);
+  double *G0 = (double *)malloc(sizeof(double) * cells);
+  double *K1 = (double *)calloc(ny ? ny : 1, sizeof(double));
+  double *G1 = (double *)calloc(ny ? ny : 1, sizeof(double));
+#define AT(M, a, b) M[(size_t)(a) * ny + (b)]
+  for (int i = 0; i != nx; ++i) {
+    const onode *xi = &x->tree[i];
+    for (int j = 0; j != ny; ++j) {
+      const onode *yj = &y->tree[j];
+      if (xi->n_edges == 0 && yj->n_edges == 0) {
+        AT(K0, i, j) = AT(G0, i, j) = 1.0;
+        continue;
+      }
+      K1[j] = G1[j] = 0.0;
+      if (xi->n_edges && yj->n_edges &&
+          (S->band == 0 ||
+           (unsigned)abs((int)((xi->last - xi->first) - (yj->last - yj->first))) <= S->band)) {
+        double v_s = node_match_score(S, x, y, i, j);
+        for (int ex = 0; ex != xi->n_edges; ++ex) {
+          for (int ey = 0; ey != yj->n_edges; ++ey) {
+            double e_s = g[xi->edges[ex].gaps] * g[yj->edges[ey].gaps] * 1.0f * 1.0f;
+            double v = AT(G0, xi->edges[ex].to, yj->edges[ey].to) * v_s * e_s;
+            K1[j] += v;
+            G1[j] += v;
+          }
+        }
+      }
+      for (int ey = 0; ey != yj->n_edges; ++ey) {
+        double v_s = node_gap_score(S, y, j);
+        double e_s = g[yj->edges[ey].gaps] * 1.0f;
+        K1[j] += K1[yj->edges[ey].to];
+        G1[j] += G1[yj->edges[ey].to] * v_s * e_s;
+      }
+      AT(K0, i, j) = K1[j];
+      AT(G0, i, j) = G1[j];
+      for (int ex = 0; ex != xi->n_edges; ++ex) {
+        double v_s = node_gap_score(S, x, i);
+        double e_s = g[xi->edges[ex].gaps] * 1.0f;
+        AT(K0, i, j) += AT(K0, xi->edges[ex].to, j);
+        AT(G0, i, j) += AT(G0, xi->edges[ex].to, j) * v_s * e_s;
+      }
+    }
+  }
+  double ret = 0.0;
+  for (int a = 0; a != x->n_root; ++a)
+    for (int b = 0; b != y->n_root; ++b) ret += AT(K0, x->root[a], y->root[b]);
+#undef AT
+  free(K0);
+  free(G0);
+  free(K1);
+  free(G1);
+  free(g);
+  return ret;
+}
+
+double orc_su_stem(const orc_mdata *x, const orc_mdata *y, double loop_gap,
+                   double beta, unsigned band) {
+  stem_params S;
+  memset(&S, 0, sizeof(S));
+  S.subst = 1;
+  S.gap = loop_gap;
+  S.band = band;
+  /* SubstNodeScore ctor (score_table.cpp:297-313) */
+  for (int k = 0; k != 256; ++k) S.co_subst[k] = exp(SK_RIBOSUM_P[k] * beta);
+  return stem_dp(&S, x, y);
+}
+
+double orc_si_stem(const orc_mdata *x, const orc_mdata *y, double loop_gap,
+                   double stack, double covar, unsigned band) {
+  stem_params S;
+  memset(&S, 0, sizeof(S));
+  S.subst = 0;
+  S.gap = loop_gap;
+  S.match = stack;
+  S.mismatch = covar;
+  S.band = band;
+  return stem_dp(&S, x, y);
+}
+
+/* ------------------------------------------------------------------ */
+/* StringKernel<double,MData> (stem_kernel_lite/string_kernel.cpp) */
+static double prof_subst(const double *st, const float *x, const float *y) {
+  double v_c = 0.0;
+  float n = 0;
+  for (int i = 0; i != N_RNA; ++i) {
+    if (x[i] == 0) continue;
+    for (int j = 0; j != N_RNA; ++j) {
+      if (y[j] == 0) continue;
+      n += x[i] * y[j];
+      v_c += st[i * 4 + j] * x[i] * y[j];
+    }
+  }
+  return n == 0 ? 1.0 : v_c / n;
+}
+
+double orc_profile_string(const orc_mdata *xx, const orc_mdata *yy, double gap,
+                          int ribosum, double alpha, double match,
+                          double mismatch) {
+  double st[16];
+  for (int i = 0; i != 4; ++i)
+    for (int k = 0; k != 4; ++k)
+      st[i * 4 + k] = ribosum ? exp(SK_RIBOSUM_S[i * 4 + k] * alpha)
+                              : (i == k ? match : mismatch);
+  int sx = xx->len, sy = yy->len;
+  int use_weight = xx->weight != NULL && yy->weight != NULL && sx > 0 && sy > 0;
+  double *K0p = (double *)malloc(sizeof(double) * (sy + 1));
+  double *G0p = (double *)malloc(sizeof(double) * (sy + 1));
+  double *K0c = (double *)malloc(sizeof(double) * (sy + 1));
+  double *G0c = (double *)malloc(sizeof(double) * (sy + 1));
+  double *K1 = (double *)calloc(sy + 1, sizeof(double));
+  double *G1 = (double *)calloc(sy + 1, sizeof(double));
+  K0p[0] = G0p[0] = 1.0;
+  for (int j = 1; j != sy + 1; ++j) {
+    K0p[j] = 1.0;
+    G0p[j] = G0p[j - 1] * gap;
+  }
+  for (int i = 1; i != sx + 1; ++i) {
+    K0c[0] = 1.0;
+    G0c[0] = G0p[0] * gap;
+    K1[0] = G1[0] = 0.0;
+    for (int j = 1; j != sy + 1; ++j) {
+      double v;
+      if (use_weight) {
+        v = G0p[j - 1] * xx->weight[i - 1] * yy->weight[j - 1];
+      } else {
+        v = G0p[j - 1];
+      }
+      v *= prof_subst(st, &xx->prof5[(i - 1) * 5], &yy->prof5[(j - 1) * 5]);
+      K1[j] = v + K1[j - 1];
+      G1[j] = v + G1[j - 1] * gap;
+      K0c[j] = K1[j] + K0p[j];
+      G0c[j] = G1[j] + G0p[j] * gap;
+    }
+    double *t;
+    t = K0p; K0p = K0c; K0c = t;
+    t = G0p; G0p = G0c; G0c = t;
+  }
+  double ret = K0p[sy];
+  free(K0p); free(G0p); free(K0c); free(G0c); free(K1); free(G1);
+  return ret;
+}
+
+/* ------------------------------------------------------------------ */
+/* StringKernel<double>::operator() (string_kernel/string_kernel.cpp:11-50) */
+double orc_naive_string(const char *x, const char *y, double gap) {
+  int nx = (int)strlen(x), ny = (int)strlen(y);
+  double g = gap, g2 = g * g;
+  double *K0 = (double *)malloc(sizeof(double) * (size_t)(nx + 1) * (ny + 1));
+  double *G0 = (double *)malloc(sizeof(double) * (size_t)(nx + 1) * (ny + 1));
+  double *K1 = (double *)calloc(ny + 1, sizeof(double));
+  double *G1 = (double *)calloc(ny + 1, sizeof(double));
+#define A(M, i, j) M[(size_t)(i) * (ny + 1) + (j)]
+  A(K0, 0, 0) = A(G0, 0, 0) = 1.0;
+  for (int i = 1; i != nx + 1; ++i) {
+    A(K0, i, 0) = 1.0;
+    A(G0, i, 0) = A(G0, i - 1, 0) * g;
+  }
+  for (int j = 1; j != ny + 1; ++j) {
+    A(K0, 0, j) = 1.0;
+    A(G0, 0, j) = A(G0, 0, j - 1) * g;
+  }
+  for (int i = 1; i != nx + 1; ++i) {
+    K1[0] = G1[0] = 0.0;
+    for (int j = 1; j != ny + 1; ++j) {
+      K1[j] = K1[j - 1];
+      G1[j] = G1[j - 1] * g;
+      if (x[i - 1] == y[j - 1]) {
+        K1[j] += A(G0, i - 1, j - 1) * g2;
+        G1[j] += A(G0, i - 1, j - 1) * g2;
+      }
+      A(K0, i, j) = A(K0, i - 1, j) + K1[j];
+      A(G0, i, j) = A(G0, i - 1, j) * g + G1[j];
+    }
+  }
+  double r = A(K0, nx, ny);
+#undef A
+  free(K0); free(G0); free(K1); free(G1);
+  return r;
+}

@@ -1,0 +1,93 @@
+/*
+ * sk_oracle.h -- CPU ORACLE for the stem-kernel hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This is a plain-C restatement of the reference algorithms
+ * (keio-bioinformatics/stem_kernel rev 296), written from the reference
+ * sources read as text.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it, and only as the checker; the product library
+ * (stem_kernel_amd) never links or calls it.
+ *
+ * Pinning status:
+ *   - alphabet (char2rna), IUPAC profile columns and the RIBOSUM85-60 tables
+ *     are PINNED against the reference's own translation units
+ *     (common/rna.cpp, common/profile.cpp, stem_kernel_lite/ribosum.cpp),
+ *     compiled unmodified from /root/reference into oracle/_ref/ by
+ *     oracle/Makefile and compared in tests/test_oracle_pinning.py;
+ *   - the DAG builder and every kernel DP are "parity unpinned": the
+ *     reference TUs that hold them need Boost, ViennaRNA and the
+ *     configure-generated config.h, none of which exist in this image, and
+ *     the reference ships no tests, fixtures or golden values.
+ */
+#ifndef SK_ORACLE_H
+#define SK_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_mdata orc_mdata;
+
+/* MData ctor (stem_kernel_lite/data.cpp:466-487) for one example of n_rows
+ * aligned rows (equal length).  bpp_rows[r] is the base-pairing-probability
+ * matrix of row r AFTER erase_gap (length n_r = #non-gap chars), packed as the
+ * strict upper triangle, row-major: p(i,j), 0<=i<j<n_r at
+ * index i*n_r - i*(i+1)/2 + (j-i-1).  (Stands for Vienna pf_fold output,
+ * common/bpmatrix.cpp:166-173.)  th = --basepair threshold.
+ * use_bp=0 gives MData(ma) (no DAG, empty weight; data.cpp:489-494). */
+orc_mdata *orc_mdata_new(int n_rows, const char *const *rows,
+                         const double *const *bpp_rows, float th, int use_bp);
+void orc_mdata_free(orc_mdata *d);
+
+/* DAG introspection (dag.h, data.h:33-37) for packer parity tests. */
+int orc_mdata_n_nodes(const orc_mdata *d);
+int orc_mdata_n_edges(const orc_mdata *d);
+int orc_mdata_n_bpfreq(const orc_mdata *d);
+int orc_mdata_seq_len(const orc_mdata *d);
+/* node arrays (length n_nodes): first,last,n_edges,n_bpfreq,weight,max_pa */
+void orc_mdata_nodes(const orc_mdata *d, uint32_t *first, uint32_t *last,
+                     uint32_t *n_edges, uint32_t *n_bpfreq, float *weight,
+                     uint32_t *max_pa);
+/* edge arrays (length n_edges, node-major, list order): to, gaps */
+void orc_mdata_edges(const orc_mdata *d, uint32_t *to, uint32_t *gaps);
+/* bp_freq arrays (length n_bpfreq): code=a*4+b, p */
+void orc_mdata_bpfreq(const orc_mdata *d, uint32_t *code, float *p);
+int orc_mdata_n_roots(const orc_mdata *d);
+void orc_mdata_roots(const orc_mdata *d, uint32_t *roots);
+/* per-position weight (fill_weight, data.cpp:579-595) and profile columns
+ * (ProfileSequence, common/profile.cpp) float[L][5], n_seqs */
+void orc_mdata_weight(const orc_mdata *d, float *w);
+void orc_mdata_profile(const orc_mdata *d, float *prof5, float *n_seqs);
+
+/* Averaged bp matrix (common/bpmatrix.cpp:306-342), packed as above over the
+ * aligned length. */
+void orc_mdata_bpp(const orc_mdata *d, double *packed);
+
+/* ---- kernels: each returns K(x,y) with x = row example, y = column ---- */
+/* StemKernel<SubstScoreTable> (stem_kernel_lite/stem_kernel.cpp:49-130,
+ * score_table.cpp:297-380) == SuStemKernel(loop_gap, beta, band) */
+double orc_su_stem(const orc_mdata *x, const orc_mdata *y, double loop_gap,
+                   double beta, unsigned band);
+/* StemKernel<SimpleScoreTable> == SiStemKernel(loop_gap, stack, covar, band)
+ * (def_kernel.h:238-260, score_table.cpp:193-232) */
+double orc_si_stem(const orc_mdata *x, const orc_mdata *y, double loop_gap,
+                   double stack, double covar, unsigned band);
+/* StringKernel<double,MData> (stem_kernel_lite/string_kernel.cpp:46-168):
+ * ribosum=1 -> ctor(gap, alpha); ribosum=0 -> ctor(gap, match, mismatch) */
+double orc_profile_string(const orc_mdata *x, const orc_mdata *y, double gap,
+                          int ribosum, double alpha, double match,
+                          double mismatch);
+
+/* RIBOSUM tables as restated (stem_kernel_lite/ribosum.cpp:6-120) */
+void orc_ribosum_tables(float *s16, float *p256);
+/* char2rna restated (common/rna.cpp:201-231) */
+int orc_char2rna(int c);
+
+/* Naive gapped string kernel (string_kernel/string_kernel.cpp:14-85) */
+double orc_naive_string(const char *x, const char *y, double gap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,12 @@
+"""MI355X-native stem-kernel Gram engine (gfx950 HIP kernels behind a C ABI).
+
+See include/stem_kernel.h for the ABI and DESIGN.md for the design.
+"""
+from ._lib import StemKernelError, lib, default_params  # noqa: F401
+from .kernel_matrix import (  # noqa: F401
+    Context, Dataset, KernelMatrix, LSuStemKernel, LSuStemStrKernel, SiStemKernel,
+    SiStemStrKernel, StemStrKernel, StringKernel, SuStemKernel, SuStemStrKernel, fold,
+    format_libsvm, random_sequences,
+)
+
+__version__ = "0.1.0"

@@ -1,0 +1,93 @@
+// Synthetic inputs for the stem-kernel engine.
+//
+// * Sequences: a splitmix64 stream -- base = "ACGU"[x >> 62].
+// * Base-pairing probabilities: a Boltzmann-weighted Nussinov partition
+//   function (GC/CG e^1.5, AU/UA e^1.0, GU/UG e^0.5, hairpin >= 3 unpaired),
+//   inside + outside in O(L^3).  This stands in for ViennaRNA's pf_fold
+//   (common/bpmatrix.cpp:151-177, common/pf_wrapper.cpp:15-36), which is not
+//   available in this image; it is NOT Vienna's energy model.  Its output is
+//   the same packed strict-upper-triangle layout the engine consumes, so any
+//   real folding engine's matrix can be passed in its place.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "sk_internal.h"
+
+namespace sk {
+
+uint64_t splitmix64_next(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static double pair_weight(char a, char b, bool no_gu) {
+  auto lc = [](char c) { return (c >= 'A' && c <= 'Z') ? char(c - 'A' + 'a') : c; };
+  a = lc(a);
+  b = lc(b);
+  if (a == 't') a = 'u';
+  if (b == 't') b = 'u';
+  if ((a == 'g' && b == 'c') || (a == 'c' && b == 'g')) return std::exp(1.5);
+  if ((a == 'a' && b == 'u') || (a == 'u' && b == 'a')) return std::exp(1.0);
+  if (!no_gu && ((a == 'g' && b == 'u') || (a == 'u' && b == 'g'))) return std::exp(0.5);
+  return 0.0;
+}
+
+// Inside/outside over the grammar  S(i,j) -> S(i,j-1) | S(i,k-1) (k S(k+1,j-1) j)
+// with spans scaled by s^-(len) to stay in range.  Output: p(i,j), i<j, 0-based,
+// packed strict upper triangle.
+void fold_nussinov(const char* seq, int n, bool no_gu, double* out) {
+  if (n < 2) return;
+  const double s = 2.0, inv_s = 1.0 / s, inv_s2 = inv_s * inv_s;
+  const int hp = 3;
+  // Q(i,j) for 0<=i<=j<n; empty spans (j=i-1) are 1.
+  auto at = [n](int i, int j) { return (size_t)i * n + j; };
+  std::vector<double> Q((size_t)n * n, 0.0), O((size_t)n * n, 0.0), B((size_t)n * n, 0.0);
+  auto q = [&](int i, int j) -> double { return j < i ? 1.0 : Q[at(i, j)]; };
+  for (int i = 0; i < n; ++i)
+    for (int j = i + hp + 1; j < n; ++j) B[at(i, j)] = pair_weight(seq[i], seq[j], no_gu) * inv_s2;
+  for (int d = 0; d < n; ++d) {
+    for (int i = 0; i + d < n; ++i) {
+      int j = i + d;
+      double v = q(i, j - 1) * inv_s;
+      for (int k = i; k <= j - hp - 1; ++k) {
+        double b = B[at(k, j)];
+        if (b != 0.0) v += q(i, k - 1) * b * q(k + 1, j - 1);
+      }
+      Q[at(i, j)] = v;
+    }
+  }
+  const double Z = Q[at(0, n - 1)];
+  O[at(0, n - 1)] = 1.0;
+  std::vector<double> P((size_t)n * n, 0.0);
+  for (int d = n - 1; d >= 0; --d) {
+    for (int i = 0; i + d < n; ++i) {
+      int j = i + d;
+      double o = O[at(i, j)];
+      if (o == 0.0) continue;
+      if (j - 1 >= i) O[at(i, j - 1)] += o * inv_s;
+      for (int k = i; k <= j - hp - 1; ++k) {
+        double b = B[at(k, j)];
+        if (b == 0.0) continue;
+        double left = q(i, k - 1), inner = q(k + 1, j - 1);
+        if (k - 1 >= i) O[at(i, k - 1)] += o * b * inner;
+        O[at(k + 1, j - 1)] += o * b * left;
+        P[at(k, j)] += o * left * b * inner;
+      }
+    }
+  }
+  size_t t = 0;
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) out[t++] = P[at(i, j)] / Z;
+}
+
+void random_sequence(uint64_t& state, int len, char* out) {
+  static const char kBases[4] = {'A', 'C', 'G', 'U'};
+  for (int i = 0; i < len; ++i) out[i] = kBases[splitmix64_next(state) >> 62];
+  out[len] = 0;
+}
+
+}  // namespace sk

@@ -1,0 +1,56 @@
+// Device-resident packed example set (shared by the HIP kernels and the host
+// packer).  One flat SoA buffer per field, examples concatenated.
+//
+// DAG part: only NON-LEAF nodes are stored (leaves are implicit: G0 at a
+// leaf row/column is a closed form, see dag_stem.hip), renumbered in LEVEL
+// order: level 0 = loop nodes (single leaf child), level k>0 = stems whose
+// deepest non-leaf child is at level k-1.  Level order is a topological order
+// (children first) and makes every level a contiguous node range.
+#pragma once
+#include <cstdint>
+
+namespace sk {
+
+constexpr uint32_t kLeafChild = 0xffffu;
+
+struct DevSet {
+  int32_t n_examples = 0;
+  // per example (n_examples entries; *_base are absolute indices)
+  const int32_t* ex_nl = nullptr;         // non-leaf node count
+  const int32_t* ex_node_base = nullptr;  // into nd_* arrays
+  const int32_t* ex_edge_base = nullptr;  // into ed_* arrays
+  const int32_t* ex_bpf_base = nullptr;   // into bpf_* arrays
+  const int32_t* ex_lvl_base = nullptr;   // into lvl (n_levels+1 offsets, local)
+  const int32_t* ex_nlev = nullptr;       // number of levels
+  const float* ex_nseqs = nullptr;        // ProfileSequence::n_seqs
+  const int32_t* ex_len = nullptr;        // aligned length
+  const int32_t* ex_pos_base = nullptr;   // into pos_* arrays
+  // per non-leaf node
+  const uint32_t* nd_a = nullptr;  // edge_beg_local:16 | n_edges:8 | n_bpf:8
+  const uint32_t* nd_b = nullptr;  // len(last-first):16 | bpf_beg_local:16
+  const float* nd_w = nullptr;     // node weight (loop_profile(i)*loop_profile(j))
+  const float* nd_nbp = nullptr;   // profile gap count at node.first
+  const double* nd_P = nullptr;    // sum over roots of #paths root->node
+  // per edge of a non-leaf node (reference list order)
+  const uint32_t* ed = nullptr;  // child_local:16 (kLeafChild = leaf) | gaps:16
+  // per bp-frequency entry
+  const uint32_t* bpf_code = nullptr;  // a*4+b
+  const float* bpf_p = nullptr;
+  // level offsets (local node index)
+  const int32_t* lvl = nullptr;
+  // per aligned position (string kernel)
+  const float4* pos_prof = nullptr;  // ProfileSequence columns A,C,G,U
+  const float* pos_w = nullptr;      // fill_weight (empty -> string kernel unweighted)
+  const int32_t* ex_has_w = nullptr;
+  // maxima over the set
+  int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0;
+  int64_t total_nodes = 0;
+};
+
+// Per-call, parameter-dependent node values (computed on device by sk_prep).
+struct DevParamNodes {
+  double* nd_L = nullptr;   // G0 at (node, any y-leaf column)
+  double* nd_SL = nullptr;  // sum_e g^gaps(e) * L[child(e)]
+};
+
+}  // namespace sk

@@ -1,0 +1,68 @@
+// Launch descriptors shared by the host runtime (sk_api.cpp) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "device_set.h"
+
+namespace sk {
+
+struct StemLaunch {
+  DevSet xset;        // row examples (x role)
+  DevSet yset;        // column examples (y role); may equal xset
+  DevParamNodes pn;   // parameter-dependent node values of xset
+  const double* co_subst = nullptr;  // 256: node-score table (pair x pair)
+  const double* gpow = nullptr;      // loop_gap^k, k < n_gpow
+  int32_t n_gpow = 0, n_gpow_pad = 0;
+  double gap2 = 0.0;                 // loop_gap^2
+  uint32_t band = 0;                 // --length-band (0 = off)
+  // LDS sizing (maxima over the y examples of this launch)
+  int32_t lds_max_nl = 0, lds_max_edges = 0, lds_max_bpf = 0, lds_max_nlev_pad = 0;
+  // work: items {y, base, count, 0}; pair t of an item is x = xs[base+t],
+  // result -> out[oidx[base+t]]
+  const int4* items = nullptr;
+  int32_t n_items = 0;
+  const int32_t* xs = nullptr;
+  const int64_t* oidx = nullptr;
+  double* out = nullptr;
+  int* item_counter = nullptr;
+  double* scratch = nullptr;   // per-wave G0 slabs
+  int64_t slab_doubles = 0;
+};
+
+struct StrLaunch {
+  DevSet xset, yset;
+  const double* st = nullptr;    // 16: exp(alpha*ribosum_s) or match/mismatch
+  const double* gpow = nullptr;  // gap^k, k <= max_len
+  double gap = 0.0;
+  const int32_t* xs = nullptr;
+  const int32_t* ys = nullptr;
+  int64_t n_pairs = 0;
+  double* out = nullptr;
+  unsigned long long* pair_counter = nullptr;
+  int32_t lds_max_len = 0;
+};
+
+enum CombineMode : int32_t {
+  kCombineStem = 0,      // K = stem
+  kCombineStr = 1,       // K = str
+  kCombineAdd = 2,       // K = stem + str                 (AddKernel)
+  kCombineLogStem = 3,   // K = beta*log(stem) + 0         (LTKernel(LogKernel))
+  kCombineLogAdd = 4     // K = (beta*log stem + 0) + (alpha*log str + 0)
+};
+
+hipError_t launch_prep(const DevSet& s, const DevParamNodes& pn, const double* gpow, double gap2,
+                       hipStream_t st);
+size_t stem_lds_bytes(const StemLaunch& P, int nwaves);
+hipError_t launch_stem(const StemLaunch& P, int grid, int nwaves, hipStream_t st);
+hipError_t stem_kernel_attr(int* max_dyn_lds);
+
+size_t str_lds_bytes(const StrLaunch& P, int nwaves);
+hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st);
+
+hipError_t launch_combine(const double* stem, const double* str, double* out, int64_t n,
+                          int32_t mode, double alpha, double beta, hipStream_t st);
+
+}  // namespace sk

@@ -1,0 +1,897 @@
+// C ABI of the stem-kernel engine (include/stem_kernel.h): host runtime.
+//
+// Owns: example sets (host build + device packing), per-GPU contexts
+// (stream, scratch, work lists) and the orchestration of the HIP kernels
+// that replace KernelMatrix::calculate's per-pair loop
+// (common/kernel_matrix.cpp:42-56, 485-575).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <numeric>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/stem_kernel.h"
+#include "host/sk_internal.h"
+#include "kernels/device_set.h"
+#include "kernels/launch.h"
+#include "ribosum85_60.inc"
+
+using sk::DevSet;
+using sk::Example;
+
+namespace {
+
+struct DeviceBuffers {
+  std::vector<void*> ptrs;
+  ~DeviceBuffers() { release(); }
+  void release() {
+    for (void* p : ptrs) (void)hipFree(p);
+    ptrs.clear();
+  }
+};
+
+template <class T>
+hipError_t upload(DeviceBuffers& db, const std::vector<T>& v, const T** out) {
+  void* p = nullptr;
+  const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) return e;
+  db.ptrs.push_back(p);
+  if (!v.empty()) e = hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  *out = static_cast<const T*>(p);
+  return e;
+}
+
+// Packed host image of a dataset (device_set.h layout).
+struct HostPack {
+  std::vector<int32_t> ex_nl, ex_node_base, ex_edge_base, ex_bpf_base, ex_lvl_base, ex_nlev,
+      ex_len, ex_pos_base, ex_has_w;
+  std::vector<float> ex_nseqs;
+  std::vector<uint32_t> nd_a, nd_b;
+  std::vector<float> nd_w, nd_nbp;
+  std::vector<double> nd_P;
+  std::vector<uint32_t> ed, bpf_code;
+  std::vector<float> bpf_p;
+  std::vector<int32_t> lvl;
+  std::vector<float4> pos_prof;
+  std::vector<float> pos_w;
+  int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0;
+};
+
+}  // namespace
+
+struct sk_dataset {
+  std::vector<Example> ex;
+  std::vector<std::string> labels;
+  // device image (per device ordinal; one context uploads)
+  int device = -1;
+  bool uploaded = false;
+  DevSet dev;
+  DeviceBuffers buf;
+  HostPack pack;
+  std::string err;
+};
+
+struct sk_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int n_cu = 0;
+  std::string err;
+  // reusable device buffers
+  double* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* work = nullptr;
+  size_t work_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+  double last_stem_ms = 0.0, last_str_ms = 0.0, last_cells = 0.0;
+  int32_t last_launches = 0;
+};
+
+namespace {
+
+int fail(sk_context* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+#define SK_HIP(ctx, expr)                                                              \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return fail((ctx), SK_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// --------------------------------------------------------------- packing
+int pack_dataset(sk_dataset* ds, std::string& err) {
+  HostPack& P = ds->pack;
+  P = HostPack();
+  const int n = (int)ds->ex.size();
+  P.ex_node_base.push_back(0);
+  P.ex_edge_base.push_back(0);
+  P.ex_bpf_base.push_back(0);
+  P.ex_lvl_base.push_back(0);
+  P.ex_pos_base.push_back(0);
+  for (int e = 0; e < n; ++e) {
+    const Example& X = ds->ex[e];
+    const int nn = X.n_nodes();
+    // level of every node (children first in reference numbering)
+    std::vector<int> level(nn, -1);
+    int nlev = 0;
+    for (int v = 0; v < nn; ++v) {
+      const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
+      if (e0 == e1) continue;  // leaf
+      int lv = 0;
+      bool any_leaf = false;
+      for (uint32_t k = e0; k < e1; ++k) {
+        const int c = level[X.edge_to[k]];
+        if (c < 0) any_leaf = true;
+        else lv = std::max(lv, c + 1);
+      }
+      if (any_leaf && e1 - e0 != 1) {
+        err = "unexpected DAG shape: stem with a leaf child";
+        return SK_ERR_INVALID;
+      }
+      level[v] = lv;
+      nlev = std::max(nlev, lv + 1);
+    }
+    std::vector<int> order;  // non-leaf nodes by (level, reference index)
+    for (int v = 0; v < nn; ++v)
+      if (level[v] >= 0) order.push_back(v);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return level[a] < level[b]; });
+    const int nl = (int)order.size();
+    if (nl >= 0xffff) {
+      err = "example too large: more than 65534 non-leaf DAG nodes";
+      return SK_ERR_UNSUPPORTED;
+    }
+    std::vector<int> nid(nn, -1);
+    for (int k = 0; k < nl; ++k) nid[order[k]] = k;
+    // path weights: number of root->v paths (parents have larger reference ids)
+    std::vector<double> Pw(nn, 0.0);
+    for (uint32_t r : X.roots) Pw[r] += 1.0;
+    for (int v = nn - 1; v >= 0; --v)
+      for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) Pw[X.edge_to[k]] += Pw[v];
+
+    const int ebase = (int)P.ed.size(), bbase = (int)P.bpf_code.size();
+    for (int k = 0; k < nl; ++k) {
+      const int v = order[k];
+      const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
+      const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
+      const uint32_t eloc = (uint32_t)P.ed.size() - ebase, bloc = (uint32_t)P.bpf_code.size() - bbase;
+      if (eloc > 0xffff || bloc > 0xffff || e1 - e0 > 0xff || b1 - b0 > 0xff ||
+          X.last[v] - X.first[v] > 0xffff) {
+        err = "example too large for the 16-bit packed DAG layout";
+        return SK_ERR_UNSUPPORTED;
+      }
+      P.nd_a.push_back(eloc | ((e1 - e0) << 16) | ((b1 - b0) << 24));
+      P.nd_b.push_back((X.last[v] - X.first[v]) | (bloc << 16));
+      P.nd_w.push_back(X.weight[v]);
+      P.nd_nbp.push_back(X.prof5[(size_t)X.first[v] * 5 + 4]);
+      P.nd_P.push_back(Pw[v]);
+      for (uint32_t t = e0; t < e1; ++t) {
+        const int c = nid[X.edge_to[t]];
+        const uint32_t child = c < 0 ? sk::kLeafChild : (uint32_t)c;
+        if (X.edge_gaps[t] > 0xffff) {
+          err = "gap count exceeds 16 bits";
+          return SK_ERR_UNSUPPORTED;
+        }
+        P.ed.push_back(child | (X.edge_gaps[t] << 16));
+      }
+      for (uint32_t t = b0; t < b1; ++t) {
+        P.bpf_code.push_back(X.bpf_code[t]);
+        P.bpf_p.push_back(X.bpf_p[t]);
+      }
+    }
+    std::vector<int32_t> lv(nlev + 1, 0);
+    for (int k = 0; k < nl; ++k) lv[level[order[k]] + 1]++;
+    for (int l = 0; l < nlev; ++l) lv[l + 1] += lv[l];
+    P.lvl.insert(P.lvl.end(), lv.begin(), lv.end());
+
+    P.ex_nl.push_back(nl);
+    P.ex_nlev.push_back(nlev);
+    P.ex_nseqs.push_back(X.n_seqs);
+    P.ex_len.push_back(X.len);
+    P.ex_has_w.push_back(X.has_bp ? 1 : 0);
+    for (int i = 0; i < X.len; ++i) {
+      const float* c = &X.prof5[(size_t)i * 5];
+      P.pos_prof.push_back(make_float4(c[0], c[1], c[2], c[3]));
+      P.pos_w.push_back(X.has_bp ? X.pos_weight[i] : 1.0f);
+    }
+    P.ex_node_base.push_back((int32_t)P.nd_a.size());
+    P.ex_edge_base.push_back((int32_t)P.ed.size());
+    P.ex_bpf_base.push_back((int32_t)P.bpf_code.size());
+    P.ex_lvl_base.push_back((int32_t)P.lvl.size());
+    P.ex_pos_base.push_back((int32_t)P.pos_prof.size());
+    P.max_nl = std::max(P.max_nl, nl);
+    P.max_edges = std::max(P.max_edges, (int)P.ed.size() - ebase);
+    P.max_bpf = std::max(P.max_bpf, (int)P.bpf_code.size() - bbase);
+    P.max_nlev = std::max(P.max_nlev, nlev);
+    P.max_len = std::max(P.max_len, X.len);
+  }
+  return SK_OK;
+}
+
+// ------------------------------------------------------------ parameters
+bool kind_has_stem(int k) { return k != SK_SU_STR && k != SK_SI_STR; }
+bool kind_has_str(int k) {
+  return k == SK_SU_STR || k == SK_SI_STR || k == SK_SU_STEM_STR || k == SK_SI_STEM_STR ||
+         k == SK_LSU_STEM_STR;
+}
+bool kind_subst(int k) {  // RIBOSUM (Su*) vs match/mismatch (Si*)
+  return k == SK_SU_STEM || k == SK_SU_STR || k == SK_SU_STEM_STR || k == SK_LSU_STEM ||
+         k == SK_LSU_STEM_STR;
+}
+int32_t combine_mode(int k) {
+  switch (k) {
+    case SK_SU_STEM:
+    case SK_SI_STEM: return sk::kCombineStem;
+    case SK_SU_STR:
+    case SK_SI_STR: return sk::kCombineStr;
+    case SK_SU_STEM_STR:
+    case SK_SI_STEM_STR: return sk::kCombineAdd;
+    case SK_LSU_STEM: return sk::kCombineLogStem;
+    default: return sk::kCombineLogAdd;
+  }
+}
+
+std::vector<double> gap_powers(double g, int n) {
+  // SimpleEdgeScore::initialize (score_table.cpp:239-256): g[k] = g[k-1]*gap
+  std::vector<double> v(std::max(n, 1));
+  v[0] = 1.0;
+  for (int k = 1; k < n; ++k) v[k] = v[k - 1] * g;
+  return v;
+}
+
+// ------------------------------------------------------------ work buffers
+struct Arena {
+  char* base;
+  size_t off = 0, cap;
+  template <class T>
+  T* take(size_t n) {
+    off = (off + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base + off);
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+int ensure_work(sk_context* ctx, size_t bytes) {
+  if (ctx->work_bytes >= bytes) return SK_OK;
+  if (ctx->work) {
+    SK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->work);
+    ctx->work = nullptr;
+    ctx->work_bytes = 0;
+  }
+  const size_t b = std::max(bytes, size_t(1) << 20);
+  SK_HIP(ctx, hipMalloc(&ctx->work, b));
+  ctx->work_bytes = b;
+  return SK_OK;
+}
+
+int ensure_scratch(sk_context* ctx, size_t bytes) {
+  if (ctx->scratch_bytes >= bytes) return SK_OK;
+  if (ctx->scratch) {
+    SK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->scratch);
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+  }
+  void* p = nullptr;
+  SK_HIP(ctx, hipMalloc(&p, bytes));
+  ctx->scratch = static_cast<double*>(p);
+  ctx->scratch_bytes = bytes;
+  return SK_OK;
+}
+
+int check_set(sk_context* ctx, sk_dataset* ds) {
+  if (!ds) return fail(ctx, SK_ERR_INVALID, "null dataset");
+  if (!ds->uploaded || ds->device != ctx->device)
+    return fail(ctx, SK_ERR_INVALID, "dataset not uploaded to this context's device");
+  return SK_OK;
+}
+
+// Core: out_dev[k] = K(xset[x[k]], yset[y[k]]) (device buffer), async.
+int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
+              const int32_t* x, const int32_t* y, int64_t n, double* out_dev) {
+  if (!ctx || !kp) return fail(ctx, SK_ERR_INVALID, "null argument");
+  int rc = check_set(ctx, xs_);
+  if (rc) return rc;
+  rc = check_set(ctx, ys_);
+  if (rc) return rc;
+  if (n < 0) return fail(ctx, SK_ERR_INVALID, "negative pair count");
+  if (kp->kind < SK_SU_STEM || kp->kind > SK_LSU_STEM_STR)
+    return fail(ctx, SK_ERR_UNSUPPORTED, "unknown kernel kind");
+  ctx->last_stem_ms = ctx->last_str_ms = ctx->last_cells = 0.0;
+  ctx->last_launches = 0;
+  if (n == 0) return SK_OK;
+  const int nx = (int)xs_->ex.size(), ny = (int)ys_->ex.size();
+  for (int64_t k = 0; k < n; ++k)
+    if (x[k] < 0 || x[k] >= nx || y[k] < 0 || y[k] >= ny)
+      return fail(ctx, SK_ERR_RANGE, "pair index out of range");
+
+  const bool stem = kind_has_stem(kp->kind), str = kind_has_str(kp->kind);
+  const HostPack& PX = xs_->pack;
+  const HostPack& PY = ys_->pack;
+
+  // ---- host-side work lists
+  // stem items: pairs grouped by y, chunks, largest first
+  std::vector<int4> items;
+  std::vector<int32_t> ixs;
+  std::vector<int64_t> ioidx;
+  const int max_len = std::max(PX.max_len, PY.max_len);
+  int nwaves = 1, grid = 1;
+  sk::StemLaunch SL;
+  if (stem) {
+    std::vector<int64_t> cnt(ny + 1, 0);
+    for (int64_t k = 0; k < n; ++k) cnt[y[k] + 1]++;
+    for (int j = 0; j < ny; ++j) cnt[j + 1] += cnt[j];
+    std::vector<int64_t> byy(n);
+    {
+      std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+      for (int64_t k = 0; k < n; ++k) byy[pos[y[k]]++] = k;
+    }
+    // LDS need and wave count
+    SL.lds_max_nl = std::max(PY.max_nl, 1);
+    SL.lds_max_nl = (SL.lds_max_nl + 1) & ~1;
+    SL.lds_max_edges = (std::max(PY.max_edges, 1) + 3) & ~3;
+    SL.lds_max_bpf = (std::max(PY.max_bpf, 1) + 3) & ~3;
+    SL.lds_max_nlev_pad = (PY.max_nlev + 1 + 3) & ~3;
+    SL.n_gpow = max_len + 2;
+    SL.n_gpow_pad = (SL.n_gpow + 1) & ~1;
+    int max_dyn = 0;
+    SK_HIP(ctx, sk::stem_kernel_attr(&max_dyn));
+    int best = 0;
+    for (int w = 16; w >= 1; --w) {
+      const size_t lds = sk::stem_lds_bytes(SL, w);
+      if (lds > (size_t)max_dyn) continue;
+      const int per_cu = std::min<int>((int)(163840 / lds), 32 / w);
+      if (per_cu * w > best) {
+        best = per_cu * w;
+        nwaves = w;
+      }
+    }
+    if (best == 0) return fail(ctx, SK_ERR_UNSUPPORTED, "y example too large for LDS");
+    const int per_cu = std::max(1, std::min<int>((int)(163840 / sk::stem_lds_bytes(SL, nwaves)),
+                                                 32 / nwaves));
+    grid = ctx->n_cu * per_cu;
+    const int chunk = 2 * nwaves;
+    struct It {
+      int4 v;
+      double cost;
+    };
+    std::vector<It> tmp;
+    for (int j = 0; j < ny; ++j) {
+      for (int64_t b = cnt[j]; b < cnt[j + 1]; b += chunk) {
+        const int64_t e = std::min<int64_t>(cnt[j + 1], b + chunk);
+        double cost = 0.0;
+        for (int64_t t = b; t < e; ++t)
+          cost += (double)PX.ex_nl[x[byy[t]]] * (double)PY.ex_nl[j];
+        tmp.push_back({make_int4(j, (int)b, (int)(e - b), 0), cost});
+      }
+    }
+    std::stable_sort(tmp.begin(), tmp.end(), [](const It& a, const It& b) { return a.cost > b.cost; });
+    items.reserve(tmp.size());
+    for (auto& t : tmp) items.push_back(t.v);
+    ixs.resize(n);
+    ioidx.resize(n);
+    for (int64_t t = 0; t < n; ++t) {
+      ixs[t] = x[byy[t]];
+      ioidx[t] = byy[t];
+    }
+    double cells = 0.0;
+    for (int64_t k = 0; k < n; ++k) cells += (double)PX.ex_nl[x[k]] * (double)PY.ex_nl[y[k]];
+    ctx->last_cells = cells;
+  }
+
+  // ---- device work arena
+  const size_t nb = (size_t)n;
+  size_t need = 0;
+  need += 256 * 8 + 16 * 8 + (size_t)(max_len + 4) * 8 * 2;
+  need += (size_t)PX.nd_a.size() * 8 * 2 + 1024;  // L, SL
+  need += items.size() * sizeof(int4) + nb * (4 + 8) + nb * 8 * 2 + nb * 4 * 2 + 64 + 8 * 256;
+  need += 16 * 256;
+  rc = ensure_work(ctx, need);
+  if (rc) return rc;
+  Arena A{static_cast<char*>(ctx->work), 0, ctx->work_bytes};
+  double* d_co = A.take<double>(256);
+  double* d_gp_loop = A.take<double>(max_len + 4);
+  double* d_st = A.take<double>(16);
+  double* d_gp_str = A.take<double>(max_len + 4);
+  double* d_L = A.take<double>(std::max<size_t>(PX.nd_a.size(), 1));
+  double* d_SL = A.take<double>(std::max<size_t>(PX.nd_a.size(), 1));
+  int4* d_items = A.take<int4>(std::max<size_t>(items.size(), 1));
+  int32_t* d_ixs = A.take<int32_t>(std::max<size_t>(nb, 1));
+  int64_t* d_oidx = A.take<int64_t>(std::max<size_t>(nb, 1));
+  double* d_stem = A.take<double>(nb);
+  double* d_str = A.take<double>(nb);
+  int32_t* d_px = A.take<int32_t>(nb);
+  int32_t* d_py = A.take<int32_t>(nb);
+  int* d_ctr = A.take<int>(64);
+
+  // parameter tables
+  std::vector<double> co(256), st(16);
+  const bool subst = kind_subst(kp->kind);
+  for (int k = 0; k < 256; ++k)
+    co[k] = subst ? std::exp(SK_RIBOSUM_P[k] * kp->beta)
+                  : ((k >> 4) == (k & 15) ? kp->stack : kp->covar);
+  for (int k = 0; k < 16; ++k)
+    st[k] = subst ? std::exp(SK_RIBOSUM_S[k] * kp->alpha)
+                  : ((k >> 2) == (k & 3) ? kp->match : kp->mismatch);
+  const std::vector<double> gl = gap_powers(kp->loop_gap, max_len + 4);
+  const std::vector<double> gs = gap_powers(kp->gap, max_len + 4);
+  hipStream_t S = ctx->stream;
+  SK_HIP(ctx, hipMemcpyAsync(d_co, co.data(), 256 * 8, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemcpyAsync(d_st, st.data(), 16 * 8, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemcpyAsync(d_gp_loop, gl.data(), gl.size() * 8, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemcpyAsync(d_gp_str, gs.data(), gs.size() * 8, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemsetAsync(d_ctr, 0, 64 * sizeof(int), S));
+
+  double* stem_out = (combine_mode(kp->kind) == sk::kCombineStem) ? out_dev : d_stem;
+  double* str_out = (combine_mode(kp->kind) == sk::kCombineStr) ? out_dev : d_str;
+
+  if (stem) {
+    SK_HIP(ctx, hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(int4),
+                               hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_ixs, ixs.data(), nb * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_oidx, ioidx.data(), nb * 8, hipMemcpyHostToDevice, S));
+    sk::DevParamNodes pn{d_L, d_SL};
+    const double gap2 = kp->loop_gap * kp->loop_gap;
+    SK_HIP(ctx, sk::launch_prep(xs_->dev, pn, d_gp_loop, gap2, S));
+    SL.xset = xs_->dev;
+    SL.yset = ys_->dev;
+    SL.pn = pn;
+    SL.co_subst = d_co;
+    SL.gpow = d_gp_loop;
+    SL.gap2 = gap2;
+    SL.band = kp->len_band;
+    SL.items = d_items;
+    SL.n_items = (int32_t)items.size();
+    SL.xs = d_ixs;
+    SL.oidx = d_oidx;
+    SL.out = stem_out;
+    SL.item_counter = d_ctr;
+    SL.slab_doubles = (int64_t)std::max(PX.max_nl, 1) * std::max(PY.max_nl, 1);
+    SL.slab_doubles = (SL.slab_doubles + 31) & ~int64_t(31);
+    grid = std::min<int64_t>(grid, std::max<int64_t>(1, (int64_t)items.size()));
+    rc = ensure_scratch(ctx, (size_t)grid * nwaves * SL.slab_doubles * sizeof(double));
+    if (rc) return rc;
+    SL.scratch = ctx->scratch;
+    SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
+    SK_HIP(ctx, sk::launch_stem(SL, grid, nwaves, S));
+    SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
+    ctx->last_launches = 1;
+  }
+  if (str) {
+    SK_HIP(ctx, hipMemcpyAsync(d_px, x, nb * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_py, y, nb * 4, hipMemcpyHostToDevice, S));
+    sk::StrLaunch T;
+    T.xset = xs_->dev;
+    T.yset = ys_->dev;
+    T.st = d_st;
+    T.gpow = d_gp_str;
+    T.gap = kp->gap;
+    T.xs = d_px;
+    T.ys = d_py;
+    T.n_pairs = n;
+    T.out = str_out;
+    T.pair_counter = reinterpret_cast<unsigned long long*>(d_ctr + 8);
+    T.lds_max_len = (std::max(PY.max_len, 1) + 1) & ~1;
+    const int w = 4;
+    const size_t lds = sk::str_lds_bytes(T, w);
+    if (lds > 65536) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for string kernel LDS");
+    const int per_cu = std::max(1, std::min<int>((int)(163840 / lds), 8));
+    const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (n + w - 1) / w);
+    SK_HIP(ctx, hipEventRecord(ctx->ev2, S));
+    SK_HIP(ctx, sk::launch_str(T, (int)g, w, S));
+    SK_HIP(ctx, hipEventRecord(ctx->ev3, S));
+  }
+  const int32_t mode = combine_mode(kp->kind);
+  if (mode != sk::kCombineStem && mode != sk::kCombineStr)
+    SK_HIP(ctx, sk::launch_combine(d_stem, d_str, out_dev, n, mode, kp->alpha, kp->beta, S));
+  // timings (blocking read of the events happens in sk_last_timing callers)
+  SK_HIP(ctx, hipStreamSynchronize(S));
+  if (stem) {
+    float ms = 0.f;
+    SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last_stem_ms = ms;
+  }
+  if (str) {
+    float ms = 0.f;
+    SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev2, ctx->ev3));
+    ctx->last_str_ms = ms;
+  }
+  return SK_OK;
+}
+
+int pairs_host(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
+               const int32_t* x, const int32_t* y, int64_t n, double* out) {
+  if (n == 0) return SK_OK;
+  double* d = nullptr;
+  SK_HIP(ctx, hipMalloc(&d, (size_t)n * sizeof(double)));
+  int rc = run_pairs(ctx, xs_, ys_, kp, x, y, n, d);
+  if (rc == SK_OK) {
+    hipError_t e = hipMemcpy(out, d, (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = fail(ctx, SK_ERR_HIP, hipGetErrorString(e));
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
+}  // namespace
+
+// =================================================================== ABI
+extern "C" {
+
+void sk_kernel_params_default(sk_kernel_params* p, int32_t kind) {
+  if (!p) return;
+  p->kind = kind;
+  p->len_band = 10;
+  p->beta = 0.3;
+  p->loop_gap = 0.2;
+  p->stack = 1.3;
+  p->covar = 0.8;
+  p->alpha = 0.2;
+  p->gap = 0.8;
+  p->match = 1.0;
+  p->mismatch = 0.8;
+}
+
+const char* sk_strerror(int s) {
+  switch (s) {
+    case SK_OK: return "ok";
+    case SK_ERR_INVALID: return "invalid argument";
+    case SK_ERR_HIP: return "HIP runtime error";
+    case SK_ERR_NO_DEVICE: return "no usable gfx950 device";
+    case SK_ERR_ALLOC: return "allocation failed";
+    case SK_ERR_RANGE: return "index out of range";
+    case SK_ERR_UNSUPPORTED: return "unsupported";
+    default: return "unknown status";
+  }
+}
+
+const char* sk_last_error(const sk_context* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+int sk_open(int device, void* hip_stream, sk_context** out) {
+  if (!out) return SK_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SK_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return SK_ERR_RANGE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SK_ERR_NO_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SK_ERR_NO_DEVICE;
+  std::unique_ptr<sk_context> c(new (std::nothrow) sk_context());
+  if (!c) return SK_ERR_ALLOC;
+  c->device = device;
+  c->n_cu = prop.multiProcessorCount;
+  if (hipSetDevice(device) != hipSuccess) return SK_ERR_HIP;
+  if (hip_stream) {
+    c->stream = static_cast<hipStream_t>(hip_stream);
+  } else {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return SK_ERR_HIP;
+    c->own_stream = true;
+  }
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess)
+    return SK_ERR_HIP;
+  *out = c.release();
+  return SK_OK;
+}
+
+int sk_close(sk_context* ctx) {
+  if (!ctx) return SK_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->work) (void)hipFree(ctx->work);
+  for (hipEvent_t e : {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3})
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return SK_OK;
+}
+
+int sk_dataset_create(sk_dataset** ds) {
+  if (!ds) return SK_ERR_INVALID;
+  *ds = new (std::nothrow) sk_dataset();
+  return *ds ? SK_OK : SK_ERR_ALLOC;
+}
+
+int sk_dataset_free(sk_dataset* ds) {
+  delete ds;
+  return SK_OK;
+}
+
+int sk_dataset_add(sk_dataset* ds, const char* label, int n_rows, const char* const* rows,
+                   const double* const* bpp_rows, float th, int use_bp) {
+  if (!ds || n_rows <= 0 || !rows) return SK_ERR_INVALID;
+  if (use_bp && !bpp_rows) return SK_ERR_INVALID;
+  if (ds->uploaded) return SK_ERR_INVALID;
+  try {
+    Example ex;
+    sk::build_example(ex, n_rows, rows, bpp_rows, th, use_bp != 0);
+    ds->ex.push_back(std::move(ex));
+    ds->labels.emplace_back(label ? label : "");
+  } catch (const std::bad_alloc&) {
+    return SK_ERR_ALLOC;
+  } catch (const std::exception& e) {
+    ds->err = e.what();
+    return SK_ERR_INVALID;
+  }
+  return SK_OK;
+}
+
+int sk_dataset_size(const sk_dataset* ds) { return ds ? (int)ds->ex.size() : 0; }
+
+const char* sk_dataset_label(const sk_dataset* ds, int i) {
+  if (!ds || i < 0 || i >= (int)ds->labels.size()) return nullptr;
+  return ds->labels[i].c_str();
+}
+
+int sk_dataset_shape(const sk_dataset* ds, int i, int32_t* n_nodes, int32_t* n_edges,
+                     int32_t* n_bpfreq, int32_t* n_roots, int32_t* seq_len) {
+  if (!ds) return SK_ERR_INVALID;
+  if (i < 0 || i >= (int)ds->ex.size()) return SK_ERR_RANGE;
+  const Example& X = ds->ex[i];
+  if (n_nodes) *n_nodes = X.n_nodes();
+  if (n_edges) *n_edges = X.n_edges();
+  if (n_bpfreq) *n_bpfreq = (int32_t)X.bpf_code.size();
+  if (n_roots) *n_roots = (int32_t)X.roots.size();
+  if (seq_len) *seq_len = X.len;
+  return SK_OK;
+}
+
+int sk_dataset_dag(const sk_dataset* ds, int i, uint32_t* first, uint32_t* last,
+                   uint32_t* n_edges, uint32_t* n_bpfreq, float* weight, uint32_t* max_pa,
+                   uint32_t* edge_to, uint32_t* edge_gaps, uint32_t* bp_code, float* bp_p,
+                   uint32_t* roots, float* pos_weight) {
+  if (!ds) return SK_ERR_INVALID;
+  if (i < 0 || i >= (int)ds->ex.size()) return SK_ERR_RANGE;
+  const Example& X = ds->ex[i];
+  const int n = X.n_nodes();
+  for (int v = 0; v < n; ++v) {
+    if (first) first[v] = X.first[v];
+    if (last) last[v] = X.last[v];
+    if (n_edges) n_edges[v] = X.edge_off[v + 1] - X.edge_off[v];
+    if (n_bpfreq) n_bpfreq[v] = X.bpf_off[v + 1] - X.bpf_off[v];
+    if (weight) weight[v] = X.weight[v];
+    if (max_pa) max_pa[v] = X.max_pa[v];
+  }
+  if (edge_to) std::copy(X.edge_to.begin(), X.edge_to.end(), edge_to);
+  if (edge_gaps) std::copy(X.edge_gaps.begin(), X.edge_gaps.end(), edge_gaps);
+  if (bp_code) std::copy(X.bpf_code.begin(), X.bpf_code.end(), bp_code);
+  if (bp_p) std::copy(X.bpf_p.begin(), X.bpf_p.end(), bp_p);
+  if (roots) std::copy(X.roots.begin(), X.roots.end(), roots);
+  if (pos_weight && X.has_bp) std::copy(X.pos_weight.begin(), X.pos_weight.end(), pos_weight);
+  return SK_OK;
+}
+
+int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
+  if (!ctx || !ds) return SK_ERR_INVALID;
+  if (ds->uploaded) return ds->device == ctx->device ? SK_OK : fail(ctx, SK_ERR_INVALID, "dataset bound to another device");
+  std::string err;
+  int rc = pack_dataset(ds, err);
+  if (rc) return fail(ctx, rc, err);
+  SK_HIP(ctx, hipSetDevice(ctx->device));
+  HostPack& P = ds->pack;
+  DevSet& D = ds->dev;
+  DeviceBuffers& B = ds->buf;
+  D.n_examples = (int32_t)ds->ex.size();
+  SK_HIP(ctx, upload(B, P.ex_nl, &D.ex_nl));
+  SK_HIP(ctx, upload(B, P.ex_node_base, &D.ex_node_base));
+  SK_HIP(ctx, upload(B, P.ex_edge_base, &D.ex_edge_base));
+  SK_HIP(ctx, upload(B, P.ex_bpf_base, &D.ex_bpf_base));
+  SK_HIP(ctx, upload(B, P.ex_lvl_base, &D.ex_lvl_base));
+  SK_HIP(ctx, upload(B, P.ex_nlev, &D.ex_nlev));
+  SK_HIP(ctx, upload(B, P.ex_nseqs, &D.ex_nseqs));
+  SK_HIP(ctx, upload(B, P.ex_len, &D.ex_len));
+  SK_HIP(ctx, upload(B, P.ex_pos_base, &D.ex_pos_base));
+  SK_HIP(ctx, upload(B, P.ex_has_w, &D.ex_has_w));
+  SK_HIP(ctx, upload(B, P.nd_a, &D.nd_a));
+  SK_HIP(ctx, upload(B, P.nd_b, &D.nd_b));
+  SK_HIP(ctx, upload(B, P.nd_w, &D.nd_w));
+  SK_HIP(ctx, upload(B, P.nd_nbp, &D.nd_nbp));
+  SK_HIP(ctx, upload(B, P.nd_P, &D.nd_P));
+  SK_HIP(ctx, upload(B, P.ed, &D.ed));
+  SK_HIP(ctx, upload(B, P.bpf_code, &D.bpf_code));
+  SK_HIP(ctx, upload(B, P.bpf_p, &D.bpf_p));
+  SK_HIP(ctx, upload(B, P.lvl, &D.lvl));
+  SK_HIP(ctx, upload(B, P.pos_prof, &D.pos_prof));
+  SK_HIP(ctx, upload(B, P.pos_w, &D.pos_w));
+  D.max_nl = P.max_nl;
+  D.max_edges = P.max_edges;
+  D.max_bpf = P.max_bpf;
+  D.max_nlev = P.max_nlev;
+  D.max_len = P.max_len;
+  D.total_nodes = (int64_t)P.nd_a.size();
+  ds->device = ctx->device;
+  ds->uploaded = true;
+  return SK_OK;
+}
+
+int sk_pairs_device(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp, const int32_t* x,
+                    const int32_t* y, int64_t n_pairs, double* out_dev) {
+  return run_pairs(ctx, ds, ds, kp, x, y, n_pairs, out_dev);
+}
+
+int sk_pairs(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp, const int32_t* x,
+             const int32_t* y, int64_t n_pairs, double* out) {
+  return pairs_host(ctx, ds, ds, kp, x, y, n_pairs, out);
+}
+
+int sk_gram(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp, int normalize,
+            double* out) {
+  if (!ctx || !ds || !kp || !out) return fail(ctx, SK_ERR_INVALID, "null argument");
+  const int n = (int)ds->ex.size();
+  std::vector<int32_t> xi, yi;
+  xi.reserve((size_t)n * (n + 1) / 2);
+  yi.reserve((size_t)n * (n + 1) / 2);
+  // the reference's cell order (kernel_matrix.cpp:44-55): i outer, j >= i
+  for (int i = 0; i < n; ++i)
+    for (int j = i; j < n; ++j) {
+      xi.push_back(i);
+      yi.push_back(j);
+    }
+  std::vector<double> v(xi.size());
+  int rc = pairs_host(ctx, ds, ds, kp, xi.data(), yi.data(), (int64_t)xi.size(), v.data());
+  if (rc) return rc;
+  size_t k = 0;
+  for (int i = 0; i < n; ++i)
+    for (int j = i; j < n; ++j, ++k) {
+      out[(size_t)i * n + j] = v[k];
+      if (i != j) out[(size_t)j * n + i] = v[k];
+    }
+  if (normalize && n > 0) {
+    // kernel_matrix.cpp:560-571
+    for (int i = 0; i + 1 < n; ++i)
+      for (int j = i + 1; j < n; ++j) {
+        out[(size_t)i * n + j] /= std::sqrt(out[(size_t)i * n + i] * out[(size_t)j * n + j]);
+        out[(size_t)j * n + i] = out[(size_t)i * n + j];
+      }
+    for (int i = 0; i < n; ++i) out[(size_t)i * n + i] = 1;
+  }
+  return SK_OK;
+}
+
+int sk_test_row(sk_context* ctx, sk_dataset* test, int t, sk_dataset* train,
+                const int32_t* sv_index, int32_t n_sv, const sk_kernel_params* kp, double* out,
+                double* self) {
+  if (!ctx || !test || !train || !kp || !out) return fail(ctx, SK_ERR_INVALID, "null argument");
+  if (t < 0 || t >= (int)test->ex.size()) return fail(ctx, SK_ERR_RANGE, "test index");
+  const int ntr = (int)train->ex.size();
+  std::vector<int32_t> xi, yi;
+  if (sv_index) {
+    for (int32_t k = 0; k < n_sv; ++k) {
+      if (sv_index[k] < 0 || sv_index[k] >= ntr) return fail(ctx, SK_ERR_RANGE, "sv index");
+      xi.push_back(sv_index[k]);
+    }
+  } else {
+    for (int i = 0; i < ntr; ++i) xi.push_back(i);
+  }
+  yi.assign(xi.size(), t);
+  std::vector<double> v(xi.size());
+  // kernel_(train_[i].second, data_.second): x = train, y = test
+  int rc = pairs_host(ctx, train, test, kp, xi.data(), yi.data(), (int64_t)xi.size(), v.data());
+  if (rc) return rc;
+  for (size_t k = 0; k < xi.size(); ++k) out[xi[k]] = v[k];
+  if (self) {
+    const int32_t a = t;
+    rc = pairs_host(ctx, test, test, kp, &a, &a, 1, self);
+    if (rc) return rc;
+  }
+  return SK_OK;
+}
+
+int sk_diagonal(sk_context* ctx, sk_dataset* ds, const int32_t* sv_index, int32_t n_sv,
+                const sk_kernel_params* kp, double* out) {
+  if (!ctx || !ds || !kp || !out) return fail(ctx, SK_ERR_INVALID, "null argument");
+  const int n = (int)ds->ex.size();
+  std::vector<int32_t> xi;
+  if (sv_index) {
+    for (int32_t k = 0; k < n_sv; ++k) {
+      if (sv_index[k] < 0 || sv_index[k] >= n) return fail(ctx, SK_ERR_RANGE, "sv index");
+      xi.push_back(sv_index[k]);
+    }
+  } else {
+    for (int i = 0; i < n; ++i) xi.push_back(i);
+  }
+  std::vector<double> v(xi.size());
+  int rc = pairs_host(ctx, ds, ds, kp, xi.data(), xi.data(), (int64_t)xi.size(), v.data());
+  if (rc) return rc;
+  for (size_t k = 0; k < xi.size(); ++k) out[xi[k]] = v[k];
+  return SK_OK;
+}
+
+int sk_test_matrix(sk_context* ctx, sk_dataset* test, sk_dataset* train,
+                   const sk_kernel_params* kp, int norm_test, int normalize, double* out,
+                   double* self_out) {
+  if (!ctx || !test || !train || !kp || !out) return fail(ctx, SK_ERR_INVALID, "null argument");
+  const int nt = (int)test->ex.size(), ntr = (int)train->ex.size();
+  std::vector<int32_t> xi, yi;
+  for (int i = 0; i < nt; ++i)
+    for (int j = 0; j < ntr; ++j) {
+      xi.push_back(j);
+      yi.push_back(i);
+    }
+  int rc = pairs_host(ctx, train, test, kp, xi.data(), yi.data(), (int64_t)xi.size(), out);
+  if (rc) return rc;
+  std::vector<double> self(nt, 0.0);
+  if (norm_test || normalize) {
+    std::vector<int32_t> ti(nt);
+    std::iota(ti.begin(), ti.end(), 0);
+    rc = pairs_host(ctx, test, test, kp, ti.data(), ti.data(), nt, self.data());
+    if (rc) return rc;
+    if (self_out) std::copy(self.begin(), self.end(), self_out);
+  }
+  if (normalize) {
+    std::vector<double> diag(ntr);
+    rc = sk_diagonal(ctx, train, nullptr, 0, kp, diag.data());
+    if (rc) return rc;
+    for (int i = 0; i < nt; ++i)
+      for (int j = 0; j < ntr; ++j) out[(size_t)i * ntr + j] /= std::sqrt(self[i] * diag[j]);
+  }
+  return SK_OK;
+}
+
+int sk_format_libsvm(const double* m, int32_t rows, int32_t cols, const char* const* labels,
+                     char* buf, size_t buf_size, size_t* needed) {
+  if ((!m && rows * cols) || rows < 0 || cols < 0) return SK_ERR_INVALID;
+  // KernelMatrix::print (kernel_matrix.cpp:756-770): ostream defaults
+  std::ostringstream os;
+  for (int32_t i = 0; i < rows; ++i) {
+    os << (labels && labels[i] ? labels[i] : "") << " 0:" << (i + 1) << " ";
+    for (int32_t j = 0; j < cols; ++j) os << (j + 1) << ":" << m[(size_t)i * cols + j] << " ";
+    os << "\n";
+  }
+  const std::string s = os.str();
+  if (needed) *needed = s.size() + 1;
+  if (buf) {
+    if (buf_size < s.size() + 1) return SK_ERR_RANGE;
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+  }
+  return SK_OK;
+}
+
+int sk_fold_synthetic(const char* seq, int32_t n, int32_t no_gu, double* out) {
+  if (!seq || n < 0 || (!out && n > 1)) return SK_ERR_INVALID;
+  try {
+    sk::fold_nussinov(seq, n, no_gu != 0, out);
+  } catch (const std::bad_alloc&) {
+    return SK_ERR_ALLOC;
+  }
+  return SK_OK;
+}
+
+int sk_random_sequences(uint64_t* state, int32_t n_seqs, int32_t len, char* out) {
+  if (!state || !out || n_seqs < 0 || len < 0) return SK_ERR_INVALID;
+  for (int32_t s = 0; s < n_seqs; ++s) sk::random_sequence(*state, len, out + (size_t)s * (len + 1));
+  return SK_OK;
+}
+
+int sk_last_timing(const sk_context* ctx, double* stem_ms, double* string_ms, double* cells,
+                   int32_t* launches) {
+  if (!ctx) return SK_ERR_INVALID;
+  if (stem_ms) *stem_ms = ctx->last_stem_ms;
+  if (string_ms) *string_ms = ctx->last_str_ms;
+  if (cells) *cells = ctx->last_cells;
+  if (launches) *launches = ctx->last_launches;
+  return SK_OK;
+}
+
+void sk_ribosum_tables(float* s16, float* p256) {
+  if (s16) std::memcpy(s16, SK_RIBOSUM_S, sizeof(SK_RIBOSUM_S));
+  if (p256) std::memcpy(p256, SK_RIBOSUM_P, sizeof(SK_RIBOSUM_P));
+}
+
+int sk_char2rna(int c) { return sk::char2rna(c); }
+
+}  // extern "C"

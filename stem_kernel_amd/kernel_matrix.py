@@ -1,0 +1,374 @@
+"""Host-side mirror of the reference's plugin interface for the hot path.
+
+Names, argument meaning and defaults follow the reference:
+
+* kernel classes -- ``stem_kernel_lite/def_kernel.h`` (SuStemKernel,
+  SiStemKernel, SuStemStrKernel, SiStemStrKernel, LSuStemKernel,
+  LSuStemStrKernel), ``stem_kernel_lite/string_kernel.h`` (StringKernel) and
+  ``stem_kernel_lite/ss_kernel.h`` (StemStrKernel == SuStemStrKernel);
+* ``Dataset`` -- the ExampleSet of (label, MData) that ``App::load_examples``
+  builds (``common/framework.h:308-353``; ``MData`` ctor
+  ``stem_kernel_lite/data.cpp:466-487``);
+* ``KernelMatrix`` -- ``common/kernel_matrix.h:13-108``: ``calculate`` (train
+  Gram / test x train), ``calculate_row`` (test row), ``diagonal``, ``print``.
+
+Every computation goes through the HIP engine (libstem_kernel_amd.so); there
+is no CPU fallback.  Errors raise ``StemKernelError`` (the reference threw
+``const char*``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import sys
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import KernelParams, StemKernelError, check, lib
+
+__all__ = [
+    "fold", "random_sequences", "Dataset", "Context", "KernelMatrix",
+    "SuStemKernel", "SiStemKernel", "StringKernel", "SuStemStrKernel", "StemStrKernel",
+    "SiStemStrKernel", "LSuStemKernel", "LSuStemStrKernel", "StemKernelError",
+]
+
+
+# --------------------------------------------------------------------- inputs
+def fold(seq: str, no_gu: bool = False) -> np.ndarray:
+    """Synthetic base-pairing probabilities (Nussinov-Boltzmann stand-in for
+    Vienna pf_fold), packed strict upper triangle of length n(n-1)/2."""
+    n = len(seq)
+    out = np.zeros(max(n * (n - 1) // 2, 1), dtype=np.float64)
+    check(lib().sk_fold_synthetic(seq.encode(), n, int(no_gu),
+                                  out.ctypes.data_as(C.POINTER(C.c_double))))
+    return out[: n * (n - 1) // 2]
+
+
+def random_sequences(n: int, length: int, seed: int) -> List[str]:
+    """splitmix64 ACGU sequences (SURVEY.md §8d generator)."""
+    st = C.c_uint64(seed)
+    buf = C.create_string_buffer(n * (length + 1))
+    check(lib().sk_random_sequences(C.byref(st), n, length, buf))
+    raw = buf.raw
+    return [raw[i * (length + 1): i * (length + 1) + length].decode() for i in range(n)]
+
+
+# --------------------------------------------------------------------- kernels
+class _Kernel:
+    kind = _lib.SU_STEM
+
+    def __init__(self, **kw):
+        self.params = _lib.default_params(self.kind, **kw)
+
+    def __repr__(self):
+        p = self.params
+        f = {k: getattr(p, k) for k, _ in KernelParams._fields_}
+        return f"{type(self).__name__}({f})"
+
+
+class SuStemKernel(_Kernel):
+    """SuStemKernel(loop_gap, beta, len_band)  def_kernel.h:262-283 (--no-string)."""
+    kind = _lib.SU_STEM
+
+    def __init__(self, loop_gap=0.2, beta=0.3, len_band=10):
+        super().__init__(loop_gap=loop_gap, beta=beta, len_band=len_band)
+
+
+class SiStemKernel(_Kernel):
+    """SiStemKernel(loop_gap, stack, covar, len_band)  def_kernel.h:238-260."""
+    kind = _lib.SI_STEM
+
+    def __init__(self, loop_gap=0.2, stack=1.3, covar=0.8, len_band=10):
+        super().__init__(loop_gap=loop_gap, stack=stack, covar=covar, len_band=len_band)
+
+
+class StringKernel(_Kernel):
+    """StringKernel(gap, alpha) or StringKernel(gap, match, mismatch)
+    (stem_kernel_lite/string_kernel.cpp:46-70)."""
+
+    def __init__(self, gap=0.8, alpha=None, match=None, mismatch=None):
+        if match is not None or mismatch is not None:
+            self.kind = _lib.SI_STR
+            super().__init__(gap=gap, match=1.0 if match is None else match,
+                             mismatch=0.8 if mismatch is None else mismatch)
+        else:
+            self.kind = _lib.SU_STR
+            super().__init__(gap=gap, alpha=0.2 if alpha is None else alpha)
+
+
+class SuStemStrKernel(_Kernel):
+    """SuStemStrKernel(alpha, beta, loop_gap, gap, len_band)  def_kernel.h:313-338;
+    identical to StemStrKernel<SubstScoreTable> of ss_kernel.h:9-38."""
+    kind = _lib.SU_STEM_STR
+
+    def __init__(self, alpha=0.2, beta=0.3, loop_gap=0.2, gap=0.8, len_band=10):
+        super().__init__(alpha=alpha, beta=beta, loop_gap=loop_gap, gap=gap, len_band=len_band)
+
+
+StemStrKernel = SuStemStrKernel
+
+
+class SiStemStrKernel(_Kernel):
+    """SiStemStrKernel(loop_gap, stack, covar, gap, match, mismatch, len_band)
+    def_kernel.h:285-311 (--no-ribosum)."""
+    kind = _lib.SI_STEM_STR
+
+    def __init__(self, loop_gap=0.2, stack=1.3, covar=0.8, gap=0.8, match=1.0, mismatch=0.8,
+                 len_band=10):
+        super().__init__(loop_gap=loop_gap, stack=stack, covar=covar, gap=gap, match=match,
+                         mismatch=mismatch, len_band=len_band)
+
+
+class LSuStemKernel(_Kernel):
+    """LSuStemKernel: beta*log(K_stem)  def_kernel.h:340-364 (--log --no-string)."""
+    kind = _lib.LSU_STEM
+
+    def __init__(self, loop_gap=0.2, beta=0.3, len_band=10):
+        super().__init__(loop_gap=loop_gap, beta=beta, len_band=len_band)
+
+
+class LSuStemStrKernel(_Kernel):
+    """LSuStemStrKernel: beta*log K_stem + alpha*log K_str  def_kernel.h:392-417 (--log)."""
+    kind = _lib.LSU_STEM_STR
+
+    def __init__(self, alpha=0.2, beta=0.3, loop_gap=0.2, gap=0.8, len_band=10):
+        super().__init__(alpha=alpha, beta=beta, loop_gap=loop_gap, gap=gap, len_band=len_band)
+
+
+# --------------------------------------------------------------------- data
+class Dataset:
+    """ExampleSet of (label, MData); examples are built on the host by the
+    engine's DAG builder and uploaded once per device."""
+
+    def __init__(self):
+        self._h = C.c_void_p()
+        check(lib().sk_dataset_create(C.byref(self._h)))
+        self._uploaded_ctx = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.sk_dataset_free(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def add(self, label: str, rows: Sequence[str], bpp_rows: Optional[Sequence[np.ndarray]] = None,
+            th: float = 0.01, use_bp: bool = True) -> None:
+        """Append one example (an alignment of ``rows``).  ``bpp_rows[r]`` is the
+        packed bp matrix of the gap-erased row r; computed with ``fold`` when
+        omitted."""
+        rows = list(rows)
+        if use_bp and bpp_rows is None:
+            bpp_rows = [fold(r.replace("-", "").lower()) for r in rows]
+        n = len(rows)
+        carr = (C.c_char_p * n)(*[r.encode() for r in rows])
+        keep = []
+        if use_bp:
+            barr = (C.POINTER(C.c_double) * n)()
+            for k, b in enumerate(bpp_rows):
+                b = np.ascontiguousarray(b, dtype=np.float64)
+                if b.size == 0:
+                    b = np.zeros(1)
+                keep.append(b)
+                barr[k] = b.ctypes.data_as(C.POINTER(C.c_double))
+        else:
+            barr = None
+        rc = lib().sk_dataset_add(self._h, label.encode(), n, carr, barr, C.c_float(th), int(use_bp))
+        check(rc)
+
+    @classmethod
+    def from_sequences(cls, seqs: Iterable[str], labels: Optional[Iterable[str]] = None,
+                       th: float = 0.01, bpp: Optional[Sequence[np.ndarray]] = None):
+        ds = cls()
+        seqs = list(seqs)
+        labels = list(labels) if labels is not None else ["+1"] * len(seqs)
+        for k, s in enumerate(seqs):
+            ds.add(labels[k], [s], None if bpp is None else [bpp[k]], th=th)
+        return ds
+
+    def __len__(self):
+        return lib().sk_dataset_size(self._h)
+
+    def label(self, i: int) -> str:
+        return lib().sk_dataset_label(self._h, i).decode()
+
+    def shape(self, i: int):
+        v = [C.c_int32() for _ in range(5)]
+        check(lib().sk_dataset_shape(self._h, i, *[C.byref(a) for a in v]))
+        return tuple(a.value for a in v)  # nodes, edges, bpfreq, roots, len
+
+    def dag(self, i: int) -> dict:
+        """The DAG of example i (reference numbering), for packer parity."""
+        nn, ne, nb, nr, L = self.shape(i)
+        u = lambda k: np.zeros(max(k, 1), np.uint32)
+        f = lambda k: np.zeros(max(k, 1), np.float32)
+        d = dict(first=u(nn), last=u(nn), n_edges=u(nn), n_bpfreq=u(nn), weight=f(nn),
+                 max_pa=u(nn), edge_to=u(ne), edge_gaps=u(ne), bp_code=u(nb), bp_p=f(nb),
+                 roots=u(nr), pos_weight=f(L))
+        ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint32 if a.dtype == np.uint32 else C.c_float))
+        check(lib().sk_dataset_dag(self._h, i, *[ptr(d[k]) for k in
+                                                 ("first", "last", "n_edges", "n_bpfreq", "weight",
+                                                  "max_pa", "edge_to", "edge_gaps", "bp_code",
+                                                  "bp_p", "roots", "pos_weight")]))
+        sizes = dict(first=nn, last=nn, n_edges=nn, n_bpfreq=nn, weight=nn, max_pa=nn,
+                     edge_to=ne, edge_gaps=ne, bp_code=nb, bp_p=nb, roots=nr, pos_weight=L)
+        return {k: v[: sizes[k]] for k, v in d.items()}
+
+
+# --------------------------------------------------------------------- device
+class Context:
+    """One context per GPU (sk_open)."""
+
+    def __init__(self, device: int = 0, stream: Optional[int] = None):
+        self._h = C.c_void_p()
+        check(lib().sk_open(device, C.c_void_p(stream) if stream else None, C.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            lib().sk_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _chk(self, rc):
+        return check(rc, self._h)
+
+    def upload(self, ds: Dataset):
+        self._chk(lib().sk_dataset_upload(self._h, ds.handle))
+
+    def gram(self, ds: Dataset, kernel: _Kernel, normalize: bool = False) -> np.ndarray:
+        self.upload(ds)
+        n = len(ds)
+        out = np.zeros((n, n), dtype=np.float64)
+        self._chk(lib().sk_gram(self._h, ds.handle, C.byref(kernel.params), int(normalize),
+                                out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
+    def pairs(self, ds: Dataset, kernel: _Kernel, x, y) -> np.ndarray:
+        self.upload(ds)
+        x = np.ascontiguousarray(x, dtype=np.int32)
+        y = np.ascontiguousarray(y, dtype=np.int32)
+        out = np.zeros(x.size, dtype=np.float64)
+        self._chk(lib().sk_pairs(self._h, ds.handle, C.byref(kernel.params),
+                                 x.ctypes.data_as(C.POINTER(C.c_int32)),
+                                 y.ctypes.data_as(C.POINTER(C.c_int32)), x.size,
+                                 out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
+    def pairs_device(self, ds: Dataset, kernel: _Kernel, x, y, out_ptr: int) -> None:
+        self.upload(ds)
+        x = np.ascontiguousarray(x, dtype=np.int32)
+        y = np.ascontiguousarray(y, dtype=np.int32)
+        self._chk(lib().sk_pairs_device(self._h, ds.handle, C.byref(kernel.params),
+                                        x.ctypes.data_as(C.POINTER(C.c_int32)),
+                                        y.ctypes.data_as(C.POINTER(C.c_int32)), x.size,
+                                        C.c_void_p(out_ptr)))
+
+    def test_row(self, test: Dataset, t: int, train: Dataset, kernel: _Kernel,
+                 sv_index=None, self_value: bool = False):
+        self.upload(test)
+        self.upload(train)
+        out = np.zeros(len(train), dtype=np.float64)
+        sv = None if sv_index is None else np.ascontiguousarray(sv_index, dtype=np.int32)
+        sf = C.c_double(0.0)
+        self._chk(lib().sk_test_row(self._h, test.handle, t, train.handle,
+                                    None if sv is None else sv.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    0 if sv is None else sv.size, C.byref(kernel.params),
+                                    out.ctypes.data_as(C.POINTER(C.c_double)),
+                                    C.byref(sf) if self_value else None))
+        return (out, sf.value) if self_value else out
+
+    def diagonal(self, ds: Dataset, kernel: _Kernel, sv_index=None) -> np.ndarray:
+        self.upload(ds)
+        out = np.zeros(len(ds), dtype=np.float64)
+        sv = None if sv_index is None else np.ascontiguousarray(sv_index, dtype=np.int32)
+        self._chk(lib().sk_diagonal(self._h, ds.handle,
+                                    None if sv is None else sv.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    0 if sv is None else sv.size, C.byref(kernel.params),
+                                    out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
+    def test_matrix(self, test: Dataset, train: Dataset, kernel: _Kernel, norm_test=False,
+                    normalize=False):
+        self.upload(test)
+        self.upload(train)
+        out = np.zeros((len(test), len(train)), dtype=np.float64)
+        self_ = np.zeros(len(test), dtype=np.float64)
+        self._chk(lib().sk_test_matrix(self._h, test.handle, train.handle, C.byref(kernel.params),
+                                       int(norm_test), int(normalize),
+                                       out.ctypes.data_as(C.POINTER(C.c_double)),
+                                       self_.ctypes.data_as(C.POINTER(C.c_double))))
+        return out, self_
+
+    def last_timing(self):
+        a, b, c, d = C.c_double(), C.c_double(), C.c_double(), C.c_int32()
+        self._chk(lib().sk_last_timing(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return dict(stem_ms=a.value, string_ms=b.value, cells=c.value, launches=d.value)
+
+
+def format_libsvm(matrix: np.ndarray, labels: Sequence[str]) -> str:
+    m = np.ascontiguousarray(matrix, dtype=np.float64)
+    rows, cols = m.shape
+    larr = (C.c_char_p * rows)(*[l.encode() for l in labels])
+    need = C.c_size_t()
+    check(lib().sk_format_libsvm(m.ctypes.data_as(C.POINTER(C.c_double)), rows, cols, larr, None,
+                                 0, C.byref(need)))
+    buf = C.create_string_buffer(need.value)
+    check(lib().sk_format_libsvm(m.ctypes.data_as(C.POINTER(C.c_double)), rows, cols, larr, buf,
+                                 need.value, C.byref(need)))
+    return buf.value.decode()
+
+
+class KernelMatrix:
+    """Mirror of KernelMatrix<double> (common/kernel_matrix.h:13-108)."""
+
+    def __init__(self, ctx: Optional[Context] = None):
+        self.ctx = ctx if ctx is not None else Context(0)
+        self.matrix = np.zeros((0, 0))
+        self.self_ = np.zeros(0)
+        self.label: List[str] = []
+
+    def calculate(self, train: Dataset, kernel: _Kernel, normalize: bool = False, n_th: int = 1):
+        """Train Gram (kernel_matrix.cpp:485-575).  n_th is accepted for API
+        parity; the GPU decides its own parallelism."""
+        self.matrix = self.ctx.gram(train, kernel, normalize)
+        self.label = [train.label(i) for i in range(len(train))]
+        return 0.0
+
+    def calculate_test(self, test: Dataset, train: Dataset, kernel: _Kernel, norm_test=False,
+                       normalize=False, n_th: int = 1):
+        """Test x train (kernel_matrix.cpp:699-754)."""
+        self.matrix, self.self_ = self.ctx.test_matrix(test, train, kernel, norm_test, normalize)
+        self.label = [test.label(i) for i in range(len(test))]
+        return 0.0
+
+    @staticmethod
+    def calculate_row(ctx: Context, data: Dataset, t: int, train: Dataset, kernel: _Kernel,
+                      sv_index=None, want_self=False):
+        """Test row (kernel_matrix.cpp:635-697)."""
+        return ctx.test_row(data, t, train, kernel, sv_index, want_self)
+
+    @staticmethod
+    def diagonal(ctx: Context, train: Dataset, kernel: _Kernel, sv_index=None):
+        """kernel_matrix.cpp:577-633."""
+        return ctx.diagonal(train, kernel, sv_index)
+
+    def __call__(self, i, j=None):
+        return self.self_[i] if j is None else self.matrix[i, j]
+
+    def print(self, out=sys.stdout):
+        """libsvm precomputed-kernel layout (kernel_matrix.cpp:756-770)."""
+        out.write(format_libsvm(self.matrix, self.label))
