@@ -42,3 +42,12 @@ clean:
 	$(MAKE) -C $(ROOT)oracle clean
 
 .PHONY: all lib oracle clean
+
+# diagnostic build with in-kernel phase stamps (never the shipped library)
+STAMPS_LIB := $(ROOT)build/libstem_kernel_amd_stamps.so
+stamps:
+	@mkdir -p $(BUILD)/stamps
+	$(HIPCC) $(HIPFLAGS) -DSK_STAMPS -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip -o $(BUILD)/stamps/dag_stem.o
+	$(HIPCC) $(CXXFLAGS) -DSK_STAMPS -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/stamps/sk_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o -Wl,-rpath,/opt/rocm/lib
+.PHONY: stamps

@@ -100,6 +100,12 @@ int sk_dataset_free(sk_dataset *ds);
 int sk_dataset_add(sk_dataset *ds, const char *label, int n_rows,
                    const char *const *rows, const double *const *bpp_rows,
                    float th, int use_bp);
+/* Append n single-sequence examples, folding each with sk_fold_synthetic and
+ * building its DAG on n_threads host threads (0 = hardware concurrency).
+ * labels may be NULL ("+1").  Parallel form of the reference's load loop
+ * (common/framework.h:308-353 + DataLoader<MData>::get). */
+int sk_dataset_add_synthetic(sk_dataset *ds, int32_t n, const char *const *seqs,
+                             const char *const *labels, float th, int32_t n_threads);
 int sk_dataset_size(const sk_dataset *ds);
 /* label of example i (pointer valid while ds lives) */
 const char *sk_dataset_label(const sk_dataset *ds, int i);

@@ -14,7 +14,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstem_kernel_amd.so")
+LIB_PATH = os.environ.get("SK_LIB_PATH") or os.path.join(_HERE, "libstem_kernel_amd.so")
 
 SK_OK = 0
 STATUS = {
@@ -52,6 +52,8 @@ SIGNATURES = {
     "sk_dataset_free": (C.c_int, [_P]),
     "sk_dataset_add": (C.c_int, [_P, C.c_char_p, C.c_int, C.POINTER(C.c_char_p),
                                  C.POINTER(_F64P), C.c_float, C.c_int]),
+    "sk_dataset_add_synthetic": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_char_p),
+                                           C.POINTER(C.c_char_p), C.c_float, C.c_int32]),
     "sk_dataset_size": (C.c_int, [_P]),
     "sk_dataset_label": (C.c_char_p, [_P, C.c_int]),
     "sk_dataset_shape": (C.c_int, [_P, C.c_int, _I32P, _I32P, _I32P, _I32P, _I32P]),

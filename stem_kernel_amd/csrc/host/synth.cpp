@@ -45,7 +45,11 @@ void fold_nussinov(const char* seq, int n, bool no_gu, double* out) {
   const int hp = 3;
   // Q(i,j) for 0<=i<=j<n; empty spans (j=i-1) are 1.
   auto at = [n](int i, int j) { return (size_t)i * n + j; };
-  std::vector<double> Q((size_t)n * n, 0.0), O((size_t)n * n, 0.0), B((size_t)n * n, 0.0);
+  // per-thread workspace: repeated folds reuse already-faulted pages
+  thread_local std::vector<double> Q, O, B, P;
+  Q.assign((size_t)n * n, 0.0);
+  O.assign((size_t)n * n, 0.0);
+  B.assign((size_t)n * n, 0.0);
   auto q = [&](int i, int j) -> double { return j < i ? 1.0 : Q[at(i, j)]; };
   for (int i = 0; i < n; ++i)
     for (int j = i + hp + 1; j < n; ++j) B[at(i, j)] = pair_weight(seq[i], seq[j], no_gu) * inv_s2;
@@ -62,7 +66,7 @@ void fold_nussinov(const char* seq, int n, bool no_gu, double* out) {
   }
   const double Z = Q[at(0, n - 1)];
   O[at(0, n - 1)] = 1.0;
-  std::vector<double> P((size_t)n * n, 0.0);
+  P.assign((size_t)n * n, 0.0);
   for (int d = n - 1; d >= 0; --d) {
     for (int i = 0; i + d < n; ++i) {
       int j = i + d;

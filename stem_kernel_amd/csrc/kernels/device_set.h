@@ -11,7 +11,6 @@
 
 namespace sk {
 
-constexpr uint32_t kLeafChild = 0xffffu;
 
 struct DevSet {
   int32_t n_examples = 0;
@@ -25,14 +24,16 @@ struct DevSet {
   const float* ex_nseqs = nullptr;        // ProfileSequence::n_seqs
   const int32_t* ex_len = nullptr;        // aligned length
   const int32_t* ex_pos_base = nullptr;   // into pos_* arrays
-  // per non-leaf node
-  const uint32_t* nd_a = nullptr;  // edge_beg_local:16 | n_edges:8 | n_bpf:8
+  // per non-leaf node (level order)
+  const uint32_t* nd_a = nullptr;  // edge_beg_local:16 | n_edges:8 | n_bpf:8  (non-leaf edges only)
   const uint32_t* nd_b = nullptr;  // len(last-first):16 | bpf_beg_local:16
+  const uint32_t* nd_c = nullptr;  // loop nodes: gaps of the leaf edge (else 0)
   const float* nd_w = nullptr;     // node weight (loop_profile(i)*loop_profile(j))
   const float* nd_nbp = nullptr;   // profile gap count at node.first
   const double* nd_P = nullptr;    // sum over roots of #paths root->node
-  // per edge of a non-leaf node (reference list order)
-  const uint32_t* ed = nullptr;  // child_local:16 (kLeafChild = leaf) | gaps:16
+  // non-leaf edges of stem nodes, node-major in reference list order; level
+  // order of nodes makes every level's edges one contiguous range
+  const uint2* ed = nullptr;  // {child_local | gaps<<16, parent_local}
   // per bp-frequency entry
   const uint32_t* bpf_code = nullptr;  // a*4+b
   const float* bpf_p = nullptr;
@@ -42,15 +43,30 @@ struct DevSet {
   const float4* pos_prof = nullptr;  // ProfileSequence columns A,C,G,U
   const float* pos_w = nullptr;      // fill_weight (empty -> string kernel unweighted)
   const int32_t* ex_has_w = nullptr;
+  // x-role schedule, in the reference's post-order (children first, a row's
+  // last parent soon after it).  Row r of example e is xr_*[ex_node_base[e]+r];
+  // its children are xr_ch[ex_xch_base[e] + sum of earlier rows' n_ch ...].
+  const int32_t* ex_nslots = nullptr;   // recycled HBM row slots this example needs
+  const int32_t* ex_xch_base = nullptr; // into xr_ch
+  const uint32_t* xr_a = nullptr;  // n_ch:8 | n_bpf:8 | loop leaf-edge gaps:16
+  const uint32_t* xr_b = nullptr;  // len:16 | out slot:16 (0xffff = row never read)
+  const uint32_t* xr_c = nullptr;  // bpf_beg_local:16 | code of first bp entry:8
+  const uint32_t* xr_node = nullptr;  // level-order node id (for nd_SL)
+  const float* xr_w = nullptr;
+  const float* xr_nbp = nullptr;
+  const float* xr_bp0 = nullptr;   // p of the first bp entry
+  const double* xr_P = nullptr;
+  const uint32_t* xr_ch = nullptr;  // per child edge: child slot:16 | gaps:16
   // maxima over the set
-  int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0;
+  int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
   int64_t total_nodes = 0;
 };
 
 // Per-call, parameter-dependent node values (computed on device by sk_prep).
 struct DevParamNodes {
-  double* nd_L = nullptr;   // G0 at (node, any y-leaf column)
-  double* nd_SL = nullptr;  // sum_e g^gaps(e) * L[child(e)]
+  double* nd_L = nullptr;   // G0 at (node, any y-leaf column), level order
+  double* nd_SL = nullptr;  // sum_e g^gaps(e) * L[child(e)], level order
+  double* xr_SL = nullptr;  // nd_SL in x-row (post-)order
 };
 
 }  // namespace sk

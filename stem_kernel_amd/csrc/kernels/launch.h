@@ -30,6 +30,7 @@ struct StemLaunch {
   int* item_counter = nullptr;
   double* scratch = nullptr;   // per-wave G0 slabs
   int64_t slab_doubles = 0;
+  unsigned long long* stamps = nullptr;  // diagnostic builds (SK_STAMPS) only
 };
 
 struct StrLaunch {
@@ -57,7 +58,8 @@ hipError_t launch_prep(const DevSet& s, const DevParamNodes& pn, const double* g
                        hipStream_t st);
 size_t stem_lds_bytes(const StemLaunch& P, int nwaves);
 hipError_t launch_stem(const StemLaunch& P, int grid, int nwaves, hipStream_t st);
-hipError_t stem_kernel_attr(int* max_dyn_lds);
+hipError_t stem_kernel_attr(int max_nl, int* max_dyn_lds, int* vgprs);
+int stem_maxk(int max_nl);
 
 size_t str_lds_bytes(const StrLaunch& P, int nwaves);
 hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st);

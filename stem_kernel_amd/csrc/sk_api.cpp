@@ -14,6 +14,8 @@
 #include <new>
 #include <numeric>
 #include <sstream>
+#include <thread>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -54,15 +56,20 @@ struct HostPack {
   std::vector<int32_t> ex_nl, ex_node_base, ex_edge_base, ex_bpf_base, ex_lvl_base, ex_nlev,
       ex_len, ex_pos_base, ex_has_w;
   std::vector<float> ex_nseqs;
-  std::vector<uint32_t> nd_a, nd_b;
+  std::vector<uint32_t> nd_a, nd_b, nd_c;
   std::vector<float> nd_w, nd_nbp;
   std::vector<double> nd_P;
-  std::vector<uint32_t> ed, bpf_code;
+  std::vector<uint2> ed;
+  std::vector<uint32_t> bpf_code;
   std::vector<float> bpf_p;
   std::vector<int32_t> lvl;
   std::vector<float4> pos_prof;
   std::vector<float> pos_w;
-  int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0;
+  std::vector<int32_t> ex_nslots, ex_xch_base;
+  std::vector<uint32_t> xr_a, xr_b, xr_c, xr_node, xr_ch;
+  std::vector<float> xr_w, xr_nbp, xr_bp0;
+  std::vector<double> xr_P;
+  int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
 };
 
 }  // namespace
@@ -165,25 +172,29 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       const int v = order[k];
       const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
       const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
+      const bool loop = level[v] == 0;  // single leaf child
       const uint32_t eloc = (uint32_t)P.ed.size() - ebase, bloc = (uint32_t)P.bpf_code.size() - bbase;
-      if (eloc > 0xffff || bloc > 0xffff || e1 - e0 > 0xff || b1 - b0 > 0xff ||
+      const uint32_t ne = loop ? 0u : e1 - e0;
+      if (eloc > 0xffff || bloc > 0xffff || ne > 0xff || b1 - b0 > 0xff ||
           X.last[v] - X.first[v] > 0xffff) {
         err = "example too large for the 16-bit packed DAG layout";
         return SK_ERR_UNSUPPORTED;
       }
-      P.nd_a.push_back(eloc | ((e1 - e0) << 16) | ((b1 - b0) << 24));
+      P.nd_a.push_back(eloc | (ne << 16) | ((b1 - b0) << 24));
       P.nd_b.push_back((X.last[v] - X.first[v]) | (bloc << 16));
+      P.nd_c.push_back(loop ? X.edge_gaps[e0] : 0u);
       P.nd_w.push_back(X.weight[v]);
       P.nd_nbp.push_back(X.prof5[(size_t)X.first[v] * 5 + 4]);
       P.nd_P.push_back(Pw[v]);
-      for (uint32_t t = e0; t < e1; ++t) {
-        const int c = nid[X.edge_to[t]];
-        const uint32_t child = c < 0 ? sk::kLeafChild : (uint32_t)c;
-        if (X.edge_gaps[t] > 0xffff) {
-          err = "gap count exceeds 16 bits";
-          return SK_ERR_UNSUPPORTED;
+      if (!loop) {
+        for (uint32_t t = e0; t < e1; ++t) {
+          const int c = nid[X.edge_to[t]];
+          if (c < 0 || X.edge_gaps[t] > 0xffff) {
+            err = c < 0 ? "unexpected DAG shape: stem with a leaf child" : "gap count exceeds 16 bits";
+            return SK_ERR_UNSUPPORTED;
+          }
+          P.ed.push_back(make_uint2((uint32_t)c | (X.edge_gaps[t] << 16), (uint32_t)k));
         }
-        P.ed.push_back(child | (X.edge_gaps[t] << 16));
       }
       for (uint32_t t = b0; t < b1; ++t) {
         P.bpf_code.push_back(X.bpf_code[t]);
@@ -195,6 +206,65 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     for (int l = 0; l < nlev; ++l) lv[l + 1] += lv[l];
     P.lvl.insert(P.lvl.end(), lv.begin(), lv.end());
 
+    // x-role schedule: rows in reference (post-)order; a row's HBM slot is
+    // recycled once its last parent has been produced (LIFO free list keeps
+    // hot addresses hot).  Rows nobody reads (roots) get no slot.
+    {
+      std::vector<int> last_parent(nn, -1);
+      for (int v = 0; v < nn; ++v)
+        for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k)
+          last_parent[X.edge_to[k]] = std::max(last_parent[X.edge_to[k]], v);
+      std::vector<uint32_t> slot(nn, 0xffff);
+      std::vector<int> free_list;
+      int nslots = 0;
+      P.ex_xch_base.push_back((int32_t)P.xr_ch.size());
+      for (int v = 0; v < nn; ++v) {
+        if (level[v] < 0) continue;
+        const bool loop = level[v] == 0;
+        const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
+        const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
+        uint32_t nch = 0;
+        if (!loop) {
+          for (uint32_t k = e0; k < e1; ++k) {
+            const int c = X.edge_to[k];
+            P.xr_ch.push_back(slot[c] | (X.edge_gaps[k] << 16));
+            ++nch;
+          }
+        }
+        for (uint32_t k = e0; k < e1; ++k) {
+          const int c = X.edge_to[k];
+          if (level[c] >= 0 && last_parent[c] == v && slot[c] != 0xffff) free_list.push_back(slot[c]);
+        }
+        if (last_parent[v] >= 0) {
+          int sl;
+          if (!free_list.empty()) {
+            sl = free_list.back();
+            free_list.pop_back();
+          } else {
+            sl = nslots++;
+          }
+          slot[v] = (uint32_t)sl;
+        }
+        const uint32_t bloc = (uint32_t)nid[v];  // placeholder, fixed below
+        (void)bloc;
+        P.xr_a.push_back(nch | ((b1 - b0) << 8) | ((loop ? X.edge_gaps[e0] : 0u) << 16));
+        P.xr_b.push_back((X.last[v] - X.first[v]) | (slot[v] << 16));
+        P.xr_node.push_back((uint32_t)nid[v]);
+        P.xr_w.push_back(X.weight[v]);
+        P.xr_nbp.push_back(X.prof5[(size_t)X.first[v] * 5 + 4]);
+        P.xr_bp0.push_back(b1 > b0 ? X.bpf_p[b0] : 0.0f);
+        P.xr_P.push_back(Pw[v]);
+        // bpf_beg in the level-order bpf array of this example (see nd_b)
+        P.xr_c.push_back((P.nd_b[P.ex_node_base.back() + nid[v]] >> 16) |
+                         ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16));
+      }
+      if (nslots >= 0xffff) {
+        err = "too many live DAG rows";
+        return SK_ERR_UNSUPPORTED;
+      }
+      P.ex_nslots.push_back(nslots);
+      P.max_slots = std::max(P.max_slots, nslots);
+    }
     P.ex_nl.push_back(nl);
     P.ex_nlev.push_back(nlev);
     P.ex_nseqs.push_back(X.n_seqs);
@@ -342,26 +412,30 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     // LDS need and wave count
     SL.lds_max_nl = std::max(PY.max_nl, 1);
     SL.lds_max_nl = (SL.lds_max_nl + 1) & ~1;
-    SL.lds_max_edges = (std::max(PY.max_edges, 1) + 3) & ~3;
+    SL.lds_max_edges = (std::max(PY.max_edges, 1) + 1) & ~1;
+    SL.lds_max_nl = (SL.lds_max_nl + 3) & ~3;
     SL.lds_max_bpf = (std::max(PY.max_bpf, 1) + 3) & ~3;
     SL.lds_max_nlev_pad = (PY.max_nlev + 1 + 3) & ~3;
     SL.n_gpow = max_len + 2;
     SL.n_gpow_pad = (SL.n_gpow + 1) & ~1;
-    int max_dyn = 0;
-    SK_HIP(ctx, sk::stem_kernel_attr(&max_dyn));
-    int best = 0;
-    for (int w = 16; w >= 1; --w) {
+    if (sk::stem_maxk(SL.lds_max_nl) < 0)
+      return fail(ctx, SK_ERR_UNSUPPORTED, "y example has more than 2048 non-leaf DAG nodes");
+    int max_dyn = 0, vgprs = 0;
+    SK_HIP(ctx, sk::stem_kernel_attr(SL.lds_max_nl, &max_dyn, &vgprs));
+    const int valloc = ((std::max(vgprs, 1) + 7) / 8) * 8;
+    const int waves_cu_vgpr = 4 * std::min(8, 512 / valloc);
+    int best = 0, per_cu = 1;
+    for (int w = 8; w >= 1; --w) {  // __launch_bounds__(512)
       const size_t lds = sk::stem_lds_bytes(SL, w);
       if (lds > (size_t)max_dyn) continue;
-      const int per_cu = std::min<int>((int)(163840 / lds), 32 / w);
-      if (per_cu * w > best) {
-        best = per_cu * w;
+      const int pc = std::min<int>((int)(163840 / lds), std::min(32, waves_cu_vgpr) / w);
+      if (pc * w > best) {
+        best = pc * w;
         nwaves = w;
+        per_cu = pc;
       }
     }
     if (best == 0) return fail(ctx, SK_ERR_UNSUPPORTED, "y example too large for LDS");
-    const int per_cu = std::max(1, std::min<int>((int)(163840 / sk::stem_lds_bytes(SL, nwaves)),
-                                                 32 / nwaves));
     grid = ctx->n_cu * per_cu;
     const int chunk = 2 * nwaves;
     struct It {
@@ -396,7 +470,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   const size_t nb = (size_t)n;
   size_t need = 0;
   need += 256 * 8 + 16 * 8 + (size_t)(max_len + 4) * 8 * 2;
-  need += (size_t)PX.nd_a.size() * 8 * 2 + 1024;  // L, SL
+  need += (size_t)PX.nd_a.size() * 8 * 3 + 1024;  // L, SL, xr_SL
   need += items.size() * sizeof(int4) + nb * (4 + 8) + nb * 8 * 2 + nb * 4 * 2 + 64 + 8 * 256;
   need += 16 * 256;
   rc = ensure_work(ctx, need);
@@ -408,6 +482,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   double* d_gp_str = A.take<double>(max_len + 4);
   double* d_L = A.take<double>(std::max<size_t>(PX.nd_a.size(), 1));
   double* d_SL = A.take<double>(std::max<size_t>(PX.nd_a.size(), 1));
+  double* d_xSL = A.take<double>(std::max<size_t>(PX.nd_a.size(), 1));
   int4* d_items = A.take<int4>(std::max<size_t>(items.size(), 1));
   int32_t* d_ixs = A.take<int32_t>(std::max<size_t>(nb, 1));
   int64_t* d_oidx = A.take<int64_t>(std::max<size_t>(nb, 1));
@@ -443,7 +518,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
                                hipMemcpyHostToDevice, S));
     SK_HIP(ctx, hipMemcpyAsync(d_ixs, ixs.data(), nb * 4, hipMemcpyHostToDevice, S));
     SK_HIP(ctx, hipMemcpyAsync(d_oidx, ioidx.data(), nb * 8, hipMemcpyHostToDevice, S));
-    sk::DevParamNodes pn{d_L, d_SL};
+    sk::DevParamNodes pn{d_L, d_SL, d_xSL};
     const double gap2 = kp->loop_gap * kp->loop_gap;
     SK_HIP(ctx, sk::launch_prep(xs_->dev, pn, d_gp_loop, gap2, S));
     SL.xset = xs_->dev;
@@ -459,15 +534,35 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     SL.oidx = d_oidx;
     SL.out = stem_out;
     SL.item_counter = d_ctr;
-    SL.slab_doubles = (int64_t)std::max(PX.max_nl, 1) * std::max(PY.max_nl, 1);
+    SL.slab_doubles = (int64_t)std::max(PX.max_slots, 1) * std::max(PY.max_nl, 1);
     SL.slab_doubles = (SL.slab_doubles + 31) & ~int64_t(31);
     grid = std::min<int64_t>(grid, std::max<int64_t>(1, (int64_t)items.size()));
     rc = ensure_scratch(ctx, (size_t)grid * nwaves * SL.slab_doubles * sizeof(double));
     if (rc) return rc;
     SL.scratch = ctx->scratch;
+#ifdef SK_STAMPS
+    unsigned long long* d_stamps = nullptr;
+    SK_HIP(ctx, hipMalloc(&d_stamps, 8 * sizeof(unsigned long long)));
+    SK_HIP(ctx, hipMemsetAsync(d_stamps, 0, 8 * sizeof(unsigned long long), S));
+    SL.stamps = d_stamps;
+#endif
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     SK_HIP(ctx, sk::launch_stem(SL, grid, nwaves, S));
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
+#ifdef SK_STAMPS
+    {
+      unsigned long long h[8];
+      SK_HIP(ctx, hipMemcpyAsync(h, d_stamps, sizeof(h), hipMemcpyDeviceToHost, S));
+      SK_HIP(ctx, hipStreamSynchronize(S));
+      (void)hipFree(d_stamps);
+      const double rows = (double)h[6];
+      std::fprintf(stderr, "[stamps] grid=%d waves/wg=%d pairs=%llu rows=%.0f cycles/row:", grid,
+                   nwaves, h[7], rows);
+      const char* nm[6] = {"hdr", "load", "gather", "match", "sweep", "store"};
+      for (int i = 0; i < 6; ++i) std::fprintf(stderr, " %s=%.0f", nm[i], h[i] / rows);
+      std::fprintf(stderr, "\n");
+    }
+#endif
     ctx->last_launches = 1;
   }
   if (str) {
@@ -630,6 +725,52 @@ int sk_dataset_add(sk_dataset* ds, const char* label, int n_rows, const char* co
   return SK_OK;
 }
 
+int sk_dataset_add_synthetic(sk_dataset* ds, int32_t n, const char* const* seqs,
+                             const char* const* labels, float th, int32_t n_threads) {
+  if (!ds || n < 0 || (n > 0 && !seqs)) return SK_ERR_INVALID;
+  if (ds->uploaded) return SK_ERR_INVALID;
+  const size_t base = ds->ex.size();
+  try {
+    ds->ex.resize(base + n);
+    for (int32_t i = 0; i < n; ++i) ds->labels.emplace_back(labels && labels[i] ? labels[i] : "+1");
+  } catch (const std::bad_alloc&) {
+    return SK_ERR_ALLOC;
+  }
+  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  nt = std::max(1, std::min(nt, std::max<int32_t>(n, 1)));
+  std::atomic<int32_t> next(0), status(SK_OK);
+  auto work = [&]() {
+    std::vector<double> bpp;
+    for (;;) {
+      const int32_t i = next.fetch_add(1);
+      if (i >= n || status.load() != SK_OK) return;
+      try {
+        const char* s = seqs[i];
+        const int L = (int)std::strlen(s);
+        // fold the gap-erased, lower-cased row (common/bpmatrix.cpp:404-414)
+        std::string row;
+        for (int k = 0; k < L; ++k)
+          if (s[k] != '-') row.push_back((char)std::tolower((unsigned char)s[k]));
+        bpp.assign(row.size() > 1 ? row.size() * (row.size() - 1) / 2 : 1, 0.0);
+        sk::fold_nussinov(row.c_str(), (int)row.size(), false, bpp.data());
+        const double* b = bpp.data();
+        sk::build_example(ds->ex[base + i], 1, &s, &b, th, true);
+      } catch (...) {
+        status.store(SK_ERR_INVALID);
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  if (status.load() != SK_OK) {
+    ds->ex.resize(base);
+    ds->labels.resize(base);
+  }
+  return status.load();
+}
+
 int sk_dataset_size(const sk_dataset* ds) { return ds ? (int)ds->ex.size() : 0; }
 
 const char* sk_dataset_label(const sk_dataset* ds, int i) {
@@ -683,6 +824,7 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   if (rc) return fail(ctx, rc, err);
   SK_HIP(ctx, hipSetDevice(ctx->device));
   HostPack& P = ds->pack;
+  P.xr_ch.insert(P.xr_ch.end(), 8, 0u);  // the kernel prefetches 4 records past a row
   DevSet& D = ds->dev;
   DeviceBuffers& B = ds->buf;
   D.n_examples = (int32_t)ds->ex.size();
@@ -698,6 +840,7 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.ex_has_w, &D.ex_has_w));
   SK_HIP(ctx, upload(B, P.nd_a, &D.nd_a));
   SK_HIP(ctx, upload(B, P.nd_b, &D.nd_b));
+  SK_HIP(ctx, upload(B, P.nd_c, &D.nd_c));
   SK_HIP(ctx, upload(B, P.nd_w, &D.nd_w));
   SK_HIP(ctx, upload(B, P.nd_nbp, &D.nd_nbp));
   SK_HIP(ctx, upload(B, P.nd_P, &D.nd_P));
@@ -707,11 +850,23 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.lvl, &D.lvl));
   SK_HIP(ctx, upload(B, P.pos_prof, &D.pos_prof));
   SK_HIP(ctx, upload(B, P.pos_w, &D.pos_w));
+  SK_HIP(ctx, upload(B, P.ex_nslots, &D.ex_nslots));
+  SK_HIP(ctx, upload(B, P.ex_xch_base, &D.ex_xch_base));
+  SK_HIP(ctx, upload(B, P.xr_a, &D.xr_a));
+  SK_HIP(ctx, upload(B, P.xr_b, &D.xr_b));
+  SK_HIP(ctx, upload(B, P.xr_c, &D.xr_c));
+  SK_HIP(ctx, upload(B, P.xr_node, &D.xr_node));
+  SK_HIP(ctx, upload(B, P.xr_w, &D.xr_w));
+  SK_HIP(ctx, upload(B, P.xr_nbp, &D.xr_nbp));
+  SK_HIP(ctx, upload(B, P.xr_bp0, &D.xr_bp0));
+  SK_HIP(ctx, upload(B, P.xr_P, &D.xr_P));
+  SK_HIP(ctx, upload(B, P.xr_ch, &D.xr_ch));
   D.max_nl = P.max_nl;
   D.max_edges = P.max_edges;
   D.max_bpf = P.max_bpf;
   D.max_nlev = P.max_nlev;
   D.max_len = P.max_len;
+  D.max_slots = P.max_slots;
   D.total_nodes = (int64_t)P.nd_a.size();
   ds->device = ctx->device;
   ds->uploaded = true;

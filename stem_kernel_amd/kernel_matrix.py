@@ -190,6 +190,17 @@ class Dataset:
             ds.add(labels[k], [s], None if bpp is None else [bpp[k]], th=th)
         return ds
 
+    @classmethod
+    def synthetic(cls, seqs: Sequence[str], labels: Optional[Sequence[str]] = None,
+                  th: float = 0.01, threads: int = 0):
+        """Fold (synthetic model) and build all examples on host threads."""
+        ds = cls()
+        n = len(seqs)
+        sarr = (C.c_char_p * n)(*[s.encode() for s in seqs])
+        larr = None if labels is None else (C.c_char_p * n)(*[l.encode() for l in labels])
+        check(lib().sk_dataset_add_synthetic(ds._h, n, sarr, larr, C.c_float(th), threads))
+        return ds
+
     def __len__(self):
         return lib().sk_dataset_size(self._h)
 
