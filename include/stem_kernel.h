@@ -50,7 +50,9 @@ typedef enum {
   SK_SU_STEM_STR = 4,  /* SuStemStrKernel == StemStrKernel (ss_kernel.h)  default   */
   SK_SI_STEM_STR = 5,  /* SiStemStrKernel                                --no-ribosum */
   SK_LSU_STEM = 6,     /* LSuStemKernel: beta*log(K_stem)                --log --no-string */
-  SK_LSU_STEM_STR = 7  /* LSuStemStrKernel: beta*log K_stem + alpha*log K_str  --log */
+  SK_LSU_STEM_STR = 7, /* LSuStemStrKernel: beta*log K_stem + alpha*log K_str  --log */
+  SK_NAIVE_STR = 8     /* StringKernel<double>(gap) of string_kernel/ (exact character
+                          match of row 0, weight gap^2, string_kernel.cpp:11-50) */
 } sk_kernel_kind;
 
 /* Kernel parameters; defaults are stem_kernel_lite/main.cpp:103-149
@@ -121,6 +123,10 @@ int sk_dataset_dag(const sk_dataset *ds, int i, uint32_t *first, uint32_t *last,
                    uint32_t *max_pa, uint32_t *edge_to, uint32_t *edge_gaps,
                    uint32_t *bp_code, float *bp_p, uint32_t *roots,
                    float *pos_weight);
+
+/* ProfileSequence of example i (common/profile.cpp): prof5 gets len*5 floats
+ * (A,C,G,U,gap), *n_seqs the row count. */
+int sk_dataset_profile(const sk_dataset *ds, int i, float *prof5, float *n_seqs);
 
 /* Upload the packed example set to the context's device (idempotent).
  * Must be called after the last sk_dataset_add and before any compute. */

@@ -162,6 +162,8 @@ def kernel_value(kind: int, x: OMData, y: OMData, p) -> float:
         return si_stem(x, y, p.loop_gap, p.stack, p.covar, p.len_band) + si_str(x, y, p.gap, p.match, p.mismatch)
     if kind == 6:
         return p.beta * math.log(stem()) + 0.0
+    if kind == 8:
+        raise ValueError("naive string kernel compares raw strings: use naive_string()")
     if kind == 7:
         return (p.beta * math.log(stem()) + 0.0) + (p.alpha * math.log(su_str(x, y, p.gap, p.alpha)) + 0.0)
     raise ValueError(kind)

@@ -23,7 +23,7 @@ STATUS = {
 }
 
 # sk_kernel_kind
-SU_STEM, SI_STEM, SU_STR, SI_STR, SU_STEM_STR, SI_STEM_STR, LSU_STEM, LSU_STEM_STR = range(8)
+SU_STEM, SI_STEM, SU_STR, SI_STR, SU_STEM_STR, SI_STEM_STR, LSU_STEM, LSU_STEM_STR, NAIVE_STR = range(9)
 
 
 class KernelParams(C.Structure):
@@ -59,6 +59,7 @@ SIGNATURES = {
     "sk_dataset_shape": (C.c_int, [_P, C.c_int, _I32P, _I32P, _I32P, _I32P, _I32P]),
     "sk_dataset_dag": (C.c_int, [_P, C.c_int, _U32P, _U32P, _U32P, _U32P, _F32P, _U32P,
                                  _U32P, _U32P, _U32P, _F32P, _U32P, _F32P]),
+    "sk_dataset_profile": (C.c_int, [_P, C.c_int, _F32P, _F32P]),
     "sk_dataset_upload": (C.c_int, [_P, _P]),
     "sk_gram": (C.c_int, [_P, _P, C.POINTER(KernelParams), C.c_int, _F64P]),
     "sk_pairs_device": (C.c_int, [_P, _P, C.POINTER(KernelParams), _I32P, _I32P, C.c_int64,

@@ -43,6 +43,7 @@ struct DevSet {
   const float4* pos_prof = nullptr;  // ProfileSequence columns A,C,G,U
   const float* pos_w = nullptr;      // fill_weight (empty -> string kernel unweighted)
   const int32_t* ex_has_w = nullptr;
+  const uint8_t* pos_chr = nullptr;  // raw characters of row 0 (naive string kernel)
   // x-role schedule, in the reference's post-order (children first, a row's
   // last parent soon after it).  Row r of example e is xr_*[ex_node_base[e]+r];
   // its children are xr_ch[ex_xch_base[e] + sum of earlier rows' n_ch ...].

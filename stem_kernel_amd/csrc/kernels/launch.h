@@ -38,6 +38,7 @@ struct StrLaunch {
   const double* st = nullptr;    // 16: exp(alpha*ribosum_s) or match/mismatch
   const double* gpow = nullptr;  // gap^k, k <= max_len
   double gap = 0.0;
+  int32_t naive = 0;  // StringKernel<double> of string_kernel/: exact char match, g^2, no weights
   const int32_t* xs = nullptr;
   const int32_t* ys = nullptr;
   int64_t n_pairs = 0;

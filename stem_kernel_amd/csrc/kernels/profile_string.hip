@@ -76,12 +76,14 @@ __global__ void __launch_bounds__(256) sk_profile_string_kernel(StrLaunch P) {
     const int x = P.xs[pr], y = P.ys[pr];
     const int Lx = sx.ex_len[x], Ly = sy.ex_len[y];
     const int xpb = sx.ex_pos_base[x], ypb = sy.ex_pos_base[y];
-    const bool use_w = sx.ex_has_w[x] && sy.ex_has_w[y];
+    const bool naive = P.naive != 0;
+    const bool use_w = !naive && sx.ex_has_w[x] && sy.ex_has_w[y];
     for (int j = lane; j < Ly; j += 64) {
       const float4 c = sy.pos_prof[ypb + j];
       yprof[j] = c;
       ywt[j] = use_w ? sy.pos_w[ypb + j] : 1.0f;
-      ycode[j] = onehot_code(c);
+      // naive kernel: the raw character (codes >= 16 never meet the profile path)
+      ycode[j] = naive ? 16 + (int)sy.pos_chr[ypb + j] : onehot_code(c);
     }
     // row 0: K0[0][j] = 1, G0[0][j] = G0[0][j-1]*gap
     for (int j = lane; j <= Ly; j += 64) {
@@ -103,7 +105,7 @@ __global__ void __launch_bounds__(256) sk_profile_string_kernel(StrLaunch P) {
       if (row_ok) {
         xc = sx.pos_prof[xpb + i - 1];
         xw = use_w ? sx.pos_w[xpb + i - 1] : 1.0f;
-        xcode = onehot_code(xc);
+        xcode = naive ? 16 + (int)sx.pos_chr[xpb + i - 1] : onehot_code(xc);
       }
       const double g0col = row_ok ? P.gpow[i] : 0.0;  // G0[i][0] = G0[i-1][0]*gap
       // outputs of steps t-1 (myK0, myG0) and t-2 (myG0p).  Lane l reaches
@@ -129,7 +131,12 @@ __global__ void __launch_bounds__(256) sk_profile_string_kernel(StrLaunch P) {
         } else if (j >= 1 && j <= Ly && row_ok) {
           double v = use_w ? dG * (double)xw * (double)ywt[j - 1] : dG;
           const int yc = ycode[j - 1];
-          v *= (xcode >= 0 && yc >= 0) ? st[xcode * 4 + yc] : prof_subst(st, xc, yprof[j - 1]);
+          if (naive) {
+            // string_kernel.cpp:41-44: K1/G1 += G0[i-1][j-1]*g2 on x[i-1]==y[j-1]
+            v = (xcode == yc) ? dG * (gap * gap) : 0.0;
+          } else {
+            v *= (xcode >= 0 && yc >= 0) ? st[xcode * 4 + yc] : prof_subst(st, xc, yprof[j - 1]);
+          }
           const double K1 = v + K1p;
           const double G1 = v + G1p * gap;
           nK0 = K1 + upK;

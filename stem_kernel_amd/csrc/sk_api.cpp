@@ -65,6 +65,7 @@ struct HostPack {
   std::vector<int32_t> lvl;
   std::vector<float4> pos_prof;
   std::vector<float> pos_w;
+  std::vector<uint8_t> pos_chr;
   std::vector<int32_t> ex_nslots, ex_xch_base;
   std::vector<uint32_t> xr_a, xr_b, xr_c, xr_node, xr_ch;
   std::vector<float> xr_w, xr_nbp, xr_bp0;
@@ -274,6 +275,7 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       const float* c = &X.prof5[(size_t)i * 5];
       P.pos_prof.push_back(make_float4(c[0], c[1], c[2], c[3]));
       P.pos_w.push_back(X.has_bp ? X.pos_weight[i] : 1.0f);
+      P.pos_chr.push_back((uint8_t)X.rows[0][i]);
     }
     P.ex_node_base.push_back((int32_t)P.nd_a.size());
     P.ex_edge_base.push_back((int32_t)P.ed.size());
@@ -290,10 +292,10 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
 }
 
 // ------------------------------------------------------------ parameters
-bool kind_has_stem(int k) { return k != SK_SU_STR && k != SK_SI_STR; }
+bool kind_has_stem(int k) { return k != SK_SU_STR && k != SK_SI_STR && k != SK_NAIVE_STR; }
 bool kind_has_str(int k) {
   return k == SK_SU_STR || k == SK_SI_STR || k == SK_SU_STEM_STR || k == SK_SI_STEM_STR ||
-         k == SK_LSU_STEM_STR;
+         k == SK_LSU_STEM_STR || k == SK_NAIVE_STR;
 }
 bool kind_subst(int k) {  // RIBOSUM (Su*) vs match/mismatch (Si*)
   return k == SK_SU_STEM || k == SK_SU_STR || k == SK_SU_STEM_STR || k == SK_LSU_STEM ||
@@ -304,7 +306,8 @@ int32_t combine_mode(int k) {
     case SK_SU_STEM:
     case SK_SI_STEM: return sk::kCombineStem;
     case SK_SU_STR:
-    case SK_SI_STR: return sk::kCombineStr;
+    case SK_SI_STR:
+    case SK_NAIVE_STR: return sk::kCombineStr;
     case SK_SU_STEM_STR:
     case SK_SI_STEM_STR: return sk::kCombineAdd;
     case SK_LSU_STEM: return sk::kCombineLogStem;
@@ -378,7 +381,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   rc = check_set(ctx, ys_);
   if (rc) return rc;
   if (n < 0) return fail(ctx, SK_ERR_INVALID, "negative pair count");
-  if (kp->kind < SK_SU_STEM || kp->kind > SK_LSU_STEM_STR)
+  if (kp->kind < SK_SU_STEM || kp->kind > SK_NAIVE_STR)
     return fail(ctx, SK_ERR_UNSUPPORTED, "unknown kernel kind");
   ctx->last_stem_ms = ctx->last_str_ms = ctx->last_cells = 0.0;
   ctx->last_launches = 0;
@@ -574,6 +577,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     T.st = d_st;
     T.gpow = d_gp_str;
     T.gap = kp->gap;
+    T.naive = kp->kind == SK_NAIVE_STR ? 1 : 0;
     T.xs = d_px;
     T.ys = d_py;
     T.n_pairs = n;
@@ -816,6 +820,15 @@ int sk_dataset_dag(const sk_dataset* ds, int i, uint32_t* first, uint32_t* last,
   return SK_OK;
 }
 
+int sk_dataset_profile(const sk_dataset* ds, int i, float* prof5, float* n_seqs) {
+  if (!ds) return SK_ERR_INVALID;
+  if (i < 0 || i >= (int)ds->ex.size()) return SK_ERR_RANGE;
+  const Example& X = ds->ex[i];
+  if (prof5) std::copy(X.prof5.begin(), X.prof5.end(), prof5);
+  if (n_seqs) *n_seqs = X.n_seqs;
+  return SK_OK;
+}
+
 int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   if (!ctx || !ds) return SK_ERR_INVALID;
   if (ds->uploaded) return ds->device == ctx->device ? SK_OK : fail(ctx, SK_ERR_INVALID, "dataset bound to another device");
@@ -850,6 +863,7 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.lvl, &D.lvl));
   SK_HIP(ctx, upload(B, P.pos_prof, &D.pos_prof));
   SK_HIP(ctx, upload(B, P.pos_w, &D.pos_w));
+  SK_HIP(ctx, upload(B, P.pos_chr, &D.pos_chr));
   SK_HIP(ctx, upload(B, P.ex_nslots, &D.ex_nslots));
   SK_HIP(ctx, upload(B, P.ex_xch_base, &D.ex_xch_base));
   SK_HIP(ctx, upload(B, P.xr_a, &D.xr_a));

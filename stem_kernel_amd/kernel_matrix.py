@@ -30,7 +30,8 @@ from ._lib import KernelParams, StemKernelError, check, lib
 __all__ = [
     "fold", "random_sequences", "Dataset", "Context", "KernelMatrix",
     "SuStemKernel", "SiStemKernel", "StringKernel", "SuStemStrKernel", "StemStrKernel",
-    "SiStemStrKernel", "LSuStemKernel", "LSuStemStrKernel", "StemKernelError",
+    "SiStemStrKernel", "LSuStemKernel", "LSuStemStrKernel", "NaiveStringKernel",
+    "StemKernelError",
 ]
 
 
@@ -107,6 +108,15 @@ class SuStemStrKernel(_Kernel):
 
 
 StemStrKernel = SuStemStrKernel
+
+
+class NaiveStringKernel(_Kernel):
+    """StringKernel<double>(gap) of string_kernel/ (string_kernel.cpp:11-50):
+    exact character match of the first row, weight gap^2, no profiles."""
+    kind = _lib.NAIVE_STR
+
+    def __init__(self, gap=0.8):
+        super().__init__(gap=gap)
 
 
 class SiStemStrKernel(_Kernel):
@@ -203,6 +213,15 @@ class Dataset:
 
     def __len__(self):
         return lib().sk_dataset_size(self._h)
+
+    def profile(self, i: int):
+        """ProfileSequence columns [len][5] and n_seqs of example i."""
+        L = self.shape(i)[4]
+        out = np.zeros((max(L, 1), 5), np.float32)
+        ns = C.c_float()
+        check(lib().sk_dataset_profile(self._h, i, out.ctypes.data_as(C.POINTER(C.c_float)),
+                                       C.byref(ns)))
+        return out[:L], ns.value
 
     def label(self, i: int) -> str:
         return lib().sk_dataset_label(self._h, i).decode()

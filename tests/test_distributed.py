@@ -1,0 +1,80 @@
+"""Multi-process path on CPU: world_size-2 gloo over 127.0.0.1.
+
+The shard plan must cover the upper triangle exactly once, and the gathered,
+mirrored, normalised Gram must equal the single-process one (the compute
+function is the oracle here; on GPUs it is stem_kernel_amd.shard.gpu_compute).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from stem_kernel_amd import shard
+
+
+@pytest.mark.parametrize("n,world", [(1, 2), (7, 2), (10, 3), (33, 4), (64, 8)])
+def test_plan_covers_triangle_once(n, world):
+    seen = np.zeros((n, n), int)
+    for r in range(world):
+        x, y = shard.rank_pairs(n, world, r)
+        assert np.all(x <= y)
+        np.add.at(seen, (x, y), 1)
+    assert np.array_equal(seen, np.triu(np.ones((n, n), int)))
+    sizes = [shard.rank_pairs(n, world, r)[0].size for r in range(world)]
+    if n >= 8 * world:
+        assert max(sizes) / min(sizes) < 1.35  # folding balances the triangle
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import stem_kernel_amd as ska
+    from oracle import pyoracle as po
+    seqs = ska.random_sequences(7, 50, 0x5EED0004)
+    om = [po.OMData([s], [ska.fold(s)], 0.01) for s in seqs]
+    p = ska.SuStemStrKernel().params
+
+    def compute(x, y):
+        return np.array([po.kernel_value(p.kind, om[a], om[b], p) for a, b in zip(x, y)])
+
+    g = shard.distributed_gram(compute, len(seqs), normalize=True)
+    dist.destroy_process_group()
+    q.put((rank, g))
+
+
+def test_gloo_world2_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    import stem_kernel_amd as ska
+    from oracle import pyoracle as po
+    seqs = ska.random_sequences(7, 50, 0x5EED0004)
+    om = [po.OMData([s], [ska.fold(s)], 0.01) for s in seqs]
+    p = ska.SuStemStrKernel().params
+    n = len(seqs)
+    raw = np.zeros((n, n))
+    for i in range(n):
+        for j in range(i, n):
+            raw[i, j] = raw[j, i] = po.kernel_value(p.kind, om[i], om[j], p)
+    ref = shard.assemble([raw[np.triu_indices(n)]], n, 1, normalize=True)
+    assert np.array_equal(res[0], res[1])
+    assert np.array_equal(res[0], ref)
