@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--slices", type=int, default=64)
     ap.add_argument("--full", action="store_true", help="time every slice (whole Gram)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-pairs", type=int, default=1024, help="pairs in the CPU sample")
+    ap.add_argument("--cpu-pairs", type=int, default=12288, help="pairs in the CPU sample (~15 s on 16 cores)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "stem_traffic.json"))
     return ap.parse_args()
 

@@ -78,3 +78,26 @@ def test_gloo_world2_matches_single_process():
     ref = shard.assemble([raw[np.triu_indices(n)]], n, 1, normalize=True)
     assert np.array_equal(res[0], res[1])
     assert np.array_equal(res[0], ref)
+
+
+@pytest.mark.gpu
+def test_rccl_world1_gpu_compute_matches_gram(gpu_ctx):
+    """The RCCL path (nccl backend, one rank) through the HIP engine writing
+    straight into the device buffer that is all-gathered."""
+    import torch
+    import torch.distributed as dist
+    import stem_kernel_amd as ska
+
+    seqs = ska.random_sequences(9, 70, 0x5EED0005)
+    ds = ska.Dataset.synthetic(seqs, th=0.01, threads=4)
+    kern = ska.SuStemStrKernel()
+    ref = gpu_ctx.gram(ds, kern, normalize=True)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1)
+    try:
+        g = shard.distributed_gram(shard.gpu_compute(gpu_ctx, ds, kern, dev), len(seqs),
+                                   normalize=True)
+    finally:
+        dist.destroy_process_group()
+    np.testing.assert_allclose(g, ref, rtol=1e-12)
