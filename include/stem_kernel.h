@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 1
+#define SK_ABI_VERSION 2
 
 typedef enum {
   SK_OK = 0,
@@ -51,12 +51,19 @@ typedef enum {
   SK_SI_STEM_STR = 5,  /* SiStemStrKernel                                --no-ribosum */
   SK_LSU_STEM = 6,     /* LSuStemKernel: beta*log(K_stem)                --log --no-string */
   SK_LSU_STEM_STR = 7, /* LSuStemStrKernel: beta*log K_stem + alpha*log K_str  --log */
-  SK_NAIVE_STR = 8     /* StringKernel<double>(gap) of string_kernel/ (exact character
+  SK_NAIVE_STR = 8,    /* StringKernel<double>(gap) of string_kernel/ (exact character
                           match of row 0, weight gap^2, string_kernel.cpp:11-50) */
+  /* BPLAKernel<double,MData> of bpla_kernel/ (bpla_kernel.cpp:159-174) */
+  SK_BPLA = 9,         /* local_alignment_exp with BPLAScore            (default)    */
+  SK_LA = 10,          /* local_alignment_exp with LAScore               --noBP      */
+  SK_BPLA_SW = 11,     /* local_alignment_max with BPLAScore             --SW        */
+  SK_LA_SW = 12        /* local_alignment_max with LAScore               --noBP --SW */
 } sk_kernel_kind;
 
 /* Kernel parameters; defaults are stem_kernel_lite/main.cpp:103-149
- * (sk_kernel_params_default). */
+ * (sk_kernel_params_default).  BPLA kinds use alpha, beta, gap, ext and
+ * score_table with the defaults of bpla_kernel/main.cpp:20-26, 68-76; that
+ * CLI parses them as float, so the defaults are float-rounded. */
 typedef struct {
   int32_t kind;       /* sk_kernel_kind */
   uint32_t len_band;  /* --length-band (0 = off), default 10 */
@@ -68,6 +75,8 @@ typedef struct {
   double gap;         /* -G   0.8 */
   double match;       /* --match 1.0 */
   double mismatch;    /* --mismatch 0.8 */
+  double ext;         /* BPLA -e (gap extension), -0.75 */
+  double score_table[16]; /* BPLA --score table, [x residue][y residue] ACGU */
 } sk_kernel_params;
 
 void sk_kernel_params_default(sk_kernel_params *p, int32_t kind);
@@ -127,6 +136,12 @@ int sk_dataset_dag(const sk_dataset *ds, int i, uint32_t *first, uint32_t *last,
 /* ProfileSequence of example i (common/profile.cpp): prof5 gets len*5 floats
  * (A,C,G,U,gap), *n_seqs the row count. */
 int sk_dataset_profile(const sk_dataset *ds, int i, float *prof5, float *n_seqs);
+
+/* BPLA position weights of example i (bpla_kernel/data.cpp:19-45: sqrt of
+ * the left, right and unpaired probabilities; 0,0,1 without base pairs),
+ * len floats each (packer-parity introspection). */
+int sk_dataset_bpla_weights(const sk_dataset *ds, int i, float *p_left,
+                            float *p_right, float *p_unpair);
 
 /* Upload the packed example set to the context's device (idempotent).
  * Must be called after the last sk_dataset_add and before any compute. */

@@ -55,6 +55,10 @@ def oracle():
         L.orc_ribosum_tables.argtypes = [_F, _F]
         L.orc_char2rna.argtypes = [C.c_int]
         L.orc_char2rna.restype = C.c_int
+        L.orc_bpla.restype = C.c_double
+        L.orc_bpla.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double,
+                               C.c_double, C.c_double, _D]
+        L.orc_bpla_weights.argtypes = [C.c_void_p, _F, _F, _F]
         L.orc_naive_string.restype = C.c_double
         L.orc_naive_string.argtypes = [C.c_char_p, C.c_char_p, C.c_double]
         _o = L
@@ -162,6 +166,9 @@ def kernel_value(kind: int, x: OMData, y: OMData, p) -> float:
         return si_stem(x, y, p.loop_gap, p.stack, p.covar, p.len_band) + si_str(x, y, p.gap, p.match, p.mismatch)
     if kind == 6:
         return p.beta * math.log(stem()) + 0.0
+    if 9 <= kind <= 12:
+        return bpla(x, y, kind in (10, 12), kind in (11, 12), p.gap, p.ext, p.alpha, p.beta,
+                    list(p.score_table))
     if kind == 8:
         raise ValueError("naive string kernel compares raw strings: use naive_string()")
     if kind == 7:
@@ -171,3 +178,15 @@ def kernel_value(kind: int, x: OMData, y: OMData, p) -> float:
 
 def naive_string(x: str, y: str, gap=0.8) -> float:
     return oracle().orc_naive_string(x.encode(), y.encode(), gap)
+
+
+def bpla(x: OMData, y: OMData, no_bp: bool, sw: bool, gap, ext, alpha, beta, table16) -> float:
+    t = (C.c_double * 16)(*table16)
+    return oracle().orc_bpla(x.h, y.h, int(no_bp), int(sw), gap, ext, alpha, beta, t)
+
+
+def bpla_weights(x: OMData):
+    L = oracle().orc_mdata_seq_len(x.h)
+    a = [np.zeros(max(L, 1), np.float32) for _ in range(3)]
+    oracle().orc_bpla_weights(x.h, *(v.ctypes.data_as(_F) for v in a))
+    return [v[:L] for v in a]

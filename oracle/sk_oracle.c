@@ -794,3 +794,131 @@ double orc_naive_string(const char *x, const char *y, double gap) {
   free(K0); free(G0); free(K1); free(G1);
   return r;
 }
+
+/* ------------------------------------------------------------------ */
+/* BPLA kernel (bpla_kernel/).  Data<ProfileSequence, list<string>>:
+ * profile of all rows + fill_weight over the averaged BPMatrix
+ * (bpla_kernel/data.cpp:19-45). */
+void orc_bpla_weights(const orc_mdata *d, float *p_left, float *p_right, float *p_unpair) {
+  const int L = d->len;
+  for (int i = 0; i < L; ++i) {
+    float pl = 0.0f, pr = 0.0f, pu;
+    /* p_r[i] += bp(j+1,i+1), j<i ; p_l[i] += bp(i+1,j+1), j>i: float
+     * accumulators, each add done in double then stored (data.cpp:33-36) */
+    for (int j = 0; j < i; ++j) pr = (float)((double)pr + d->bpp[tri_index(L, j, i)]);
+    for (int j = i + 1; j < L; ++j) pl = (float)((double)pl + d->bpp[tri_index(L, i, j)]);
+    pu = (float)(1.0 - (double)(pl + pr));           /* data.cpp:37 */
+    if (pu < 0.0f) pu = 0.0f;                        /* data.cpp:38 */
+    p_right[i] = (float)sqrt((double)pr);            /* data.cpp:39-41 */
+    p_left[i] = (float)sqrt((double)pl);
+    p_unpair[i] = (float)sqrt((double)pu);
+  }
+}
+
+typedef struct {
+  const orc_mdata *x, *y;
+  const float *xl, *xr, *xu, *yl, *yr, *yu;
+  const double *table; /* 4x4 */
+  double alpha;
+  int bp;              /* BPLAScore (1) or LAScore (0) */
+} la_score;
+
+/* LAScore::operator() (bpla_kernel.cpp:24-43): counts-weighted mean of the
+ * score table over the residue columns, 0 when either column has none. */
+static double la_score_fn(const la_score *S, int i, int j) {
+  const float *xc = S->x->prof5 + (size_t)i * 5, *yc = S->y->prof5 + (size_t)j * 5;
+  double v = 0.0;
+  float n = 0.0f;
+  for (int k = 0; k != 4; ++k) {
+    if (xc[k] == 0.0f) continue;
+    for (int l = 0; l != 4; ++l) {
+      if (yc[l] == 0.0f) continue;
+      n += xc[k] * yc[l];
+      v += S->table[k * 4 + l] * xc[k] * yc[l];
+    }
+  }
+  return n == 0.0f ? 0.0 : v / n;
+}
+
+/* BPLAScore::operator() (bpla_kernel.cpp:48-62); float products as written */
+static double score_fn(const la_score *S, int i, int j) {
+  if (!S->bp) return la_score_fn(S, i, j);
+  float lr = S->xr[i] * S->yr[j];
+  float ll = S->xl[i] * S->yl[j];
+  float u = S->xu[i] * S->yu[j];
+  return S->alpha * (double)(lr + ll) + (double)u * la_score_fn(S, i, j);
+}
+
+static double bpla_exp(const la_score *S, double beta, double gap, double ext) {
+  /* local_alignment_exp (bpla_kernel.cpp:64-115) */
+  const int n = S->x->len, m = S->y->len, W = m + 1;
+  const double bg = exp(beta * gap), be = exp(beta * ext);
+  size_t cells = (size_t)(n + 1) * (m + 1);
+  double *M = (double *)calloc(cells, sizeof(double)), *X = (double *)calloc(cells, sizeof(double));
+  double *Y = (double *)calloc(cells, sizeof(double)), *X2 = (double *)calloc(cells, sizeof(double));
+  double *Y2 = (double *)calloc(cells, sizeof(double));
+#define AT(T, i, j) T[(size_t)(i) * W + (j)]
+  for (int i = 1; i <= n; ++i)
+    for (int j = 1; j <= m; ++j) {
+      AT(M, i, j) = exp(beta * score_fn(S, i - 1, j - 1)) *
+                    (1 + AT(X, i - 1, j - 1) + AT(Y, i - 1, j - 1) + AT(M, i - 1, j - 1));
+      AT(X, i, j) = bg * AT(M, i - 1, j) + be * AT(X, i - 1, j);
+      AT(Y, i, j) = bg * (AT(M, i, j - 1) + AT(X, i, j - 1)) + be * AT(Y, i, j - 1);
+      AT(X2, i, j) = AT(M, i - 1, j) + AT(X2, i - 1, j);
+      AT(Y2, i, j) = AT(M, i, j - 1) + AT(X2, i, j - 1) + AT(Y2, i, j - 1);
+    }
+  double r = 1 + AT(X2, n, m) + AT(Y2, n, m) + AT(M, n, m);
+#undef AT
+  free(M); free(X); free(Y); free(X2); free(Y2);
+  return r;
+}
+
+static double dmax(double a, double b) { return a < b ? b : a; }
+
+static double bpla_max(const la_score *S, double gap, double ext) {
+  /* local_alignment_max (bpla_kernel.cpp:117-157) */
+  const int n = S->x->len, m = S->y->len, W = m + 1;
+  size_t cells = (size_t)(n + 1) * (m + 1);
+  double *M = (double *)calloc(cells, sizeof(double)), *X = (double *)calloc(cells, sizeof(double));
+  double *Y = (double *)calloc(cells, sizeof(double));
+  double Mmax = 0;
+#define AT(T, i, j) T[(size_t)(i) * W + (j)]
+  for (int i = 1; i <= n; ++i)
+    for (int j = 1; j <= m; ++j) {
+      double v = dmax(0.0, AT(M, i - 1, j - 1));
+      v = dmax(v, AT(X, i - 1, j - 1));
+      v = dmax(v, AT(Y, i - 1, j - 1));
+      AT(M, i, j) = v + score_fn(S, i - 1, j - 1);
+      Mmax = dmax(Mmax, AT(M, i, j));
+      AT(X, i, j) = dmax(AT(M, i - 1, j) + gap, AT(X, i - 1, j) + ext);
+      AT(Y, i, j) = dmax(dmax(AT(M, i, j - 1) + gap, AT(X, i, j - 1) + gap), AT(Y, i, j - 1) + ext);
+    }
+#undef AT
+  free(M); free(X); free(Y);
+  return Mmax;
+}
+
+double orc_bpla(const orc_mdata *x, const orc_mdata *y, int no_bp, int sw, double gap, double ext,
+                double alpha, double beta, const double *table16) {
+  /* BPLAKernel::operator() (bpla_kernel.cpp:159-174) */
+  la_score S;
+  memset(&S, 0, sizeof(S));
+  S.x = x;
+  S.y = y;
+  S.table = table16;
+  S.alpha = alpha;
+  S.bp = !no_bp;
+  float *w = NULL;
+  if (S.bp) {
+    if (!x->bpp || !y->bpp) return NAN; /* the reference indexes empty vectors */
+    w = (float *)malloc(sizeof(float) * 3 * (size_t)(x->len + y->len + 1));
+    float *xl = w, *xr = xl + x->len, *xu = xr + x->len;
+    float *yl = xu + x->len, *yr = yl + y->len, *yu = yr + y->len;
+    orc_bpla_weights(x, xl, xr, xu);
+    orc_bpla_weights(y, yl, yr, yu);
+    S.xl = xl; S.xr = xr; S.xu = xu; S.yl = yl; S.yr = yr; S.yu = yu;
+  }
+  double r = sw ? bpla_max(&S, gap, ext) : bpla_exp(&S, beta, gap, ext);
+  free(w);
+  return r;
+}

@@ -87,6 +87,18 @@ int orc_char2rna(int c);
 /* Naive gapped string kernel (string_kernel/string_kernel.cpp:14-85) */
 double orc_naive_string(const char *x, const char *y, double gap);
 
+/* BPLA kernel (bpla_kernel/bpla_kernel.cpp:159-174): local-alignment
+ * partition function (sw=0, :64-115) or Smith-Waterman score (sw=1,
+ * :117-157) over profile columns, with the base-pairing score of BPLAScore
+ * (no_bp=0, :48-62) or LAScore alone (no_bp=1, :24-43).  table16 is the 4x4
+ * score table (row = x residue).  The CLI parses gap/ext/alpha/beta as float
+ * (bpla_kernel/main.cpp:52-76): pass float-rounded values for CLI parity. */
+double orc_bpla(const orc_mdata *x, const orc_mdata *y, int no_bp, int sw, double gap, double ext,
+                double alpha, double beta, const double *table16);
+/* fill_weight of bpla_kernel/data.cpp:19-45 (sqrt of left / right / unpaired
+ * probabilities per aligned position); example built with use_bp. */
+void orc_bpla_weights(const orc_mdata *d, float *p_left, float *p_right, float *p_unpair);
+
 #ifdef __cplusplus
 }
 #endif

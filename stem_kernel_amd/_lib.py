@@ -23,7 +23,8 @@ STATUS = {
 }
 
 # sk_kernel_kind
-SU_STEM, SI_STEM, SU_STR, SI_STR, SU_STEM_STR, SI_STEM_STR, LSU_STEM, LSU_STEM_STR, NAIVE_STR = range(9)
+(SU_STEM, SI_STEM, SU_STR, SI_STR, SU_STEM_STR, SI_STEM_STR, LSU_STEM, LSU_STEM_STR, NAIVE_STR,
+ BPLA, LA, BPLA_SW, LA_SW) = range(13)
 
 
 class KernelParams(C.Structure):
@@ -31,7 +32,7 @@ class KernelParams(C.Structure):
         ("kind", C.c_int32), ("len_band", C.c_uint32), ("beta", C.c_double),
         ("loop_gap", C.c_double), ("stack", C.c_double), ("covar", C.c_double),
         ("alpha", C.c_double), ("gap", C.c_double), ("match", C.c_double),
-        ("mismatch", C.c_double),
+        ("mismatch", C.c_double), ("ext", C.c_double), ("score_table", C.c_double * 16),
     ]
 
 
@@ -60,6 +61,7 @@ SIGNATURES = {
     "sk_dataset_dag": (C.c_int, [_P, C.c_int, _U32P, _U32P, _U32P, _U32P, _F32P, _U32P,
                                  _U32P, _U32P, _U32P, _F32P, _U32P, _F32P]),
     "sk_dataset_profile": (C.c_int, [_P, C.c_int, _F32P, _F32P]),
+    "sk_dataset_bpla_weights": (C.c_int, [_P, C.c_int, _F32P, _F32P, _F32P]),
     "sk_dataset_upload": (C.c_int, [_P, _P]),
     "sk_gram": (C.c_int, [_P, _P, C.POINTER(KernelParams), C.c_int, _F64P]),
     "sk_pairs_device": (C.c_int, [_P, _P, C.POINTER(KernelParams), _I32P, _I32P, C.c_int64,
@@ -126,5 +128,9 @@ def default_params(kind=SU_STEM_STR, **over):
     p = KernelParams()
     lib().sk_kernel_params_default(C.byref(p), kind)
     for k, v in over.items():
-        setattr(p, k, v)
+        if k == "score_table":
+            for i, t in enumerate(v):
+                p.score_table[i] = float(t)
+        else:
+            setattr(p, k, v)
     return p

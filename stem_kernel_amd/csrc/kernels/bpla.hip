@@ -1,0 +1,215 @@
+// BPLA kernel on CDNA4 (gfx950): local-alignment partition function (or
+// Smith-Waterman score) over profile columns with base-pairing scores.
+//
+// Reference: BPLAKernel<double,MData>::operator()  bpla_kernel/bpla_kernel.cpp:159-174
+//   local_alignment_exp :64-115 (M, X, Y, X2, Y2; result 1 + X2 + Y2 + M)
+//   local_alignment_max :117-157 (M, X, Y; result max M)
+//   LAScore :16-43, BPLAScore :45-62, fill_weight bpla_kernel/data.cpp:19-45.
+//
+// Systolic schedule (as the profile string kernel): one wavefront per pair,
+// lane l owns DP row i = 64*strip + l + 1 and computes column j = t - l + 1 at
+// step t.  Row i-1 lives one lane down and one step ahead, so the "up" cell
+// (i-1, j) is lane l-1's previous output (one DPP wave_shr), and the diagonal
+// (i-1, j-1) is what lane l received one step earlier.  The strip boundary
+// row goes through a per-wave LDS row of the four states lane 0 reads.
+// FP64 throughout; one exp per cell is the bound.
+#include <hip/hip_runtime.h>
+
+#include "device_set.h"
+#include "launch.h"
+
+namespace sk {
+
+// lane l receives lane l-1's value (lane 0 receives `low`): DPP wave_shr:1
+__device__ __forceinline__ double wave_shr1(double v, double low) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int llo = __double2loint(low), lhi = __double2hiint(low);
+  const int rlo = __builtin_amdgcn_update_dpp(llo, lo, 0x138, 0xf, 0xf, false);
+  const int rhi = __builtin_amdgcn_update_dpp(lhi, hi, 0x138, 0xf, 0xf, false);
+  return __hiloint2double(rhi, rlo);
+}
+
+__device__ __forceinline__ int bpla_onehot(float4 c) {
+  if (c.x == 1.0f && c.y == 0.0f && c.z == 0.0f && c.w == 0.0f) return 0;
+  if (c.x == 0.0f && c.y == 1.0f && c.z == 0.0f && c.w == 0.0f) return 1;
+  if (c.x == 0.0f && c.y == 0.0f && c.z == 1.0f && c.w == 0.0f) return 2;
+  if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f && c.w == 1.0f) return 3;
+  return -1;
+}
+
+// LAScore::operator() (bpla_kernel.cpp:24-43): 0 when either column is empty
+__device__ __forceinline__ double la_score(const double* __restrict__ tb, float4 xc, float4 yc) {
+  const float xa[4] = {xc.x, xc.y, xc.z, xc.w};
+  const float yb[4] = {yc.x, yc.y, yc.z, yc.w};
+  double v = 0.0;
+  float n = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (xa[k] == 0.0f) continue;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      if (yb[l] == 0.0f) continue;
+      n = __fadd_rn(n, __fmul_rn(xa[k], yb[l]));
+      v += tb[k * 4 + l] * (double)xa[k] * (double)yb[l];
+    }
+  }
+  return n == 0.0f ? 0.0 : v / (double)n;
+}
+
+__global__ void __launch_bounds__(256) sk_bpla_kernel(BplaLaunch P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const DevSet& sx = P.xset;
+  const DevSet& sy = P.yset;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
+  const int maxlen = P.lds_max_len;  // even
+  // LDS: table[16] | per wave: bM,bX,bY,bX2 [maxlen+2] | yprof, ylru float4 [maxlen] | ycode [maxlen]
+  double* tb = reinterpret_cast<double*>(smem);
+  const size_t wbytes = bpla_wave_lds_bytes(maxlen);
+  unsigned char* wbase = smem + 16 * 8 + (size_t)wave * wbytes;
+  double* bM = reinterpret_cast<double*>(wbase);
+  double* bX = bM + (maxlen + 2);
+  double* bY = bX + (maxlen + 2);
+  double* bX2 = bY + (maxlen + 2);
+  float4* yprof = reinterpret_cast<float4*>(bX2 + (maxlen + 2));
+  float4* ylru = yprof + maxlen;
+  int* ycode = reinterpret_cast<int*>(ylru + maxlen);
+  (void)nwaves;
+
+  if (threadIdx.x < 16) tb[threadIdx.x] = P.table[threadIdx.x];
+  __syncthreads();
+  const bool sw = P.sw != 0, bp = P.bp != 0;
+  const double beta = P.beta, alpha = P.alpha, gap = P.gap, ext = P.ext;
+  const double bg = P.beta_gap, be = P.beta_ext;
+
+  for (;;) {
+    unsigned long long pr = 0;
+    if (lane == 0) pr = atomicAdd(P.pair_counter, 1ull);
+    pr = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(pr >> 32)) << 32) |
+         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)pr);
+    if ((int64_t)pr >= P.n_pairs) break;
+    const int x = P.xs[pr], y = P.ys[pr];
+    const int Lx = sx.ex_len[x], Ly = sy.ex_len[y];
+    const int xpb = sx.ex_pos_base[x], ypb = sy.ex_pos_base[y];
+    for (int j = lane; j < Ly; j += 64) {
+      const float4 c = sy.pos_prof[ypb + j];
+      yprof[j] = c;
+      ylru[j] = sy.pos_lru[ypb + j];
+      ycode[j] = bpla_onehot(c);
+    }
+    for (int j = lane; j <= Ly; j += 64) {  // row 0 (bpla_kernel.cpp:90-96)
+      bM[j] = 0.0;
+      bX[j] = 0.0;
+      bY[j] = 0.0;
+      bX2[j] = 0.0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    double result = 0.0, mmax = 0.0;
+    const int nstrips = (Lx + 63) / 64;
+    for (int strip = 0; strip < nstrips; ++strip) {
+      const int i = strip * 64 + lane + 1;
+      const bool row_ok = i <= Lx;
+      float4 xc = make_float4(0.f, 0.f, 0.f, 0.f), xw = make_float4(0.f, 0.f, 0.f, 0.f);
+      int xcode = -1;
+      if (row_ok) {
+        xc = sx.pos_prof[xpb + i - 1];
+        xw = sx.pos_lru[xpb + i - 1];
+        xcode = bpla_onehot(xc);
+      }
+      // my outputs of the previous step (row i, column j-1); zero at j <= 0
+      double lM = 0.0, lX = 0.0, lY = 0.0, lX2 = 0.0, lY2 = 0.0;
+      // what I received last step: (i-1, j-1)
+      double dM = 0.0, dX = 0.0, dY = 0.0;
+      for (int t = 0; t < Ly + 64; ++t) {
+        const int j = t - lane + 1;
+        // lane 0 takes row i-1 from the boundary row (column t+1 = its j)
+        double b0M = 0.0, b0X = 0.0, b0Y = 0.0, b0X2 = 0.0;
+        if (t + 1 <= Ly) {
+          b0M = bM[t + 1];
+          b0X = bX[t + 1];
+          b0Y = bY[t + 1];
+          b0X2 = bX2[t + 1];
+        }
+        const double upM = wave_shr1(lM, b0M);
+        const double upX = wave_shr1(lX, b0X);
+        const double upY = wave_shr1(lY, b0Y);
+        const double upX2 = wave_shr1(lX2, b0X2);
+        if (j >= 1 && j <= Ly) {
+          const float4 yc = yprof[j - 1];
+          const int yk = ycode[j - 1];
+          double s = (xcode >= 0 && yk >= 0) ? tb[xcode * 4 + yk] : la_score(tb, xc, yc);
+          if (bp) {
+            // BPLAScore (bpla_kernel.cpp:55-60): float products as written
+            const float4 yw = ylru[j - 1];
+            const float pp = __fadd_rn(__fmul_rn(xw.y, yw.y), __fmul_rn(xw.x, yw.x));
+            const float uu = __fmul_rn(xw.z, yw.z);
+            s = alpha * (double)pp + (double)uu * s;
+          }
+          double nM, nX, nY, nX2 = 0.0, nY2 = 0.0;
+          if (!sw) {
+            nM = exp(beta * s) * (1.0 + dX + dY + dM);
+            nX = bg * upM + be * upX;
+            nY = bg * (lM + lX) + be * lY;
+            nX2 = upM + upX2;
+            nY2 = lM + lX2 + lY2;
+          } else {
+            double v = fmax(0.0, dM);
+            v = fmax(v, dX);
+            v = fmax(v, dY);
+            nM = v + s;
+            nX = fmax(upM + gap, upX + ext);
+            nY = fmax(fmax(lM + gap, lX + gap), lY + ext);
+          }
+          if (row_ok) {
+            lM = nM;
+            lX = nX;
+            lY = nY;
+            lX2 = nX2;
+            lY2 = nY2;
+            mmax = fmax(mmax, nM);
+            if (i == Lx && j == Ly) result = 1.0 + nX2 + nY2 + nM;
+          }
+          if (lane == 63) {
+            bM[j] = nM;
+            bX[j] = nX;
+            bY[j] = nY;
+            bX2[j] = nX2;
+          }
+        }
+        dM = upM;
+        dX = upX;
+        dY = upY;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    double r;
+    if (sw) {
+      for (int off = 32; off > 0; off >>= 1) mmax = fmax(mmax, __shfl_xor(mmax, off, 64));
+      r = mmax;
+    } else {
+      const int owner = Lx == 0 ? 0 : ((Lx - 1) & 63);
+      r = (Lx == 0 || Ly == 0) ? 1.0 : __shfl(result, owner, 64);
+    }
+    if (lane == 0) P.out[pr] = r;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+size_t bpla_lds_bytes(const BplaLaunch& P, int nwaves) {
+  return 16 * 8 + (size_t)nwaves * bpla_wave_lds_bytes(P.lds_max_len);
+}
+
+hipError_t launch_bpla(const BplaLaunch& P, int grid, int nwaves, hipStream_t st) {
+  hipLaunchKernelGGL(sk_bpla_kernel, dim3(grid), dim3(64 * nwaves), bpla_lds_bytes(P, nwaves), st,
+                     P);
+  return hipGetLastError();
+}
+
+}  // namespace sk

@@ -44,6 +44,7 @@ struct DevSet {
   const float* pos_w = nullptr;      // fill_weight (empty -> string kernel unweighted)
   const int32_t* ex_has_w = nullptr;
   const uint8_t* pos_chr = nullptr;  // raw characters of row 0 (naive string kernel)
+  const float4* pos_lru = nullptr;   // BPLA fill_weight: sqrt p_left, p_right, p_unpair, 0
   // x-role schedule, in the reference's post-order (children first, a row's
   // last parent soon after it).  Row r of example e is xr_*[ex_node_base[e]+r];
   // its children are xr_ch[ex_xch_base[e] + sum of earlier rows' n_ch ...].

@@ -47,6 +47,27 @@ struct StrLaunch {
   int32_t lds_max_len = 0;
 };
 
+struct BplaLaunch {
+  DevSet xset, yset;
+  const double* table = nullptr;  // 16: score table (x residue major)
+  double alpha = 0.0, beta = 0.0, gap = 0.0, ext = 0.0;
+  double beta_gap = 0.0, beta_ext = 0.0;  // exp(beta*gap), exp(beta*ext)
+  int32_t sw = 0;  // local_alignment_max instead of local_alignment_exp
+  int32_t bp = 0;  // BPLAScore (base-pairing terms) instead of LAScore
+  const int32_t* xs = nullptr;
+  const int32_t* ys = nullptr;
+  int64_t n_pairs = 0;
+  double* out = nullptr;
+  unsigned long long* pair_counter = nullptr;
+  int32_t lds_max_len = 0;  // even
+};
+
+// per-wave LDS of the BPLA kernel: 4 boundary rows + y columns (16-B aligned)
+__host__ __device__ inline size_t bpla_wave_lds_bytes(int maxlen) {
+  const size_t b = (size_t)4 * (maxlen + 2) * 8 + (size_t)maxlen * 32 + (size_t)maxlen * 4;
+  return (b + 15) & ~(size_t)15;
+}
+
 enum CombineMode : int32_t {
   kCombineStem = 0,      // K = stem
   kCombineStr = 1,       // K = str
@@ -64,6 +85,9 @@ int stem_maxk(int max_nl);
 
 size_t str_lds_bytes(const StrLaunch& P, int nwaves);
 hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st);
+
+size_t bpla_lds_bytes(const BplaLaunch& P, int nwaves);
+hipError_t launch_bpla(const BplaLaunch& P, int grid, int nwaves, hipStream_t st);
 
 hipError_t launch_combine(const double* stem, const double* str, double* out, int64_t n,
                           int32_t mode, double alpha, double beta, hipStream_t st);

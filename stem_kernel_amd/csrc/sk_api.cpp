@@ -51,6 +51,18 @@ hipError_t upload(DeviceBuffers& db, const std::vector<T>& v, const T** out) {
   return e;
 }
 
+// BPLA fill_weight (bpla_kernel/data.cpp:19-45) over the averaged bp matrix:
+// float accumulators with each add rounded from double, then sqrt.
+float4 bpla_weight(const Example& X, int i) {
+  if (!X.has_bp) return make_float4(0.f, 0.f, 1.f, 0.f);
+  float pl = 0.0f, pr = 0.0f;
+  for (int j = 0; j < i; ++j) pr = (float)((double)pr + X.bpp[sk::tri_index(X.len, j, i)]);
+  for (int j = i + 1; j < X.len; ++j) pl = (float)((double)pl + X.bpp[sk::tri_index(X.len, i, j)]);
+  float pu = (float)(1.0 - (double)(pl + pr));
+  if (pu < 0.0f) pu = 0.0f;
+  return make_float4(std::sqrt(pl), std::sqrt(pr), std::sqrt(pu), 0.f);
+}
+
 // Packed host image of a dataset (device_set.h layout).
 struct HostPack {
   std::vector<int32_t> ex_nl, ex_node_base, ex_edge_base, ex_bpf_base, ex_lvl_base, ex_nlev,
@@ -66,6 +78,7 @@ struct HostPack {
   std::vector<float4> pos_prof;
   std::vector<float> pos_w;
   std::vector<uint8_t> pos_chr;
+  std::vector<float4> pos_lru;
   std::vector<int32_t> ex_nslots, ex_xch_base;
   std::vector<uint32_t> xr_a, xr_b, xr_c, xr_node, xr_ch;
   std::vector<float> xr_w, xr_nbp, xr_bp0;
@@ -277,6 +290,7 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       P.pos_w.push_back(X.has_bp ? X.pos_weight[i] : 1.0f);
       P.pos_chr.push_back((uint8_t)X.rows[0][i]);
     }
+    for (int i = 0; i < X.len; ++i) P.pos_lru.push_back(bpla_weight(X, i));
     P.ex_node_base.push_back((int32_t)P.nd_a.size());
     P.ex_edge_base.push_back((int32_t)P.ed.size());
     P.ex_bpf_base.push_back((int32_t)P.bpf_code.size());
@@ -292,7 +306,10 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
 }
 
 // ------------------------------------------------------------ parameters
-bool kind_has_stem(int k) { return k != SK_SU_STR && k != SK_SI_STR && k != SK_NAIVE_STR; }
+bool kind_is_bpla(int k) { return k >= SK_BPLA && k <= SK_LA_SW; }
+bool kind_has_stem(int k) {
+  return k != SK_SU_STR && k != SK_SI_STR && k != SK_NAIVE_STR && !kind_is_bpla(k);
+}
 bool kind_has_str(int k) {
   return k == SK_SU_STR || k == SK_SI_STR || k == SK_SU_STEM_STR || k == SK_SI_STEM_STR ||
          k == SK_LSU_STEM_STR || k == SK_NAIVE_STR;
@@ -372,6 +389,69 @@ int check_set(sk_context* ctx, sk_dataset* ds) {
   return SK_OK;
 }
 
+// BPLA kinds: one systolic launch (bpla.hip), result straight to out_dev.
+int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
+             const int32_t* x, const int32_t* y, int64_t n, double* out_dev) {
+  const bool bp = kp->kind == SK_BPLA || kp->kind == SK_BPLA_SW;
+  const bool sw = kp->kind == SK_BPLA_SW || kp->kind == SK_LA_SW;
+  double cells = 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    const Example& ex = xs_->ex[x[k]];
+    const Example& ey = ys_->ex[y[k]];
+    // BPLAScore reads p_left/p_right/p_unpair, which MData(ma) leaves empty
+    if (bp && (!ex.has_bp || !ey.has_bp))
+      return fail(ctx, SK_ERR_INVALID, "BPLA with base pairs needs examples built with use_bp");
+    cells += (double)ex.len * (double)ey.len;
+  }
+  ctx->last_cells = cells;
+  const HostPack& PY = ys_->pack;
+  const size_t nb = (size_t)n;
+  int rc = ensure_work(ctx, 16 * 8 + nb * 8 + 2048);
+  if (rc) return rc;
+  Arena A{static_cast<char*>(ctx->work), 0, ctx->work_bytes};
+  double* d_tb = A.take<double>(16);
+  int32_t* d_px = A.take<int32_t>(nb);
+  int32_t* d_py = A.take<int32_t>(nb);
+  unsigned long long* d_ctr = A.take<unsigned long long>(8);
+  hipStream_t S = ctx->stream;
+  SK_HIP(ctx, hipMemcpyAsync(d_tb, kp->score_table, 16 * 8, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemcpyAsync(d_px, x, nb * 4, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemcpyAsync(d_py, y, nb * 4, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemsetAsync(d_ctr, 0, 8 * sizeof(unsigned long long), S));
+  sk::BplaLaunch T;
+  T.xset = xs_->dev;
+  T.yset = ys_->dev;
+  T.table = d_tb;
+  T.alpha = kp->alpha;
+  T.beta = kp->beta;
+  T.gap = kp->gap;
+  T.ext = kp->ext;
+  T.beta_gap = std::exp(kp->beta * kp->gap);  // bpla_kernel.cpp:70-71
+  T.beta_ext = std::exp(kp->beta * kp->ext);
+  T.sw = sw ? 1 : 0;
+  T.bp = bp ? 1 : 0;
+  T.xs = d_px;
+  T.ys = d_py;
+  T.n_pairs = n;
+  T.out = out_dev;
+  T.pair_counter = d_ctr;
+  T.lds_max_len = (std::max(PY.max_len, 1) + 1) & ~1;
+  const int w = 4;
+  const size_t lds = sk::bpla_lds_bytes(T, w);
+  if (lds > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
+  const int per_cu = std::max(1, std::min<int>((int)(163840 / lds), 8));
+  const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (n + w - 1) / w);
+  SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
+  SK_HIP(ctx, sk::launch_bpla(T, (int)g, w, S));
+  SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
+  SK_HIP(ctx, hipStreamSynchronize(S));
+  float ms = 0.f;
+  SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->last_stem_ms = ms;
+  ctx->last_launches = 1;
+  return SK_OK;
+}
+
 // Core: out_dev[k] = K(xset[x[k]], yset[y[k]]) (device buffer), async.
 int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
               const int32_t* x, const int32_t* y, int64_t n, double* out_dev) {
@@ -381,7 +461,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   rc = check_set(ctx, ys_);
   if (rc) return rc;
   if (n < 0) return fail(ctx, SK_ERR_INVALID, "negative pair count");
-  if (kp->kind < SK_SU_STEM || kp->kind > SK_NAIVE_STR)
+  if (kp->kind < SK_SU_STEM || kp->kind > SK_LA_SW)
     return fail(ctx, SK_ERR_UNSUPPORTED, "unknown kernel kind");
   ctx->last_stem_ms = ctx->last_str_ms = ctx->last_cells = 0.0;
   ctx->last_launches = 0;
@@ -390,6 +470,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   for (int64_t k = 0; k < n; ++k)
     if (x[k] < 0 || x[k] >= nx || y[k] < 0 || y[k] >= ny)
       return fail(ctx, SK_ERR_RANGE, "pair index out of range");
+  if (kind_is_bpla(kp->kind)) return run_bpla(ctx, xs_, ys_, kp, x, y, n, out_dev);
 
   const bool stem = kind_has_stem(kp->kind), str = kind_has_str(kp->kind);
   const HostPack& PX = xs_->pack;
@@ -642,6 +723,18 @@ void sk_kernel_params_default(sk_kernel_params* p, int32_t kind) {
   p->gap = 0.8;
   p->match = 1.0;
   p->mismatch = 0.8;
+  // bpla_kernel/main.cpp:20-26 (float table), 68-76 (float options)
+  static const float kBplaTable[16] = {5.846613f,  -1.860000f, -1.460000f, -1.390000f,
+                                       -1.860000f, 4.786613f,  -2.480000f, -1.050000f,
+                                       -1.460000f, -2.480000f, 4.656613f,  -1.740000f,
+                                       -1.390000f, -1.050000f, -1.740000f, 5.276613f};
+  for (int k = 0; k < 16; ++k) p->score_table[k] = (double)kBplaTable[k];
+  p->ext = (double)-0.75f;
+  if (kind >= SK_BPLA && kind <= SK_LA_SW) {
+    p->gap = (double)-8.0f;
+    p->alpha = (double)4.5f;
+    p->beta = (double)0.11f;
+  }
 }
 
 const char* sk_strerror(int s) {
@@ -829,6 +922,20 @@ int sk_dataset_profile(const sk_dataset* ds, int i, float* prof5, float* n_seqs)
   return SK_OK;
 }
 
+int sk_dataset_bpla_weights(const sk_dataset* ds, int i, float* p_left, float* p_right,
+                            float* p_unpair) {
+  if (!ds) return SK_ERR_INVALID;
+  if (i < 0 || i >= (int)ds->ex.size()) return SK_ERR_RANGE;
+  const Example& X = ds->ex[i];
+  for (int k = 0; k < X.len; ++k) {
+    const float4 w = bpla_weight(X, k);
+    if (p_left) p_left[k] = w.x;
+    if (p_right) p_right[k] = w.y;
+    if (p_unpair) p_unpair[k] = w.z;
+  }
+  return SK_OK;
+}
+
 int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   if (!ctx || !ds) return SK_ERR_INVALID;
   if (ds->uploaded) return ds->device == ctx->device ? SK_OK : fail(ctx, SK_ERR_INVALID, "dataset bound to another device");
@@ -864,6 +971,7 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.pos_prof, &D.pos_prof));
   SK_HIP(ctx, upload(B, P.pos_w, &D.pos_w));
   SK_HIP(ctx, upload(B, P.pos_chr, &D.pos_chr));
+  SK_HIP(ctx, upload(B, P.pos_lru, &D.pos_lru));
   SK_HIP(ctx, upload(B, P.ex_nslots, &D.ex_nslots));
   SK_HIP(ctx, upload(B, P.ex_xch_base, &D.ex_xch_base));
   SK_HIP(ctx, upload(B, P.xr_a, &D.xr_a));

@@ -119,6 +119,27 @@ class NaiveStringKernel(_Kernel):
         super().__init__(gap=gap)
 
 
+class BPLAKernel(_Kernel):
+    """BPLAKernel<double,MData>(score_table, noBP, SW, gap, ext, alpha, beta)
+    bpla_kernel/bpla_kernel.h:14-44, operator() bpla_kernel.cpp:159-174.
+
+    noBP: LAScore only (no base-pairing terms); SW: Smith-Waterman maximum
+    instead of the local-alignment partition function.  The reference CLI
+    reads gap/ext/alpha/beta as float (bpla_kernel/main.cpp:52-76), so they
+    are rounded to float32 here, as the CLI would; score_table (4x4, ACGU,
+    x residue major) defaults to bpla_kernel/main.cpp:20-26."""
+
+    def __init__(self, noBP=False, SW=False, gap=-8.0, ext=-0.75, alpha=4.5, beta=0.11,
+                 score_table=None, cli_float=True):
+        self.kind = {(False, False): _lib.BPLA, (True, False): _lib.LA,
+                     (False, True): _lib.BPLA_SW, (True, True): _lib.LA_SW}[(bool(noBP), bool(SW))]
+        f = (lambda v: float(np.float32(v))) if cli_float else float
+        kw = dict(gap=f(gap), ext=f(ext), alpha=f(alpha), beta=f(beta))
+        if score_table is not None:
+            kw["score_table"] = np.asarray(score_table, dtype=np.float64).reshape(16)
+        super().__init__(**kw)
+
+
 class SiStemStrKernel(_Kernel):
     """SiStemStrKernel(loop_gap, stack, covar, gap, match, mismatch, len_band)
     def_kernel.h:285-311 (--no-ribosum)."""
@@ -222,6 +243,14 @@ class Dataset:
         check(lib().sk_dataset_profile(self._h, i, out.ctypes.data_as(C.POINTER(C.c_float)),
                                        C.byref(ns)))
         return out[:L], ns.value
+
+    def bpla_weights(self, i: int):
+        """sqrt p_left, p_right, p_unpair of example i (bpla_kernel/data.cpp:19-45)."""
+        L = self.shape(i)[4]
+        a = [np.zeros(max(L, 1), np.float32) for _ in range(3)]
+        check(lib().sk_dataset_bpla_weights(self._h, i, *(v.ctypes.data_as(C.POINTER(C.c_float))
+                                                           for v in a)))
+        return [v[:L] for v in a]
 
     def label(self, i: int) -> str:
         return lib().sk_dataset_label(self._h, i).decode()

@@ -1,0 +1,109 @@
+"""BPLA kernel (bpla_kernel/): host weights (CPU, bit-exact)
+and HIP parity against the oracle (GPU, 1e-6 relative; max-plus SW modes
+only reorder nothing, so they agree to rounding of the score)."""
+import numpy as np
+import pytest
+
+import stem_kernel_amd as ska
+from oracle import pyoracle as po
+from tests.helpers import make_examples, mutate_alignment, rel_err
+
+TOL = 1e-6
+MODES = [(False, False), (True, False), (False, True), (True, True)]
+
+
+def _examples():
+    seqs = ska.random_sequences(5, 90, 0x5EED0003) + ska.random_sequences(2, 64, 7)
+    seqs += ["GGGAAACCC", "A", "ACGUN"]  # short, length 1, IUPAC N
+    base = ska.random_sequences(2, 70, 0x5EED0013)
+    alns = [mutate_alignment(base[0], 4, 3), mutate_alignment(base[1], 3, 4)]
+    alns.append(["ACGU-GRYAC", "AC-UUGCYAC"])  # IUPAC codes with gaps
+    return seqs + alns
+
+
+@pytest.fixture(scope="module")
+def bpla_set():
+    return make_examples(_examples())
+
+
+def test_bpla_weights_match_oracle(bpla_set):
+    ds, om = bpla_set
+    for i in range(len(om)):
+        got = ds.bpla_weights(i)
+        ref = po.bpla_weights(om[i])
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b)
+
+
+def test_bpla_default_params_are_cli_floats():
+    p = ska.BPLAKernel().params
+    assert p.kind == 9
+    assert p.beta == float(np.float32(0.11)) and p.gap == -8.0 and p.ext == -0.75
+    assert p.alpha == 4.5
+    assert abs(p.score_table[0] - 5.846613) < 1e-6 and p.score_table[1] == float(np.float32(-1.86))
+
+
+def _oracle(om, kern, rows, cols):
+    return np.array([[po.kernel_value(kern.params.kind, om[i], om[j], kern.params) for j in cols]
+                     for i in rows])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("noBP,SW", MODES)
+def test_bpla_gram_matches_oracle(gpu_ctx, bpla_set, noBP, SW):
+    ds, om = bpla_set
+    kern = ska.BPLAKernel(noBP=noBP, SW=SW)
+    got = gpu_ctx.gram(ds, kern)
+    n = len(om)
+    ref = _oracle(om, kern, range(n), range(n))
+    up = np.triu_indices(n)
+    assert rel_err(got[up], ref[up]) < TOL
+
+
+@pytest.mark.gpu
+def test_bpla_custom_table_and_params(gpu_ctx, bpla_set):
+    ds, om = bpla_set
+    tb = np.arange(16, dtype=np.float64).reshape(4, 4) / 8.0 - 1.0
+    kern = ska.BPLAKernel(gap=-5.0, ext=-1.0, alpha=2.0, beta=0.2, score_table=tb)
+    x = np.array([0, 1, 7, 10, 12], np.int32)
+    y = np.array([1, 0, 2, 11, 3], np.int32)
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    ref = np.array([po.kernel_value(kern.params.kind, om[a], om[b], kern.params)
+                    for a, b in zip(x, y)])
+    assert rel_err(got, ref) < TOL
+
+
+@pytest.mark.gpu
+def test_bpla_long_rows_cross_strips(gpu_ctx):
+    """L > 128: three 64-row strips and the LDS boundary row twice."""
+    seqs = ska.random_sequences(3, 150, 0x5EED0023) + ska.random_sequences(1, 129, 5)
+    ds, om = make_examples(seqs)
+    for noBP, SW in MODES:
+        kern = ska.BPLAKernel(noBP=noBP, SW=SW)
+        got = gpu_ctx.gram(ds, kern)
+        ref = _oracle(om, kern, range(4), range(4))
+        up = np.triu_indices(4)
+        assert rel_err(got[up], ref[up]) < TOL
+
+
+@pytest.mark.gpu
+def test_bpla_needs_base_pairs(gpu_ctx):
+    """BPLAScore reads p_left/right/unpair; MData(ma) has none (noBP is fine)."""
+    ds, om = make_examples(ska.random_sequences(2, 30, 3), use_bp=False)
+    with pytest.raises(ska.StemKernelError):
+        gpu_ctx.gram(ds, ska.BPLAKernel())
+    got = gpu_ctx.gram(ds, ska.BPLAKernel(noBP=True))
+    kern = ska.BPLAKernel(noBP=True)
+    ref = _oracle(om, kern, range(2), range(2))
+    assert rel_err(got, ref) < TOL
+
+
+@pytest.mark.gpu
+def test_bpla_normalized_and_predict(gpu_ctx, bpla_set):
+    ds, om = bpla_set
+    kern = ska.BPLAKernel()
+    g = gpu_ctx.gram(ds, kern, normalize=True)
+    assert np.allclose(np.diag(g), 1.0)
+    row = gpu_ctx.test_row(ds, 2, ds, kern)
+    ref = np.array([po.kernel_value(9, om[i], om[2], kern.params) for i in range(len(om))])
+    assert rel_err(row, ref) < TOL
