@@ -14,7 +14,7 @@ LIB := $(ROOT)stem_kernel_amd/libstem_kernel_amd.so
 HOST_SRC := $(ROOT)stem_kernel_amd/csrc/host/synth.cpp $(ROOT)stem_kernel_amd/csrc/host/example_build.cpp
 API_SRC := $(ROOT)stem_kernel_amd/csrc/sk_api.cpp
 HIP_SRC := $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip $(ROOT)stem_kernel_amd/csrc/kernels/profile_string.hip \
-           $(ROOT)stem_kernel_amd/csrc/kernels/bpla.hip
+           $(ROOT)stem_kernel_amd/csrc/kernels/bpla.hip $(ROOT)stem_kernel_amd/csrc/kernels/stem4d.hip
 HDRS := $(wildcard $(ROOT)stem_kernel_amd/csrc/*/*.h) $(ROOT)include/stem_kernel.h $(ROOT)stem_kernel_amd/csrc/ribosum85_60.inc
 
 HOST_OBJ := $(patsubst $(ROOT)stem_kernel_amd/csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC) $(API_SRC))
@@ -50,5 +50,5 @@ stamps:
 	@mkdir -p $(BUILD)/stamps
 	$(HIPCC) $(HIPFLAGS) -DSK_STAMPS -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip -o $(BUILD)/stamps/dag_stem.o
 	$(HIPCC) $(CXXFLAGS) -DSK_STAMPS -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/stamps/sk_api.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o -Wl,-rpath,/opt/rocm/lib
 .PHONY: stamps

@@ -57,7 +57,10 @@ typedef enum {
   SK_BPLA = 9,         /* local_alignment_exp with BPLAScore            (default)    */
   SK_LA = 10,          /* local_alignment_exp with LAScore               --noBP      */
   SK_BPLA_SW = 11,     /* local_alignment_max with BPLAScore             --SW        */
-  SK_LA_SW = 12        /* local_alignment_max with LAScore               --noBP --SW */
+  SK_LA_SW = 12,       /* local_alignment_max with LAScore               --noBP --SW */
+  /* StemKernel<double,BPMat>::full_dp of stem_kernel/ (stem_kernel.cpp:282-351)
+   * over single sequences (row 0, lowercased as the loader does) */
+  SK_STEM4D = 13
 } sk_kernel_kind;
 
 /* Kernel parameters; defaults are stem_kernel_lite/main.cpp:103-149
@@ -77,6 +80,13 @@ typedef struct {
   double mismatch;    /* --mismatch 0.8 */
   double ext;         /* BPLA -e (gap extension), -0.75 */
   double score_table[16]; /* BPLA --score table, [x residue][y residue] ACGU */
+  /* 4-D stem kernel (stem_kernel/main.cpp:40-60; float options): gap -g 0.8,
+   * stack -s 1.0 (fields above), and: */
+  double subst;       /* -v substitution weight for base pairs, 0.5 */
+  double bp_bound;    /* -p pairs count when prob > bp_bound (float compare), 0.0 */
+  int32_t bp_model;   /* 0: dataset bpp (BPMatrix/PFWrapper, the -p path),
+                         1: NormalBasePair, 2: WobbleBasePair (-w) */
+  uint32_t loop;      /* -l minimum loop (Normal/Wobble models), 3 */
 } sk_kernel_params;
 
 void sk_kernel_params_default(sk_kernel_params *p, int32_t kind);

@@ -59,6 +59,9 @@ def oracle():
         L.orc_bpla.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double,
                                C.c_double, C.c_double, _D]
         L.orc_bpla_weights.argtypes = [C.c_void_p, _F, _F, _F]
+        L.orc_stem4d.restype = C.c_double
+        L.orc_stem4d.argtypes = [C.c_char_p, _D, C.c_char_p, _D, C.c_double, C.c_double,
+                                 C.c_double, C.c_float, C.c_int, C.c_uint]
         L.orc_naive_string.restype = C.c_double
         L.orc_naive_string.argtypes = [C.c_char_p, C.c_char_p, C.c_double]
         _o = L
@@ -190,3 +193,19 @@ def bpla_weights(x: OMData):
     a = [np.zeros(max(L, 1), np.float32) for _ in range(3)]
     oracle().orc_bpla_weights(x.h, *(v.ctypes.data_as(_F) for v in a))
     return [v[:L] for v in a]
+
+
+def stem4d(x: str, bpx, y: str, bpy, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0, model=0,
+           loop=3) -> float:
+    """full_dp of stem_kernel/stem_kernel.cpp:282-351 (x, y as the loader
+    gives them: lowercase)."""
+    def arr(b):
+        if b is None:
+            return None
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        return b.ctypes.data_as(_D) if b.size else np.zeros(1).ctypes.data_as(_D)
+    keep = [np.ascontiguousarray(b, dtype=np.float64) if b is not None else None for b in (bpx, bpy)]
+    px = keep[0].ctypes.data_as(_D) if keep[0] is not None and keep[0].size else None
+    py = keep[1].ctypes.data_as(_D) if keep[1] is not None and keep[1].size else None
+    return oracle().orc_stem4d(x.encode(), px, y.encode(), py, gap, stack, subst, bp_bound,
+                               model, loop)

@@ -922,3 +922,98 @@ double orc_bpla(const orc_mdata *x, const orc_mdata *y, int no_bp, int sw, doubl
   free(w);
   return r;
 }
+
+/* ------------------------------------------------------------------ */
+/* 4-D stem kernel: StemKernel<double,BPMat>::full_dp
+ * (stem_kernel/stem_kernel.cpp:282-351) with dp_init / dp_update (:85-111).
+ * BPMat::prob (:354-421): model 0 = BPMatrix (Vienna pr via PFWrapper; here
+ * the caller's matrix, prob(i,i) = 0), 1 = NormalBasePair, 2 = WobbleBasePair.
+ * Sequences are compared as given (the loader lowercases, example.cpp:33). */
+typedef struct {
+  const char *s;
+  const double *bpp; /* strict upper, packed (model 0) */
+  int n, model;
+  unsigned loop;
+} bp4;
+
+static float bp4_prob(const bp4 *B, int i, int j) {
+  if (B->model == 0) return i < j ? (float)B->bpp[tri_index(B->n, i, j)] : 0.0f;
+  const char a = B->s[i], b = B->s[j];
+  int ok = (a == 'a' && b == 'u') || (a == 'u' && b == 'a') || (a == 'g' && b == 'c') ||
+           (a == 'c' && b == 'g');
+  if (B->model == 2) ok = ok || (a == 'g' && b == 'u') || (a == 'u' && b == 'g');
+  return ((unsigned)i + 1 + B->loop <= (unsigned)j && ok) ? 1.0f : 0.0f;
+}
+
+enum { S_K0 = 0, S_K1, S_K2, S_K3, S_G0, S_G1, S_G2, S_G3 };
+
+double orc_stem4d(const char *x, const double *bpx, const char *y, const double *bpy,
+                  double gap, double stack, double subst, float bp_bound, int model,
+                  unsigned loop) {
+  const int n = (int)strlen(x), m = (int)strlen(y);
+  const double g = gap;
+  bp4 BX = {x, bpx, n, model, loop}, BY = {y, bpy, m, model, loop};
+  /* planes (i,j) of columns j-1 and j; cell (k,l), k<=l, triangular */
+  const size_t cells = (size_t)(m + 1) * (m + 2) / 2;
+  const size_t plane = cells * 8;
+#define CELL(k, l) ((size_t)(l) * ((l) + 1) / 2 + (size_t)(k))
+  double *col[2];
+  col[0] = (double *)calloc((size_t)(n + 1) * plane, sizeof(double));
+  col[1] = (double *)calloc((size_t)(n + 1) * plane, sizeof(double));
+  double result = 0.0;
+  for (int j = 0; j <= n; ++j) {
+    double *cur = col[j & 1], *prv = col[(j + 1) & 1];
+#define DP(C, s, i, k, l) ((C)[(size_t)(i) * plane + (size_t)(s) * cells + CELL(k, l)])
+    /* plane (j,j): K0 = 1, others 0, G0(k,l) = G0(k+1,l)*g */
+    memset(&cur[(size_t)j * plane], 0, plane * sizeof(double));
+    for (size_t c = 0; c < cells; ++c) cur[(size_t)j * plane + S_K0 * cells + c] = 1.0;
+    for (int l = 0; l <= m; ++l) {
+      DP(cur, S_G0, j, l, l) = 1.0;
+      for (int k = l - 1; k >= 0; --k) DP(cur, S_G0, j, k, l) = DP(cur, S_G0, j, k + 1, l) * g;
+    }
+    for (int i = j - 1; i >= 0; --i) {
+      const float bp_ij = bp4_prob(&BX, i, j - 1);
+      memset(&cur[(size_t)i * plane], 0, plane * sizeof(double));
+      for (int l = 0; l <= m; ++l) {
+        DP(cur, S_K0, i, l, l) = 1.0;
+        DP(cur, S_G0, i, l, l) = DP(cur, S_G0, i + 1, l, l) * g;
+        for (int k = l - 1; k >= 0; --k) {
+          /* dp_init (:85-96) */
+          DP(cur, S_K0, i, k, l) = DP(prv, S_K0, i, k, l);
+          DP(cur, S_G0, i, k, l) = DP(prv, S_G0, i, k, l) * g;
+          DP(cur, S_K1, i, k, l) = DP(cur, S_K1, i + 1, k, l);
+          DP(cur, S_G1, i, k, l) = DP(cur, S_G1, i + 1, k, l) * g;
+          DP(cur, S_K2, i, k, l) = DP(cur, S_K2, i, k, l - 1);
+          DP(cur, S_G2, i, k, l) = DP(cur, S_G2, i, k, l - 1) * g;
+          DP(cur, S_K3, i, k, l) = DP(cur, S_K3, i, k + 1, l);
+          DP(cur, S_G3, i, k, l) = DP(cur, S_G3, i, k + 1, l) * g;
+          if (bp_ij > bp_bound) { /* :327-340 */
+            const float bp_kl = bp4_prob(&BY, k, l - 1);
+            if (bp_kl > bp_bound) {
+              const double g0 = DP(prv, S_G0, i + 1, k + 1, l - 1);
+              if (x[i] == y[k] && x[j - 1] == y[l - 1]) {
+                DP(cur, S_K3, i, k, l) += g0 * stack * bp_ij * bp_kl;
+                DP(cur, S_G3, i, k, l) += g0;
+              } else {
+                DP(cur, S_K3, i, k, l) += g0 * stack * subst * bp_ij * bp_kl;
+              }
+            }
+          }
+          /* dp_update (:98-111) */
+          DP(cur, S_K2, i, k, l) += DP(cur, S_K3, i, k, l);
+          DP(cur, S_G2, i, k, l) += DP(cur, S_G3, i, k, l);
+          DP(cur, S_K1, i, k, l) += DP(cur, S_K2, i, k, l);
+          DP(cur, S_G1, i, k, l) += DP(cur, S_G2, i, k, l);
+          DP(cur, S_K0, i, k, l) += DP(cur, S_K1, i, k, l);
+          DP(cur, S_G0, i, k, l) += DP(cur, S_G1, i, k, l);
+        }
+      }
+    }
+    if (j == n) result = DP(cur, S_K0, 0, 0, m);
+#undef DP
+  }
+#undef CELL
+  free(col[0]);
+  free(col[1]);
+  return result;
+}

@@ -99,6 +99,14 @@ double orc_bpla(const orc_mdata *x, const orc_mdata *y, int no_bp, int sw, doubl
  * probabilities per aligned position); example built with use_bp. */
 void orc_bpla_weights(const orc_mdata *d, float *p_left, float *p_right, float *p_unpair);
 
+/* 4-D stem kernel full_dp (stem_kernel/stem_kernel.cpp:282-351) of two
+ * single sequences.  model 0: bpx/bpy are the strict-upper packed bpp of x
+ * and y (PFWrapper pr; prob(i,i)=0); 1/2: NormalBasePair / WobbleBasePair
+ * (:354-396, bpx/bpy unused).  Returns K0(0,|x|,0,|y|). */
+double orc_stem4d(const char *x, const double *bpx, const char *y, const double *bpy,
+                  double gap, double stack, double subst, float bp_bound, int model,
+                  unsigned loop);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,7 +5,7 @@ See include/stem_kernel.h for the ABI and DESIGN.md for the design.
 from ._lib import StemKernelError, lib, default_params  # noqa: F401
 from .kernel_matrix import (  # noqa: F401
     BPLAKernel, Context, Dataset, KernelMatrix, LSuStemKernel, LSuStemStrKernel, NaiveStringKernel, SiStemKernel,
-    SiStemStrKernel, StemStrKernel, StringKernel, SuStemKernel, SuStemStrKernel, fold,
+    SiStemStrKernel, StemKernel4D, StemStrKernel, StringKernel, SuStemKernel, SuStemStrKernel, fold,
     format_libsvm, random_sequences,
 )
 

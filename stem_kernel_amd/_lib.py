@@ -24,7 +24,7 @@ STATUS = {
 
 # sk_kernel_kind
 (SU_STEM, SI_STEM, SU_STR, SI_STR, SU_STEM_STR, SI_STEM_STR, LSU_STEM, LSU_STEM_STR, NAIVE_STR,
- BPLA, LA, BPLA_SW, LA_SW) = range(13)
+ BPLA, LA, BPLA_SW, LA_SW, STEM4D) = range(14)
 
 
 class KernelParams(C.Structure):
@@ -33,6 +33,8 @@ class KernelParams(C.Structure):
         ("loop_gap", C.c_double), ("stack", C.c_double), ("covar", C.c_double),
         ("alpha", C.c_double), ("gap", C.c_double), ("match", C.c_double),
         ("mismatch", C.c_double), ("ext", C.c_double), ("score_table", C.c_double * 16),
+        ("subst", C.c_double), ("bp_bound", C.c_double), ("bp_model", C.c_int32),
+        ("loop", C.c_uint32),
     ]
 
 

@@ -68,6 +68,33 @@ __host__ __device__ inline size_t bpla_wave_lds_bytes(int maxlen) {
   return (b + 15) & ~(size_t)15;
 }
 
+// 4-D stem kernel (stem4d.hip): one pair of a batch
+struct Stem4dPair {
+  int32_t n = 0, m = 0;          // |x|, |y|
+  int64_t plane_doubles = 0;     // per state, padded rows
+  int64_t scratch_off = 0;       // ring of 3 spans x (n+1) planes x 4 states
+  int64_t x_bp = 0, y_bp = 0;    // into bpdiag
+  int64_t x_chr = 0, y_chr = 0;  // into chars
+  int64_t out_index = 0;
+};
+
+struct Stem4dLaunch {
+  const Stem4dPair* pairs = nullptr;
+  const int2* items = nullptr;  // {pair slot, i} of this launch's span d1
+  int64_t n_items = 0;
+  int32_t d1 = 0;
+  double* scratch = nullptr;
+  const float* bpdiag = nullptr;  // per example: prob(a, a+e) by diagonal e
+  const uint8_t* chars = nullptr;  // lowercased sequences
+  const double* gpow = nullptr;   // gap^k
+  double gap = 0.0, stack = 0.0, subst = 0.0;
+  float bp_bound = 0.0f;
+  double* out = nullptr;
+};
+
+int stem4d_cpl(int m);
+hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st);
+
 enum CombineMode : int32_t {
   kCombineStem = 0,      // K = stem
   kCombineStr = 1,       // K = str

@@ -1,0 +1,199 @@
+// 4-D stem kernel on CDNA4 (gfx950).
+//
+// Reference: StemKernel<double,BPMat>::full_dp  stem_kernel/stem_kernel.cpp:282-351,
+//   dp_init / dp_update :85-111, BPMat::prob :354-421.
+//
+// The DP runs over pairs of substrings, x[i,j) and y[k,l): eight states
+// K0..K3, G0..G3 per cell (i,j,k,l).  Dependencies, by x span d1 = j-i and
+// y span d2 = l-k:
+//   K0,G0 <- (i, j-1)          span d1-1, same (k,l)
+//   K1,G1 <- (i+1, j)          span d1-1, same (k,l)
+//   G0    <- (i+1, j-1)        span d1-2, cell (k+1, l-1)   (stacking term)
+//   K2,G2 <- (k, l-1)          same plane, span d2-1
+//   K3,G3 <- (k+1, l)          same plane, span d2-1
+// so one launch per x span d1 computes every plane (i, i+d1) of every pair in
+// the batch in parallel, one WAVEFRONT per plane, sweeping the plane's y
+// spans d2 = 0..m in order.  K2/G2/K3/G3 never leave registers (lane owns
+// CPL consecutive k, the k+1 neighbour of the last one comes from the next
+// lane by DPP); only K0,G0,K1,G1 of each cell go to HBM, once, and are read
+// back once by the next span (72 B per cell: SURVEY.md §8d's roofline).
+//
+// HBM layout of one plane: four state arrays (K0,G0,K1,G1) over cells stored
+// row by row in d2, row d2 holding k = 0..m-d2 padded to a multiple of 4.
+// Per pair, a ring of three span buffers of n+1 planes each.
+#include <hip/hip_runtime.h>
+
+#include "device_set.h"
+#include "launch.h"
+
+namespace sk {
+
+// lane l receives lane l+1's value (lane 63 receives `high`): DPP wave_shl:1
+__device__ __forceinline__ double wave_shl1(double v, double high) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int rlo = __builtin_amdgcn_update_dpp(__double2loint(high), lo, 0x130, 0xf, 0xf, false);
+  const int rhi = __builtin_amdgcn_update_dpp(__double2hiint(high), hi, 0x130, 0xf, 0xf, false);
+  return __hiloint2double(rhi, rlo);
+}
+
+__device__ __forceinline__ int pad4(int v) { return (v + 3) & ~3; }
+
+template <int CPL>
+__global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t it = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (it >= P.n_items) return;
+  const int2 item = P.items[it];  // {pair slot, i}
+  const Stem4dPair pr = P.pairs[item.x];
+  const int i = item.y, d1 = P.d1, j = i + d1;
+  const int n = pr.n, m = pr.m;
+  const int64_t cp = pr.plane_doubles;  // per state
+  double* span_cur = P.scratch + pr.scratch_off + (int64_t)(d1 % 3) * (n + 1) * 4 * cp;
+  double* cur = span_cur + (int64_t)i * 4 * cp;
+  const double g = P.gap;
+  const int k0 = lane * CPL;
+
+  if (d1 == 0) {  // plane (j,j): K0 = 1, G0 = g^(l-k), K1 = G1 = 0  (:297-309)
+    int R = 0;
+    for (int d2 = 0; d2 <= m; ++d2) {
+      const double gd = P.gpow[d2];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int k = k0 + c;
+        if (k <= m - d2) {
+          cur[R + k] = 1.0;
+          cur[cp + R + k] = gd;
+          cur[2 * cp + R + k] = 0.0;
+          cur[3 * cp + R + k] = 0.0;
+        }
+      }
+      R += pad4(m + 1 - d2);
+    }
+    if (n == 0 && lane == 0) P.out[pr.out_index] = 1.0;
+    return;
+  }
+
+  const double* span_p1 = P.scratch + pr.scratch_off + (int64_t)((d1 - 1) % 3) * (n + 1) * 4 * cp;
+  const double* A = span_p1 + (int64_t)i * 4 * cp;        // plane (i, j-1)
+  const double* B = span_p1 + (int64_t)(i + 1) * 4 * cp;  // plane (i+1, j)
+  const double* Cg = nullptr;                              // plane (i+1, j-1), G0
+  if (d1 >= 2)
+    Cg = P.scratch + pr.scratch_off + (int64_t)((d1 - 2) % 3) * (n + 1) * 4 * cp +
+         (int64_t)(i + 1) * 4 * cp + cp;
+  const float* bpx = P.bpdiag + pr.x_bp;  // prob(a, a+e) at e*n - e*(e-1)/2 + a
+  const float* bpy = P.bpdiag + pr.y_bp;
+  const uint8_t* xs = P.chars + pr.x_chr;
+  const uint8_t* ys = P.chars + pr.y_chr;
+  const float bound = P.bp_bound;
+  // bp_ij = prob(i, j-1): diagonal e = j-1-i = d1-1 of x  (:320)
+  const int e1 = d1 - 1;
+  const float bp_ij = bpx[(int64_t)e1 * n - (int64_t)e1 * (e1 - 1) / 2 + i];
+  const bool stack_on = bp_ij > bound;
+  const uint8_t xi = xs[i], xj = xs[j - 1];
+  const double stk = P.stack, sub = P.subst;
+
+  double K2[CPL], G2[CPL], K3[CPL], G3[CPL];
+  uint8_t yk[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    K2[c] = G2[c] = K3[c] = G3[c] = 0.0;
+    const int k = k0 + c;
+    yk[c] = k < m ? ys[k] : 0;
+  }
+
+  // d2 = 0: cells (l,l): K0 = 1, G0 = G0(i+1,j,l,l)*g, K1 = G1 = 0  (:313-316)
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int k = k0 + c;
+    if (k <= m) {
+      cur[k] = 1.0;
+      cur[cp + k] = B[cp + k] * g;
+      cur[2 * cp + k] = 0.0;
+      cur[3 * cp + k] = 0.0;
+    }
+  }
+  int Rm2 = 0, Rm1 = 0, R = pad4(m + 1);  // row offsets of d2-2, d2-1, d2
+  for (int d2 = 1; d2 <= m; ++d2) {
+    // K3/G3 of (k+1, l): my next cell, or the next lane's first (span d2-1)
+    double K3n[CPL], G3n[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL - 1; ++c) {
+      K3n[c] = K3[c + 1];
+      G3n[c] = G3[c + 1];
+    }
+    K3n[CPL - 1] = wave_shl1(K3[0], 0.0);
+    G3n[CPL - 1] = wave_shl1(G3[0], 0.0);
+    const int kmax = m - d2;
+    const int e2 = d2 - 1;  // y diagonal of prob(k, l-1)
+    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int k = k0 + c;
+      if (k <= kmax) {
+        // dp_init (:85-96)
+        double K0 = A[R + k];
+        double G0 = A[cp + R + k] * g;
+        double K1 = B[2 * cp + R + k];
+        double G1 = B[3 * cp + R + k] * g;
+        double k2 = K2[c], g2 = G2[c] * g;
+        double k3 = K3n[c], g3 = G3n[c] * g;
+        if (stack_on) {  // :327-340
+          const float bp_kl = bpy[ye + k];
+          if (bp_kl > bound) {
+            const double g0 = Cg[Rm2 + k + 1];
+            if (xi == yk[c] && xj == ys[k + d2 - 1]) {
+              k3 += g0 * stk * (double)bp_ij * (double)bp_kl;
+              g3 += g0;
+            } else {
+              k3 += g0 * stk * sub * (double)bp_ij * (double)bp_kl;
+            }
+          }
+        }
+        // dp_update (:98-111)
+        k2 += k3;
+        g2 += g3;
+        K1 += k2;
+        G1 += g2;
+        K0 += K1;
+        G0 += G1;
+        cur[R + k] = K0;
+        cur[cp + R + k] = G0;
+        cur[2 * cp + R + k] = K1;
+        cur[3 * cp + R + k] = G1;
+        K2[c] = k2;
+        G2[c] = g2;
+        K3[c] = k3;
+        G3[c] = g3;
+        if (d2 == m && i == 0 && j == n) P.out[pr.out_index] = K0;  // K0(0,n,0,m)
+      }
+    }
+    Rm2 = Rm1;
+    Rm1 = R;
+    R += pad4(m + 1 - d2);
+  }
+  if (m == 0 && i == 0 && j == n && lane == 0) P.out[pr.out_index] = 1.0;
+}
+
+int stem4d_cpl(int m) {
+  if (m + 1 <= 64) return 1;
+  if (m + 1 <= 128) return 2;
+  if (m + 1 <= 256) return 4;
+  if (m + 1 <= 512) return 8;
+  return -1;
+}
+
+hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st) {
+  if (P.n_items == 0) return hipSuccess;
+  const int wpb = 4;
+  const dim3 grid((unsigned)((P.n_items + wpb - 1) / wpb)), block(64 * wpb);
+  switch (cpl) {
+    case 1: hipLaunchKernelGGL(sk_stem4d_kernel<1>, grid, block, 0, st, P); break;
+    case 2: hipLaunchKernelGGL(sk_stem4d_kernel<2>, grid, block, 0, st, P); break;
+    case 4: hipLaunchKernelGGL(sk_stem4d_kernel<4>, grid, block, 0, st, P); break;
+    default: hipLaunchKernelGGL(sk_stem4d_kernel<8>, grid, block, 0, st, P); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace sk

@@ -100,7 +100,14 @@ struct sk_dataset {
   std::string err;
 };
 
+struct Stem4dBatch {
+  sk::Stem4dPair* pairs = nullptr;
+  int2* items = nullptr;
+  size_t cap_pairs = 0, cap_items = 0;
+};
+
 struct sk_context {
+  Stem4dBatch s4d;
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -308,7 +315,8 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
 // ------------------------------------------------------------ parameters
 bool kind_is_bpla(int k) { return k >= SK_BPLA && k <= SK_LA_SW; }
 bool kind_has_stem(int k) {
-  return k != SK_SU_STR && k != SK_SI_STR && k != SK_NAIVE_STR && !kind_is_bpla(k);
+  return k != SK_SU_STR && k != SK_SI_STR && k != SK_NAIVE_STR && !kind_is_bpla(k) &&
+         k != SK_STEM4D;
 }
 bool kind_has_str(int k) {
   return k == SK_SU_STR || k == SK_SI_STR || k == SK_SU_STEM_STR || k == SK_SI_STEM_STR ||
@@ -452,6 +460,185 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   return SK_OK;
 }
 
+// 4-D stem kernel: per example, the lowercased sequence (the loader's
+// ToLower, common/example.cpp:29-36) and BPMat::prob(a, b) for a <= b by
+// diagonal e = b - a (prob(a,a) = 0), as float (stem_kernel.cpp:320, 328).
+void stem4d_tables(const Example& X, const sk_kernel_params* kp, std::vector<float>& bp,
+                   std::vector<uint8_t>& chr) {
+  const int L = X.len;
+  std::string s = X.rows[0];
+  for (char& c : s) c = (char)std::tolower((unsigned char)c);
+  chr.assign(s.begin(), s.end());
+  chr.push_back(0);
+  bp.clear();
+  for (int e = 0; e < L; ++e)
+    for (int a = 0; a + e < L; ++a) {
+      const int b = a + e;
+      float v = 0.0f;
+      if (kp->bp_model == 0) {
+        if (e > 0) v = (float)X.bpp[sk::tri_index(L, a, b)];
+      } else {  // NormalBasePair / WobbleBasePair (stem_kernel.cpp:354-396)
+        const char p = s[a], q = s[b];
+        bool ok = (p == 'a' && q == 'u') || (p == 'u' && q == 'a') || (p == 'g' && q == 'c') ||
+                  (p == 'c' && q == 'g');
+        if (kp->bp_model == 2) ok = ok || (p == 'g' && q == 'u') || (p == 'u' && q == 'g');
+        v = ((unsigned)a + 1 + kp->loop <= (unsigned)b && ok) ? 1.0f : 0.0f;
+      }
+      bp.push_back(v);
+    }
+}
+
+int64_t stem4d_plane_doubles(int m) {
+  int64_t r = 0;
+  for (int d2 = 0; d2 <= m; ++d2) r += ((m + 1 - d2) + 3) & ~3;
+  return r;
+}
+
+int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
+               const int32_t* x, const int32_t* y, int64_t n, double* out_dev) {
+  if (kp->len_band != 0)
+    return fail(ctx, SK_ERR_UNSUPPORTED, "4-D stem kernel: banded partial_dp is not implemented");
+  if (kp->bp_model < 0 || kp->bp_model > 2 || !(kp->bp_bound >= 0.0))
+    return fail(ctx, SK_ERR_INVALID, "4-D stem kernel: bp_model 0..2 and bp_bound >= 0");
+  // per-example tables of the examples this call touches
+  struct Tab { int64_t bp = -1, chr = -1; };
+  std::vector<Tab> tx(xs_->ex.size()), ty(ys_->ex.size());
+  std::vector<float> bpall;
+  std::vector<uint8_t> chall;
+  std::vector<float> bp;
+  std::vector<uint8_t> chr;
+  auto touch = [&](const Example& X, Tab& t) -> int {
+    if (t.bp >= 0) return SK_OK;
+    if (X.n_rows != 1) return fail(ctx, SK_ERR_INVALID, "4-D stem kernel takes single sequences");
+    if (kp->bp_model == 0 && !X.has_bp)
+      return fail(ctx, SK_ERR_INVALID, "4-D stem kernel with bp_model 0 needs base pairs");
+    if (sk::stem4d_cpl(X.len) < 0)
+      return fail(ctx, SK_ERR_UNSUPPORTED, "4-D stem kernel: sequence longer than 511");
+    stem4d_tables(X, kp, bp, chr);
+    t.bp = (int64_t)bpall.size();
+    t.chr = (int64_t)chall.size();
+    bpall.insert(bpall.end(), bp.begin(), bp.end());
+    chall.insert(chall.end(), chr.begin(), chr.end());
+    return SK_OK;
+  };
+  int max_m = 0;
+  double cells = 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    int rc = touch(xs_->ex[x[k]], tx[x[k]]);
+    if (rc) return rc;
+    rc = touch(ys_->ex[y[k]], ty[y[k]]);
+    if (rc) return rc;
+    const double a = xs_->ex[x[k]].len, b = ys_->ex[y[k]].len;
+    max_m = std::max(max_m, (int)b);
+    cells += (a + 1) * (a + 2) / 2 * (b + 1) * (b + 2) / 2;
+  }
+  ctx->last_cells = cells;
+  // batches bounded by scratch memory
+  size_t free_b = 0, total_b = 0;
+  SK_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
+  const double budget = std::min(32e9, 0.5 * (double)free_b);
+  std::vector<int64_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+    return xs_->ex[x[a]].len > xs_->ex[x[b]].len;
+  });
+  const std::vector<double> gp = gap_powers(kp->gap, max_m + 2);
+  // device-side tables for the whole call
+  const size_t nb_bp = std::max<size_t>(bpall.size(), 1), nb_ch = std::max<size_t>(chall.size(), 1);
+  size_t need = nb_bp * 4 + nb_ch + gp.size() * 8 + 4096;
+  int rc = ensure_work(ctx, need);
+  if (rc) return rc;
+  Arena A{static_cast<char*>(ctx->work), 0, ctx->work_bytes};
+  float* d_bp = A.take<float>(nb_bp);
+  uint8_t* d_ch = A.take<uint8_t>(nb_ch);
+  double* d_gp = A.take<double>(gp.size());
+  hipStream_t S = ctx->stream;
+  SK_HIP(ctx, hipMemcpyAsync(d_bp, bpall.data(), bpall.size() * 4, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemcpyAsync(d_ch, chall.data(), chall.size(), hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemcpyAsync(d_gp, gp.data(), gp.size() * 8, hipMemcpyHostToDevice, S));
+  const int cpl = sk::stem4d_cpl(max_m);
+  double total_ms = 0.0;
+  int launches = 0;
+  Stem4dBatch& Bt = ctx->s4d;
+  for (int64_t b0 = 0; b0 < n;) {
+    // pairs of this batch and their scratch
+    std::vector<sk::Stem4dPair> prs;
+    double bytes = 0.0;
+    int64_t b1 = b0;
+    int maxn = 0;
+    while (b1 < n && prs.size() < 4096) {
+      const int64_t q = order[b1];
+      sk::Stem4dPair p;
+      p.n = xs_->ex[x[q]].len;
+      p.m = ys_->ex[y[q]].len;
+      p.plane_doubles = stem4d_plane_doubles(p.m);
+      const double pb = 3.0 * (p.n + 1) * 4.0 * (double)p.plane_doubles * 8.0;
+      if (!prs.empty() && bytes + pb > budget) break;
+      p.scratch_off = (int64_t)(bytes / 8.0);
+      bytes += pb;
+      p.x_bp = tx[x[q]].bp;
+      p.x_chr = tx[x[q]].chr;
+      p.y_bp = ty[y[q]].bp;
+      p.y_chr = ty[y[q]].chr;
+      p.out_index = q;
+      maxn = std::max(maxn, p.n);
+      prs.push_back(p);
+      ++b1;
+    }
+    // work items {pair, i} per span d1, concatenated
+    std::vector<int2> items;
+    std::vector<int64_t> ioff(maxn + 2, 0);
+    for (int d1 = 0; d1 <= maxn; ++d1) {
+      ioff[d1] = (int64_t)items.size();
+      for (size_t p = 0; p < prs.size(); ++p)
+        for (int i = 0; i + d1 <= prs[p].n; ++i) items.push_back(make_int2((int)p, i));
+    }
+    ioff[maxn + 1] = (int64_t)items.size();
+    rc = ensure_scratch(ctx, (size_t)bytes + 64);
+    if (rc) return rc;
+    if (Bt.cap_pairs < prs.size() || Bt.cap_items < items.size()) {
+      if (Bt.pairs) (void)hipFree(Bt.pairs);
+      if (Bt.items) (void)hipFree(Bt.items);
+      Bt.cap_pairs = std::max<size_t>(prs.size(), 64);
+      Bt.cap_items = std::max<size_t>(items.size(), 4096);
+      SK_HIP(ctx, hipMalloc(&Bt.pairs, Bt.cap_pairs * sizeof(sk::Stem4dPair)));
+      SK_HIP(ctx, hipMalloc(&Bt.items, Bt.cap_items * sizeof(int2)));
+    }
+    SK_HIP(ctx, hipMemcpyAsync(Bt.pairs, prs.data(), prs.size() * sizeof(sk::Stem4dPair),
+                               hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(Bt.items, items.data(), items.size() * sizeof(int2),
+                               hipMemcpyHostToDevice, S));
+    sk::Stem4dLaunch L;
+    L.pairs = Bt.pairs;
+    L.scratch = ctx->scratch;
+    L.bpdiag = d_bp;
+    L.chars = d_ch;
+    L.gpow = d_gp;
+    L.gap = kp->gap;
+    L.stack = kp->stack;
+    L.subst = kp->subst;
+    L.bp_bound = (float)kp->bp_bound;
+    L.out = out_dev;
+    SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
+    for (int d1 = 0; d1 <= maxn; ++d1) {
+      L.d1 = d1;
+      L.items = Bt.items + ioff[d1];
+      L.n_items = ioff[d1 + 1] - ioff[d1];
+      SK_HIP(ctx, sk::launch_stem4d(L, cpl, S));
+      ++launches;
+    }
+    SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
+    SK_HIP(ctx, hipStreamSynchronize(S));
+    float ms = 0.f;
+    SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    total_ms += ms;
+    b0 = b1;
+  }
+  ctx->last_stem_ms = total_ms;
+  ctx->last_launches = launches;
+  return SK_OK;
+}
+
 // Core: out_dev[k] = K(xset[x[k]], yset[y[k]]) (device buffer), async.
 int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
               const int32_t* x, const int32_t* y, int64_t n, double* out_dev) {
@@ -461,7 +648,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   rc = check_set(ctx, ys_);
   if (rc) return rc;
   if (n < 0) return fail(ctx, SK_ERR_INVALID, "negative pair count");
-  if (kp->kind < SK_SU_STEM || kp->kind > SK_LA_SW)
+  if (kp->kind < SK_SU_STEM || kp->kind > SK_STEM4D)
     return fail(ctx, SK_ERR_UNSUPPORTED, "unknown kernel kind");
   ctx->last_stem_ms = ctx->last_str_ms = ctx->last_cells = 0.0;
   ctx->last_launches = 0;
@@ -471,6 +658,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     if (x[k] < 0 || x[k] >= nx || y[k] < 0 || y[k] >= ny)
       return fail(ctx, SK_ERR_RANGE, "pair index out of range");
   if (kind_is_bpla(kp->kind)) return run_bpla(ctx, xs_, ys_, kp, x, y, n, out_dev);
+  if (kp->kind == SK_STEM4D) return run_stem4d(ctx, xs_, ys_, kp, x, y, n, out_dev);
 
   const bool stem = kind_has_stem(kp->kind), str = kind_has_str(kp->kind);
   const HostPack& PX = xs_->pack;
@@ -730,6 +918,16 @@ void sk_kernel_params_default(sk_kernel_params* p, int32_t kind) {
                                        -1.390000f, -1.050000f, -1.740000f, 5.276613f};
   for (int k = 0; k < 16; ++k) p->score_table[k] = (double)kBplaTable[k];
   p->ext = (double)-0.75f;
+  // stem_kernel/main.cpp:40-60 (float options; bp_bound default of -p)
+  p->subst = (double)0.5f;
+  p->bp_bound = 0.0;
+  p->bp_model = 0;
+  p->loop = 3;
+  if (kind == SK_STEM4D) {
+    p->gap = (double)0.8f;
+    p->stack = (double)1.0f;
+    p->len_band = 0;
+  }
   if (kind >= SK_BPLA && kind <= SK_LA_SW) {
     p->gap = (double)-8.0f;
     p->alpha = (double)4.5f;
@@ -785,6 +983,8 @@ int sk_close(sk_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->work) (void)hipFree(ctx->work);
+  if (ctx->s4d.pairs) (void)hipFree(ctx->s4d.pairs);
+  if (ctx->s4d.items) (void)hipFree(ctx->s4d.items);
   for (hipEvent_t e : {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3})
     if (e) (void)hipEventDestroy(e);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -140,6 +140,25 @@ class BPLAKernel(_Kernel):
         super().__init__(**kw)
 
 
+class StemKernel4D(_Kernel):
+    """StemKernel<double,BPMat>(use_GU, loop, gap, stack, subst, band,
+    ali_bound, bp_bound) of stem_kernel/ (stem_kernel.h:26-60), full_dp
+    (stem_kernel.cpp:282-351) over single sequences.
+
+    bp_model 0 is the CLI's default -p path (BPMatrix: the dataset's base-pair
+    probabilities, pairs counted when p > bp_bound); 1/2 are NormalBasePair /
+    WobbleBasePair (-w), which the CLI runs with bp_bound 1.0 (so K = 1).
+    Options are float on the CLI (stem_kernel/main.cpp:40-60) and are rounded
+    to float32 here like the CLI would."""
+    kind = _lib.STEM4D
+
+    def __init__(self, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0, bp_model=0, loop=3,
+                 cli_float=True):
+        f = (lambda v: float(np.float32(v))) if cli_float else float
+        super().__init__(gap=f(gap), stack=f(stack), subst=f(subst), bp_bound=f(bp_bound),
+                         bp_model=int(bp_model), loop=int(loop), len_band=0)
+
+
 class SiStemStrKernel(_Kernel):
     """SiStemStrKernel(loop_gap, stack, covar, gap, match, mismatch, len_band)
     def_kernel.h:285-311 (--no-ribosum)."""
