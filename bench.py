@@ -1,24 +1,28 @@
 #!/usr/bin/env python3
-"""Benchmark: stem-kernel Gram matrix (north star) on MI355X.
+"""Benchmark of the stem-kernel Gram engine on MI355X.
 
-Workload (BASELINE.json north_star / metric): the 4096 x 4096 Gram matrix of
-SuStemStrKernel (== StemStrKernel of stem_kernel_lite/ss_kernel.h: DAG stem
-kernel + profile string kernel, default parameters of
-stem_kernel_lite/main.cpp:103-149) over synthetic RNA sequences of L = 200 nt
-(splitmix64 sequences, Nussinov-Boltzmann base-pairing probabilities,
---basepair 0.01).  Units are Gram cells K(i,j), i <= j, exactly the cells the
-reference evaluates (common/kernel_matrix.cpp:44-55): 8,390,656 sequence pairs.
+Default workload (BASELINE.json north_star / metric, ``--config ns``): the
+4096 x 4096 Gram matrix of SuStemStrKernel (== StemStrKernel of
+stem_kernel_lite/ss_kernel.h: DAG stem kernel + profile string kernel,
+default parameters of stem_kernel_lite/main.cpp:103-149) over synthetic RNA
+sequences of L = 200 nt (splitmix64 sequences, Nussinov-Boltzmann
+base-pairing probabilities, --basepair 0.01).  Units are Gram cells K(i,j),
+i <= j, exactly the cells the reference evaluates
+(common/kernel_matrix.cpp:44-55): 8,390,656 sequence pairs.
 
 A *step* is one slice of that upper triangle: the pairs are dealt round-robin
-into S = --slices equal slices (default 64, ~131k pairs each), so every
-slice has the same cost mix.  With N GPUs (one process per GPU, RCCL), rank r
-computes slice (step*N + r) -- per-GPU work is fixed, so scaling is weak -- and
-the ranks all-gather the step's Gram entries over RCCL (the reference
-gathered to rank 0 with MPI point-to-point, kernel_matrix.cpp:225-261).
---full runs every slice of the Gram once (whole job).
+into S equal slices, so every slice has the same cost mix.  With N GPUs (one
+process per GPU, RCCL), rank r computes slice (step*N + r) -- per-GPU work is
+fixed, so scaling is weak -- and the ranks all-gather the step's Gram entries
+over RCCL (the reference gathered to rank 0 with MPI point-to-point,
+kernel_matrix.cpp:225-261).  --full runs every slice of the Gram once.
 
-Timed region: inputs (packed DAGs) already resident in HBM; each step = the
-DAG stem DP + string DP + combine epilogue for the slice + the all-gather.
+Other SURVEY.md §8 configurations (--config): c2 ss_kernel 256 x L150,
+c3 4-D stem kernel 1024 x L200, c4 BPLA 2048 alignments L~200, c5 DAG stem
+8192 x L300.  They print the same JSON line for their own kernel.
+
+Timed region: inputs (packed examples) already resident in HBM; each step =
+the kernel launches for the slice + the all-gather.
 """
 from __future__ import annotations
 
@@ -33,8 +37,17 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-CONFIG_ID = 2           # seed 0x5EED0000 + config id (north star shares C3's L)
+PEAK_HBM_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+PEAK_FP64_TFS = 78.6    # FP64 vector
+
+# name -> kernel, n examples, length, slices, config id (seed 0x5EED0000+id)
+CONFIGS = {
+    "ns": dict(kernel="ss", n=4096, L=200, slices=64, cid=2, cpu_pairs=12288),
+    "c2": dict(kernel="ss", n=256, L=150, slices=4, cid=1, cpu_pairs=12288),
+    "c3": dict(kernel="stem4d", n=1024, L=200, slices=2050, cid=2, cpu_pairs=32),
+    "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=16, cid=3, cpu_pairs=32768),
+    "c5": dict(kernel="stem", n=8192, L=300, slices=1024, cid=4, cpu_pairs=4096),
+}
 
 
 def parse():
@@ -42,17 +55,60 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=4096, help="number of sequences")
-    ap.add_argument("--length", type=int, default=200)
-    ap.add_argument("--slices", type=int, default=64)
+    ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=None, help="number of examples")
+    ap.add_argument("--length", type=int, default=None)
+    ap.add_argument("--slices", type=int, default=None)
     ap.add_argument("--full", action="store_true", help="time every slice (whole Gram)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-pairs", type=int, default=12288, help="pairs in the CPU sample (~15 s on 16 cores)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "stem_traffic.json"))
+    ap.add_argument("--cpu-pairs", type=int, default=None, help="pairs in the CPU sample")
+    ap.add_argument("--pmc-json", default=None)
     return ap.parse_args()
 
 
-def algorithmic_bytes(shapes, x, y):
+# ------------------------------------------------------------------ inputs
+def c4_alignments(n, lo, hi, rows, seed):
+    """SURVEY.md §8d C4 generator: per alignment a seed sequence of length
+    U[lo,hi], rows with 10% point substitutions and 5% gap characters."""
+    import stem_kernel_amd as ska
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi + 1, size=n)
+    base = ska.random_sequences(n, hi, seed)
+    out = []
+    acgu = np.frombuffer(b"ACGU", np.uint8)
+    for k in range(n):
+        s = np.frombuffer(base[k][: lens[k]].encode(), np.uint8)
+        aln = []
+        for _ in range(rows):
+            u = rng.random(s.size)
+            r = s.copy()
+            sub = (u >= 0.05) & (u < 0.15)
+            r[sub] = acgu[rng.integers(0, 4, size=int(sub.sum()))]
+            r[u < 0.05] = ord("-")
+            aln.append(r.tobytes().decode())
+        out.append(aln)
+    return out
+
+
+def build_inputs(cfg, a):
+    import stem_kernel_amd as ska
+    seed = 0x5EED0000 + cfg["cid"]
+    threads = min(16, os.cpu_count() or 1)
+    if cfg["kernel"] == "bpla":
+        alns = c4_alignments(a.n, cfg["L"][0], cfg["L"][1], cfg["rows"], seed)
+        return alns, ska.Dataset.synthetic_alignments(alns, th=0.01, threads=threads)
+    seqs = ska.random_sequences(a.n, a.length, seed)
+    return seqs, ska.Dataset.synthetic(seqs, th=0.01, threads=threads)
+
+
+def make_kernel(kind):
+    import stem_kernel_amd as ska
+    return {"ss": ska.SuStemStrKernel, "stem": ska.SuStemKernel, "stem4d": ska.StemKernel4D,
+            "bpla": ska.BPLAKernel}[kind]()
+
+
+# ------------------------------------------------------------------ rooflines
+def dag_bytes(shapes, x, y):
     """SURVEY.md §8(d) DAG-stem model per pair:
     B = 32*|Vx|*|Vy| + S(x) + S(y) + 8,  S = 20|V| + 8|E| + 8|F| + 4L."""
     V, E, F, L = shapes[:, 0], shapes[:, 1], shapes[:, 2], shapes[:, 4]
@@ -60,7 +116,29 @@ def algorithmic_bytes(shapes, x, y):
     return float(np.sum(32.0 * V[x] * V[y] + S[x] + S[y] + 8.0))
 
 
-def cpu_baseline(seqs, n_pairs, seed=7):
+def stem4d_cells(lens, x, y):
+    n, m = lens[x].astype(np.float64), lens[y].astype(np.float64)
+    return float(np.sum((n + 1) * (n + 2) / 2 * (m + 1) * (m + 2) / 2))
+
+
+def roofline(kind, shapes, x, y, ms):
+    """(bound, achieved, unit, peak, model, algorithmic work of the launches)."""
+    lens = shapes[:, 4]
+    if kind in ("ss", "stem"):
+        b = dag_bytes(shapes, x, y)
+        return "hbm", b / (ms * 1e-3) / 1e9, "GB/s", PEAK_HBM_GBS, \
+            "SURVEY §8d: 32*|Vx|*|Vy| + S(x) + S(y) + 8 bytes per pair", b
+    if kind == "stem4d":
+        b = 72.0 * stem4d_cells(lens, x, y)
+        return "hbm", b / (ms * 1e-3) / 1e9, "GB/s", PEAK_HBM_GBS, \
+            "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", b
+    f = 24.0 * float(np.sum(lens[x].astype(np.float64) * lens[y]))
+    return "valu", f / (ms * 1e-3) / 1e12, "TFLOP/s", PEAK_FP64_TFS, \
+        "SURVEY §8d: 24 flop per cell (exp counted as 1), Lx*Ly cells", f
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_baseline(cfg, data, n_pairs, seed=7):
     """The C oracle (plain-C restatement of the reference kernels, oracle/)
     on a bounded random sample of the same Gram's pairs, host threads."""
     from concurrent.futures import ThreadPoolExecutor
@@ -68,29 +146,52 @@ def cpu_baseline(seqs, n_pairs, seed=7):
     import stem_kernel_amd as ska
     from oracle import pyoracle as po
     rng = np.random.default_rng(seed)
-    idx = rng.choice(len(seqs), size=min(len(seqs), 48), replace=False)
-    om = {int(i): po.OMData([seqs[i]], [ska.fold(seqs[i])], 0.01) for i in idx}
+    kind = cfg["kernel"]
+    npool = min(len(data), 48)
+    idx = [int(i) for i in rng.choice(len(data), size=npool, replace=False)]
+    kern = make_kernel(kind)
+    p = kern.params
+    if kind == "stem4d":
+        prep = {i: (data[i].lower(), ska.fold(data[i])) for i in idx}
+
+        def one(ab):
+            (xa, bx), (xb, by) = prep[ab[0]], prep[ab[1]]
+            return po.stem4d(xa, bx, xb, by, p.gap, p.stack, p.subst, p.bp_bound, p.bp_model,
+                             p.loop)
+    else:
+        def om_of(i):
+            rows = data[i] if isinstance(data[i], list) else [data[i]]
+            return po.OMData(rows, [ska.fold(r.replace("-", "")) for r in rows], 0.01)
+        om = {i: om_of(i) for i in idx}
+
+        def one(ab):
+            return po.kernel_value(p.kind, om[ab[0]], om[ab[1]], p)
     pairs = []
     while len(pairs) < n_pairs:
         a, b = sorted(rng.choice(idx, size=2))
         pairs.append((int(a), int(b)))
-    p = ska.SuStemStrKernel().params
     cores = max(1, min(16, os.cpu_count() or 1))
-
-    def one(ab):
-        return po.kernel_value(p.kind, om[ab[0]], om[ab[1]], p)
-
     t = time.perf_counter()
     with ThreadPoolExecutor(cores) as ex:  # ctypes releases the GIL
         list(ex.map(one, pairs))
     dt = time.perf_counter() - t
+    what = {"ss": "SuStemStrKernel", "stem": "SuStemKernel", "stem4d": "4-D StemKernel full_dp",
+            "bpla": "BPLAKernel"}[kind]
     return {"value": n_pairs / dt, "unit": "sequence-pairs/sec", "cores": cores, "kind": "port",
-            "sample": f"{n_pairs} random pairs (i<=j) among 48 of the {len(seqs)} L={len(seqs[0])} "
-                      f"sequences, SuStemStrKernel via the C oracle, {dt:.1f}s wall"}
+            "sample": f"{n_pairs} random pairs (i<=j) among {npool} of the {len(data)} examples, "
+                      f"{what} via the C oracle on {cores} threads, {dt:.1f}s wall"}
 
 
+# ------------------------------------------------------------------ main
 def main():
     a = parse()
+    cfg = CONFIGS[a.config]
+    a.n = a.n or cfg["n"]
+    if a.length is None:
+        a.length = cfg["L"] if isinstance(cfg["L"], int) else cfg["L"][1]
+    a.slices = a.slices or cfg["slices"]
+    a.cpu_pairs = a.cpu_pairs or cfg["cpu_pairs"]
+    kind = cfg["kernel"]
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -106,8 +207,7 @@ def main():
 
     # ---- inputs (identical on every rank), built on host threads
     t0 = time.perf_counter()
-    seqs = ska.random_sequences(a.n, a.length, 0x5EED0000 + CONFIG_ID)
-    ds = ska.Dataset.synthetic(seqs, th=0.01, threads=min(16, os.cpu_count() or 1))
+    data, ds = build_inputs(cfg, a)
     t_build = time.perf_counter() - t0
     stream = torch.cuda.current_stream(dev)
     ctx = ska.Context(local, stream=stream.cuda_stream)
@@ -116,7 +216,7 @@ def main():
     torch.cuda.synchronize(dev)
     t_upload = time.perf_counter() - t0
     shapes = np.array([ds.shape(i) for i in range(a.n)], dtype=np.float64)
-    kern = ska.SuStemStrKernel()
+    kern = make_kernel(kind)
 
     iu, ju = np.triu_indices(a.n)
     iu = iu.astype(np.int32)
@@ -125,7 +225,7 @@ def main():
     n_slices_needed = (a.warmup + a.steps) * world
     if a.full:
         S = max(world, S)
-        a.steps = S // world
+        a.steps = -(-S // world)
         a.warmup = 0
         n_slices_needed = S
     if n_slices_needed > S:
@@ -135,20 +235,16 @@ def main():
     out = torch.empty(per, dtype=torch.float64, device=dev)
     gathered = torch.empty(per * world, dtype=torch.float64, device=dev)
 
-    stem_ms = []
-    cells = []
-    alg_bytes = []
-    pairs_done = 0
-
     def run_step(step):
-        nonlocal pairs_done
         sl = step * world + rank
         x, y = slice_of(sl % S)
+        if a.full and sl >= S:
+            x, y = x[:0], y[:0]
         ctx.pairs_device(ds, kern, x, y, out.data_ptr())
         tm = ctx.last_timing()
         if dist_on:
             dist.all_gather_into_tensor(gathered, out)
-        return x.size, tm
+        return x, y, tm
 
     for w in range(a.warmup):
         run_step(w)
@@ -158,13 +254,14 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     local_pairs = 0
+    k_ms, work, cells, launches = [], [], [], []
     for k in range(a.steps):
-        n_p, tm = run_step(a.warmup + k)
-        local_pairs += n_p
-        stem_ms.append(tm["stem_ms"])
-        x, y = slice_of(((a.warmup + k) * world + rank) % S)
-        alg_bytes.append(algorithmic_bytes(shapes, x, y))
+        x, y, tm = run_step(a.warmup + k)
+        local_pairs += x.size
+        k_ms.append(tm["stem_ms"])
         cells.append(tm["cells"])
+        launches.append(tm["launches"])
+        work.append((x, y))
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
@@ -183,22 +280,36 @@ def main():
 
     if rank == 0:
         value = total_pairs / elapsed
-        # dominant kernel: DAG stem DP, per launch (one launch per step)
-        st_ms = float(np.mean(stem_ms))
-        ach = float(np.mean(alg_bytes)) / (st_ms * 1e-3) / 1e9
+        # dominant kernel (stem / 4-D / BPLA), per launch, HIP events on the
+        # launch stream (sk_last_timing)
+        tot_ms = float(np.sum(k_ms))
+        xs = np.concatenate([w[0] for w in work])
+        ys = np.concatenate([w[1] for w in work])
+        bound, ach, unit, peak, model, alg = roofline(kind, shapes, xs, ys, tot_ms)
+        n_launch = max(1, int(np.sum(launches)))
         traffic = None
+        pmc_json = a.pmc_json or os.path.join(ROOT, "profiles", f"{kind}_traffic.json")
         try:
-            with open(a.pmc_json) as f:
+            with open(pmc_json) as f:
                 pm = json.load(f)
-            if pm.get("length") == a.length:
-                traffic = pm["hbm_bytes_per_cell"] * float(np.mean(cells))
+            if pm.get("length") == a.length and pm.get("kernel") == kind:
+                traffic = pm["hbm_bytes_per_cell"] * float(np.sum(cells)) / n_launch
         except Exception:
             pass
         cpu = None
         if not a.no_cpu_baseline:
-            cpu = cpu_baseline(seqs, a.cpu_pairs)
+            cpu = cpu_baseline(cfg, data, a.cpu_pairs)
+        kname = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
+                 "stem4d": "sk_stem4d_kernel", "bpla": "sk_bpla_kernel"}[kind]
+        kdesc = {
+            "ss": "SuStemStrKernel(alpha=0.2,beta=0.3,loop_gap=0.2,gap=0.8,band=10)",
+            "stem": "SuStemKernel(beta=0.3,loop_gap=0.2,band=10)",
+            "stem4d": "StemKernel<double,BPMatrix>(gap=0.8,stack=1.0,subst=0.5,bp_bound=0) full_dp",
+            "bpla": "BPLAKernel(gap=-8,ext=-0.75,alpha=4.5,beta=0.11)"}[kind]
+        metric = "sequence-pairs/sec (Gram entries/s) at L=200 nt" if a.config == "ns" else \
+            f"sequence-pairs/sec ({a.config})"
         line = {
-            "metric": "sequence-pairs/sec (Gram entries/s) at L=200 nt",
+            "metric": metric,
             "value": value,
             "unit": "sequence-pairs/sec",
             "n_gpus": world,
@@ -212,21 +323,20 @@ def main():
             "data": "synthetic (splitmix64 ACGU sequences, Nussinov-Boltzmann bpp stand-in for "
                     "ViennaRNA; no checkpoints)",
             "config": {
-                "workload": f"{a.n}x{a.n} SuStemStrKernel (ss_kernel) Gram, L={a.length}, "
+                "workload": f"{a.config}: {a.n}x{a.n} {kdesc} Gram, L={cfg['L']}, "
                             f"step = 1/{S} of the {iu.size} upper-triangle pairs per GPU",
-                "n_sequences": a.n, "length": a.length, "pairs_per_step_per_gpu": per,
-                "kernel": "SuStemStrKernel(alpha=0.2,beta=0.3,loop_gap=0.2,gap=0.8,band=10)",
-                "basepair_th": 0.01, "parallelism": f"gram-slices x{world} (RCCL all-gather)",
+                "n_sequences": a.n, "length": cfg["L"], "pairs_per_step_per_gpu": per,
+                "kernel": kdesc, "basepair_th": 0.01,
+                "parallelism": f"gram-slices x{world} (RCCL all-gather)",
                 "mean_nodes": float(shapes[:, 0].mean()), "mean_edges": float(shapes[:, 1].mean()),
                 "mean_bpfreq": float(shapes[:, 2].mean()),
                 "host_build_s": round(t_build, 2), "upload_s": round(t_upload, 3),
             },
             "roofline": {
-                "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": ach / PEAK_HBM_GBS,
-                "traffic": traffic,
-                "kernel": "sk_dag_stem_kernel", "kernel_ms_per_launch": st_ms,
-                "model": "SURVEY §8d: 32*|Vx|*|Vy| + S(x) + S(y) + 8 bytes per pair",
+                "bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
+                "traffic": traffic, "kernel": kname,
+                "kernel_ms_per_launch": tot_ms / n_launch, "launches": n_launch,
+                "algorithmic_per_launch": alg / n_launch, "model": model,
             },
             "cpu_baseline": cpu,
         }

@@ -127,6 +127,12 @@ int sk_dataset_add(sk_dataset *ds, const char *label, int n_rows,
  * (common/framework.h:308-353 + DataLoader<MData>::get). */
 int sk_dataset_add_synthetic(sk_dataset *ds, int32_t n, const char *const *seqs,
                              const char *const *labels, float th, int32_t n_threads);
+/* Same for alignments: n examples of n_rows equal-length rows each, rows
+ * [i*n_rows + r]; every row is folded gap-erased and lowercased, then the
+ * per-row matrices are averaged (common/bpmatrix.cpp:306-342, 399-417). */
+int sk_dataset_add_synthetic_rows(sk_dataset *ds, int32_t n, int32_t n_rows,
+                                  const char *const *rows, const char *const *labels,
+                                  float th, int32_t n_threads);
 int sk_dataset_size(const sk_dataset *ds);
 /* label of example i (pointer valid while ds lives) */
 const char *sk_dataset_label(const sk_dataset *ds, int i);

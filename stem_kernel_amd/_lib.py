@@ -57,6 +57,8 @@ SIGNATURES = {
                                  C.POINTER(_F64P), C.c_float, C.c_int]),
     "sk_dataset_add_synthetic": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_char_p),
                                            C.POINTER(C.c_char_p), C.c_float, C.c_int32]),
+    "sk_dataset_add_synthetic_rows": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_char_p),
+                                                C.POINTER(C.c_char_p), C.c_float, C.c_int32]),
     "sk_dataset_size": (C.c_int, [_P]),
     "sk_dataset_label": (C.c_char_p, [_P, C.c_int]),
     "sk_dataset_shape": (C.c_int, [_P, C.c_int, _I32P, _I32P, _I32P, _I32P, _I32P]),

@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
   const int n = pr.n, m = pr.m;
   const int64_t cp = pr.plane_doubles;  // per state
   double* span_cur = P.scratch + pr.scratch_off + (int64_t)(d1 % 3) * (n + 1) * 4 * cp;
-  double* cur = span_cur + (int64_t)i * 4 * cp;
+  double* __restrict__ cur = span_cur + (int64_t)i * 4 * cp;
   const double g = P.gap;
   const int k0 = lane * CPL;
 
@@ -75,8 +75,8 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
   }
 
   const double* span_p1 = P.scratch + pr.scratch_off + (int64_t)((d1 - 1) % 3) * (n + 1) * 4 * cp;
-  const double* A = span_p1 + (int64_t)i * 4 * cp;        // plane (i, j-1)
-  const double* B = span_p1 + (int64_t)(i + 1) * 4 * cp;  // plane (i+1, j)
+  const double* __restrict__ A = span_p1 + (int64_t)i * 4 * cp;        // plane (i, j-1)
+  const double* __restrict__ B = span_p1 + (int64_t)(i + 1) * 4 * cp;  // plane (i+1, j)
   const double* Cg = nullptr;                              // plane (i+1, j-1), G0
   if (d1 >= 2)
     Cg = P.scratch + pr.scratch_off + (int64_t)((d1 - 2) % 3) * (n + 1) * 4 * cp +
@@ -113,8 +113,53 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
       cur[3 * cp + k] = 0.0;
     }
   }
+  // Row d2's inputs are prefetched during row d2-1 (they do not depend on
+  // it): K0,G0 of (i,j-1), K1,G1 of (i+1,j), and, for the stacking term,
+  // prob_y(k, l-1) and G0(i+1,j-1) at (k+1, l-1).
+  double pK0[CPL], pG0[CPL], pK1[CPL], pG1[CPL], pGs[CPL];
+  float pbp[CPL];
+  uint8_t pyl[CPL];
   int Rm2 = 0, Rm1 = 0, R = pad4(m + 1);  // row offsets of d2-2, d2-1, d2
+  auto fetch = [&](int d2, int Rd, int Rd2) {
+    const int kmax = m - d2;
+    const int e2 = d2 - 1;
+    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int k = k0 + c;
+      pbp[c] = 0.0f;
+      pGs[c] = 0.0;
+      pyl[c] = 0;
+      if (k <= kmax) {
+        pK0[c] = A[Rd + k];
+        pG0[c] = A[cp + Rd + k];
+        pK1[c] = B[2 * cp + Rd + k];
+        pG1[c] = B[3 * cp + Rd + k];
+        if (stack_on) {
+          pbp[c] = bpy[ye + k];
+          pyl[c] = ys[k + d2 - 1];
+          if (d2 >= 2) pGs[c] = Cg[Rd2 + k + 1];
+        }
+      }
+    }
+  };
+  if (m >= 1) fetch(1, R, 0);
   for (int d2 = 1; d2 <= m; ++d2) {
+    double cK0[CPL], cG0[CPL], cK1[CPL], cG1[CPL], cGs[CPL];
+    float cbp[CPL];
+    uint8_t cyl[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      cK0[c] = pK0[c];
+      cG0[c] = pG0[c];
+      cK1[c] = pK1[c];
+      cG1[c] = pG1[c];
+      cGs[c] = pGs[c];
+      cbp[c] = pbp[c];
+      cyl[c] = pyl[c];
+    }
+    const int Rn = R + pad4(m + 1 - d2);
+    if (d2 + 1 <= m) fetch(d2 + 1, Rn, Rm1);
     // K3/G3 of (k+1, l): my next cell, or the next lane's first (span d2-1)
     double K3n[CPL], G3n[CPL];
 #pragma unroll
@@ -125,24 +170,22 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
     K3n[CPL - 1] = wave_shl1(K3[0], 0.0);
     G3n[CPL - 1] = wave_shl1(G3[0], 0.0);
     const int kmax = m - d2;
-    const int e2 = d2 - 1;  // y diagonal of prob(k, l-1)
-    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + c;
       if (k <= kmax) {
         // dp_init (:85-96)
-        double K0 = A[R + k];
-        double G0 = A[cp + R + k] * g;
-        double K1 = B[2 * cp + R + k];
-        double G1 = B[3 * cp + R + k] * g;
+        double K0 = cK0[c];
+        double G0 = cG0[c] * g;
+        double K1 = cK1[c];
+        double G1 = cG1[c] * g;
         double k2 = K2[c], g2 = G2[c] * g;
         double k3 = K3n[c], g3 = G3n[c] * g;
         if (stack_on) {  // :327-340
-          const float bp_kl = bpy[ye + k];
+          const float bp_kl = cbp[c];
           if (bp_kl > bound) {
-            const double g0 = Cg[Rm2 + k + 1];
-            if (xi == yk[c] && xj == ys[k + d2 - 1]) {
+            const double g0 = cGs[c];
+            if (xi == yk[c] && xj == cyl[c]) {
               k3 += g0 * stk * (double)bp_ij * (double)bp_kl;
               g3 += g0;
             } else {
@@ -170,7 +213,7 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
     }
     Rm2 = Rm1;
     Rm1 = R;
-    R += pad4(m + 1 - d2);
+    R = Rn;
   }
   if (m == 0 && i == 0 && j == n && lane == 0) P.out[pr.out_index] = 1.0;
 }

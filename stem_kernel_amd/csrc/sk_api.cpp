@@ -1022,9 +1022,10 @@ int sk_dataset_add(sk_dataset* ds, const char* label, int n_rows, const char* co
   return SK_OK;
 }
 
-int sk_dataset_add_synthetic(sk_dataset* ds, int32_t n, const char* const* seqs,
-                             const char* const* labels, float th, int32_t n_threads) {
-  if (!ds || n < 0 || (n > 0 && !seqs)) return SK_ERR_INVALID;
+int sk_dataset_add_synthetic_rows(sk_dataset* ds, int32_t n, int32_t n_rows,
+                                  const char* const* rows, const char* const* labels, float th,
+                                  int32_t n_threads) {
+  if (!ds || n < 0 || n_rows < 1 || (n > 0 && !rows)) return SK_ERR_INVALID;
   if (ds->uploaded) return SK_ERR_INVALID;
   const size_t base = ds->ex.size();
   try {
@@ -1037,21 +1038,25 @@ int sk_dataset_add_synthetic(sk_dataset* ds, int32_t n, const char* const* seqs,
   nt = std::max(1, std::min(nt, std::max<int32_t>(n, 1)));
   std::atomic<int32_t> next(0), status(SK_OK);
   auto work = [&]() {
-    std::vector<double> bpp;
+    std::vector<std::vector<double>> bpp(n_rows);
+    std::vector<const double*> bptr(n_rows);
     for (;;) {
       const int32_t i = next.fetch_add(1);
       if (i >= n || status.load() != SK_OK) return;
       try {
-        const char* s = seqs[i];
-        const int L = (int)std::strlen(s);
-        // fold the gap-erased, lower-cased row (common/bpmatrix.cpp:404-414)
-        std::string row;
-        for (int k = 0; k < L; ++k)
-          if (s[k] != '-') row.push_back((char)std::tolower((unsigned char)s[k]));
-        bpp.assign(row.size() > 1 ? row.size() * (row.size() - 1) / 2 : 1, 0.0);
-        sk::fold_nussinov(row.c_str(), (int)row.size(), false, bpp.data());
-        const double* b = bpp.data();
-        sk::build_example(ds->ex[base + i], 1, &s, &b, th, true);
+        const char* const* ex_rows = rows + (size_t)i * n_rows;
+        for (int32_t r = 0; r < n_rows; ++r) {
+          const char* s = ex_rows[r];
+          const int L = (int)std::strlen(s);
+          // fold the gap-erased, lower-cased row (common/bpmatrix.cpp:404-414)
+          std::string row;
+          for (int k = 0; k < L; ++k)
+            if (s[k] != '-') row.push_back((char)std::tolower((unsigned char)s[k]));
+          bpp[r].assign(row.size() > 1 ? row.size() * (row.size() - 1) / 2 : 1, 0.0);
+          sk::fold_nussinov(row.c_str(), (int)row.size(), false, bpp[r].data());
+          bptr[r] = bpp[r].data();
+        }
+        sk::build_example(ds->ex[base + i], n_rows, ex_rows, bptr.data(), th, true);
       } catch (...) {
         status.store(SK_ERR_INVALID);
       }
@@ -1066,6 +1071,11 @@ int sk_dataset_add_synthetic(sk_dataset* ds, int32_t n, const char* const* seqs,
     ds->labels.resize(base);
   }
   return status.load();
+}
+
+int sk_dataset_add_synthetic(sk_dataset* ds, int32_t n, const char* const* seqs,
+                             const char* const* labels, float th, int32_t n_threads) {
+  return sk_dataset_add_synthetic_rows(ds, n, 1, seqs, labels, th, n_threads);
 }
 
 int sk_dataset_size(const sk_dataset* ds) { return ds ? (int)ds->ex.size() : 0; }

@@ -251,6 +251,22 @@ class Dataset:
         check(lib().sk_dataset_add_synthetic(ds._h, n, sarr, larr, C.c_float(th), threads))
         return ds
 
+    @classmethod
+    def synthetic_alignments(cls, alns: Sequence[Sequence[str]], labels=None, th: float = 0.01,
+                             threads: int = 0):
+        """Alignments with the same row count: fold every row on host threads."""
+        ds = cls()
+        n = len(alns)
+        nr = len(alns[0]) if n else 1
+        if any(len(a) != nr for a in alns):
+            raise ValueError("synthetic_alignments needs the same number of rows per alignment")
+        flat = [r.encode() for a in alns for r in a]
+        rarr = (C.c_char_p * max(len(flat), 1))(*flat)
+        larr = None if labels is None else (C.c_char_p * n)(*[l.encode() for l in labels])
+        check(lib().sk_dataset_add_synthetic_rows(ds._h, n, nr, rarr, larr, C.c_float(th),
+                                                  threads))
+        return ds
+
     def __len__(self):
         return lib().sk_dataset_size(self._h)
 

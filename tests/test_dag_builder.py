@@ -60,3 +60,17 @@ def test_fold_is_probability():
         M[np.triu_indices(n, 1)] = b
         M = M + M.T
         assert np.all(b >= 0) and np.all(M.sum(axis=1) <= 1 + 1e-12)
+
+
+def test_synthetic_alignments_match_per_example_build():
+    """sk_dataset_add_synthetic_rows (threaded) == sk_dataset_add per example."""
+    from tests.helpers import make_examples, mutate_alignment
+    base = ska.random_sequences(3, 60, 9)
+    alns = [mutate_alignment(b, 3, i) for i, b in enumerate(base)]
+    ds = ska.Dataset.synthetic_alignments(alns, threads=3)
+    ds2, _ = make_examples(alns)
+    for i in range(3):
+        a, b = ds.dag(i), ds2.dag(i)
+        assert all(np.array_equal(a[k], b[k]) for k in a)
+        for u, v in zip(ds.bpla_weights(i), ds2.bpla_weights(i)):
+            assert np.array_equal(u, v)

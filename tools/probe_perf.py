@@ -13,9 +13,12 @@ ds = ska.Dataset.from_sequences(seqs, th=0.01)
 print(f"build {N} examples: {time.time()-t:.2f}s", flush=True)
 ctx = ska.Context(0)
 ctx.upload(ds)
-kern = {"stem": ska.SuStemKernel(), "str": ska.StringKernel(), "ss": ska.SuStemStrKernel()}[kind]
+kern = {"stem": ska.SuStemKernel(), "str": ska.StringKernel(), "ss": ska.SuStemStrKernel(),
+        "bpla": ska.BPLAKernel(), "la": ska.BPLAKernel(noBP=True), "stem4d": ska.StemKernel4D()}[kind]
 iu = np.triu_indices(N)
 x, y = iu[0].astype(np.int32), iu[1].astype(np.int32)
+if len(sys.argv) > 4:  # limit the pair count (4-D kernel)
+    x, y = x[: int(sys.argv[4])], y[: int(sys.argv[4])]
 for rep in range(2):
     t = time.time()
     v = ctx.pairs(ds, kern, x, y)
