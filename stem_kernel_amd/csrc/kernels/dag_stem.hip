@@ -21,6 +21,8 @@
 // (persistent grid).  No MFMA: this is a recurrence, not a contraction.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "device_set.h"
 #include "launch.h"
 
@@ -60,17 +62,24 @@ __global__ void sk_prep_kernel(DevSet s, DevParamNodes pn, const double* __restr
 }
 
 // ---------------------------------------------------------------------------
+// LDS (address space 3) pointer types: every access below is a ds_* op,
+// whatever the register allocator does with the view structs.
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+
 struct YView {  // the y example staged in LDS
-  const uint32_t* b;   // len:16 | bpf_beg:16
-  const uint32_t* c;   // loop gaps
-  const float* w;
-  const float* nbp;
-  const double* P;
-  const uint2* ed;
-  const uint32_t* bc;
-  const float* bp;
-  const int32_t* lv;   // level -> first node
-  const int32_t* lve;  // level -> first edge
+  const lds_u32* b;   // len:16 | bpf_beg:16
+  const lds_u32* c;   // loop gaps
+  const lds_f32* w;
+  const lds_f32* nbp;
+  const lds_f64* P;
+  const lds_u32* ed;  // child:11 | parent:11 | gaps:10
+  const lds_u32* bc;
+  const lds_f32* bp;
+  const lds_i32* lv;   // level -> first node
+  const lds_i32* lve;  // level -> first edge
   int nl, nlev;
   float nseqs;
 };
@@ -98,11 +107,10 @@ __device__ __forceinline__ void wave_sync() {
 
 // node_score(xx,yy,i,j): score_table.cpp:343-380 (Subst) / 193-232 (Simple);
 // co[] holds exp(beta*ribosum) or the match/mismatch table.
-__device__ __forceinline__ double match_node_score(const double* __restrict__ co,
-                                                   const DevSet& s, int xbb, int xb0, int xnb,
-                                                   const YView& Y, int yb0, int ynb, double xwg,
-                                                   double ywg, double x_nbp, double y_nbp,
-                                                   double x_nseq) {
+__device__ __forceinline__ double match_node_score(const lds_f64* co, const DevSet& s, int xbb,
+                                                int xb0, int xnb, const YView& Y, int yb0, int ynb,
+                                                double xwg, double ywg, double x_nbp, double y_nbp,
+                                                double x_nseq) {
   double v = 0.0;
   for (int a = 0; a < xnb; ++a) {
     const double cx = (double)s.bpf_p[xbb + xb0 + a];
@@ -119,29 +127,29 @@ __device__ __forceinline__ double match_node_score(const double* __restrict__ co
 
 // One (x,y) pair on one wavefront.
 //
-// Rows p of G0 (x non-leaf nodes) are produced in the reference's post-order
-// (x_order), each into a recycled HBM row slot (nd_slot; 0xffff = never read,
-// not stored).  Lane l owns the y nodes q = l + 64k (k < MAXK) for phases A,
-// B and D; their y-structure fields are hoisted into registers per item.
+// Rows p of G0 (x non-leaf nodes) are produced in the reference's post-order,
+// each into a recycled HBM row slot (0xffff = never read, not stored).  Lane
+// l owns the y nodes q = l + 64k, k < kused = ceil(|Vy|/64) (wave-uniform);
+// rows are padded to a multiple of 64 in LDS and in the slab, so the per-k
+// loops need no lane predicates (padded q are masked by selects only where
+// they could reach a valid value).
 //
 // Both x-child sums of the reference are linear in the child rows, so one
 // weighted row suffices:   S[q] = sum_{c in ch(p)} g^gaps(p,c) * G0[c][q]
 //   IX term   : sum_c G0[c][q] * v_s(p) * g^gaps = v_s(p) * S[q]
 //   MATCH sum : sum_c sum_cy g^gx g^gy G0[c][cy] = sum_{cy in ch(q)} g^gy S[cy]
 // For a stem row p:
-//   A. stream the child rows from HBM (coalesced, pipelined) into S (regs);
-//      S -> per-wave LDS row R; H[k] = sum_{cy in ch(q)} g^gy R[cy] (in band);
+//   A. stream the child rows from HBM (coalesced) into S (registers);
+//      S -> per-wave LDS row R; H[k] = sum_{cy in ch(q)} g^gy R[cy] (band);
 //   B. M[q] = node_score(p,q) * H (closed forms for loop nodes) -> R (G1);
 //      K += P_x[p] * sum_q M[q] P_y[q];
 //   C. IY sweep over the y levels, edge-parallel: G1[q] += G1[cy]*w(q,cy)
 //      with w = gap^2*w_y(q)*g^gaps precomputed per item (LDS f64 atomics);
 //   D. G0[p][q] = G1[q] + v_s(p)*S[k] -> slot of p.
 template <int MAXK>
-__device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t (&qe)[MAXK],
-                            const uint32_t (&ql)[MAXK / 2], double* __restrict__ R,
-                            const double* __restrict__ yew, const double* __restrict__ co,
-                            const double* __restrict__ gp, double* __restrict__ slab, int x,
-                            int lane) {
+__device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
+                            const lds_f64* co, const lds_f64* gp, const lds_u32* ya,
+                            double* __restrict__ slab, int x, int lane, int kused, int stride) {
   const DevSet& s = P.xset;
   const int nlx = s.ex_nl[x];
   const int NLy = Y.nl;
@@ -152,6 +160,9 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
   const int nloop_y = Y.lv[1];  // level 0 = loop nodes
   const double gap2 = P.gap2;
   const int band = (int)P.band;
+  const XRow* __restrict__ xrows = s.xrow + xnb;
+  const double* __restrict__ xsl = P.pn.xr_SL + xnb;
+  const uint32_t* __restrict__ xch = s.xr_ch;
   double kacc = 0.0;
 #ifdef SK_STAMPS
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -159,18 +170,17 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
 #endif
 
   // x-row header and first child records, prefetched one row ahead
-  uint32_t na = s.xr_a[xnb], nbw = s.xr_b[xnb], nc = s.xr_c[xnb];
-  float nw = s.xr_w[xnb], nnbp = s.xr_nbp[xnb], nbp0 = s.xr_bp0[xnb];
-  double nP = s.xr_P[xnb], nSL = P.pn.xr_SL[xnb];
+  XRow nx = xrows[0];
+  double nSL = xsl[0];
   uint32_t nch[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) nch[j] = s.xr_ch[chp + j];
+  for (int j = 0; j < 4; ++j) nch[j] = xch[chp + j];
 
   for (int r = 0; r < nlx; ++r) {
-    const uint32_t xa = na, xb = nbw, xc = nc;
-    const double xwg = gap2 * (double)nw;
-    const double x_nbp = (double)nnbp;
-    const double xP = nP, xSL = nSL, xpf = (double)nbp0;
+    const uint32_t xa = nx.a, xb = nx.b, xc = nx.c;
+    const double xwg = gap2 * (double)nx.w;
+    const double x_nbp = (double)nx.nbp;
+    const double xP = nx.P, xSL = nSL, xpf = (double)nx.bp0;
     uint32_t ch[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) ch[j] = nch[j];
@@ -178,16 +188,10 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
     const int chp_r = chp;
     chp += xne;
     if (r + 1 < nlx) {
-      na = s.xr_a[xnb + r + 1];
-      nbw = s.xr_b[xnb + r + 1];
-      nc = s.xr_c[xnb + r + 1];
-      nw = s.xr_w[xnb + r + 1];
-      nnbp = s.xr_nbp[xnb + r + 1];
-      nbp0 = s.xr_bp0[xnb + r + 1];
-      nP = s.xr_P[xnb + r + 1];
-      nSL = P.pn.xr_SL[xnb + r + 1];
+      nx = xrows[r + 1];
+      nSL = xsl[r + 1];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) nch[j] = s.xr_ch[chp + j];
+      for (int j = 0; j < 4; ++j) nch[j] = xch[chp + j];
     }
     const int xlen = xb & 0xffff;
     const uint32_t pslot = xb >> 16;
@@ -197,13 +201,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
     // single bp-frequency entry of x (the common single-sequence case)
     const bool x_one = xnbf == 1 && x_nbp == 0.0;
     const uint32_t xcode = (xc >> 16) * 16u;
-    // band mask of my y nodes for this row
-    uint32_t inb = 0;
-#pragma unroll
-    for (int k = 0; k < MAXK; ++k) {
-      const int dl = xlen - (int)((ql[k >> 1] >> (16 * (k & 1))) & 0xffff);
-      if (qe[k] != 0xffffffffu && (band == 0 || (dl < 0 ? -dl : dl) <= band)) inb |= 1u << k;
-    }
     STAMP(0);
 
     // ---- A: S = sum_c g^gaps G0[c][*]  (coalesced HBM row streams)
@@ -211,17 +208,15 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) S[k] = 0.0;
     for (int t = 0; t < xne; t += 2) {
-      const uint32_t c0 = t < 4 ? ch[t] : s.xr_ch[chp_r + t];
+      const uint32_t c0 = t < 4 ? ch[t] : xch[chp_r + t];
       const bool two = t + 1 < xne;
-      const uint32_t c1 = two ? (t + 1 < 4 ? ch[t + 1] : s.xr_ch[chp_r + t + 1]) : c0;
+      const uint32_t c1 = two ? (t + 1 < 4 ? ch[t + 1] : xch[chp_r + t + 1]) : c0;
       const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
-      const double* __restrict__ r0 = slab + (size_t)(c0 & 0xffff) * NLy;
-      const double* __restrict__ r1 = slab + (size_t)(c1 & 0xffff) * NLy;
+      const double* __restrict__ r0 = slab + (size_t)(c0 & 0xffff) * stride + lane;
+      const double* __restrict__ r1 = slab + (size_t)(c1 & 0xffff) * stride + lane;
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k) {
-        const int q = lane + 64 * k;
-        if (q < NLy) S[k] += eg0 * r0[q] + eg1 * r1[q];
-      }
+      for (int k = 0; k < MAXK; ++k)
+        if (k < kused) S[k] += eg0 * r0[64 * k] + eg1 * r1[64 * k];
     }
     STAMP(1);
     double H[MAXK];
@@ -229,39 +224,39 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
     for (int k = 0; k < MAXK; ++k) H[k] = 0.0;
     if (!xloop) {
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k) {
-        const int q = lane + 64 * k;
-        if (q < NLy) R[q] = S[k];
-      }
+      for (int k = 0; k < MAXK; ++k)
+        if (k < kused) R[lane + 64 * k] = S[k];
       wave_sync();
-      // MATCH sums over y-children: up to 4 edges per node in one predicated
-      // pass (all LDS reads independent), longer edge lists after it
-      uint32_t more = 0;
+      // MATCH sums over y-children: up to 4 edges per node in one pass with
+      // selects (reads past a node's edges stay inside the padded edge
+      // array), longer edge lists after it
+      bool more = false;
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) {
-        const int q = lane + 64 * k;
-        const bool on = (inb >> k & 1u) && q >= nloop_y;
-        const int e0 = qe[k] & 0xffff, ne = on ? (int)((qe[k] >> 16) & 0xff) : 0;
-        double acc = 0.0;
+        if (k < kused) {
+          const uint32_t a = ya[lane + 64 * k];
+          const int e0 = a & 0xffff, ne = (a >> 16) & 0xff;
+          double acc = 0.0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (j < ne) {
-            const uint32_t f = Y.ed[e0 + j].x;
-            acc += gp[f >> 16] * R[f & 0xffff];
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t f = Y.ed[e0 + j];
+            const double v = gp[f >> 22] * R[f & 0x7ff];
+            acc += j < ne ? v : 0.0;
           }
+          H[k] = acc;
+          more |= ne > 4;
         }
-        H[k] = acc;
-        if (ne > 4) more |= 1u << k;
       }
-      if (__builtin_amdgcn_read_exec() && __any(more != 0)) {
+      if (__any(more)) {
 #pragma unroll
         for (int k = 0; k < MAXK; ++k) {
-          if (more >> k & 1u) {
-            const int e0 = qe[k] & 0xffff, ne = (qe[k] >> 16) & 0xff;
+          if (k < kused) {
+            const uint32_t a = ya[lane + 64 * k];
+            const int e0 = a & 0xffff, ne = (a >> 16) & 0xff;
             double acc = H[k];
             for (int j = 4; j < ne; ++j) {
-              const uint32_t f = Y.ed[e0 + j].x;
-              acc += gp[f >> 16] * R[f & 0xffff];
+              const uint32_t f = Y.ed[e0 + j];
+              acc += gp[f >> 22] * R[f & 0x7ff];
             }
             H[k] = acc;
           }
@@ -275,32 +270,24 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
     double rowk = 0.0;
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) {
-      const int q = lane + 64 * k;
-      if (q < NLy) {
-        double M = 0.0;
-        if (inb >> k & 1u) {
-          double Hq;
-          if (q < nloop_y) {
-            const double egy = gp[Y.c[q]];
-            Hq = xloop ? xeg0 * egy : xSL * egy;
-          } else {
-            Hq = H[k];
-          }
-          if (Hq != 0.0) {
-            const uint32_t e = qe[k], b = Y.b[q];
-            const float ynbp = Y.nbp[q];
-            double vs;
-            if (x_one && (e >> 24) == 1u && ynbp == 0.0f) {
-              // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:350-364)
-              vs = co[xcode + Y.bc[b >> 16]] * xpf * (double)Y.bp[b >> 16];
-            } else {
-              const double ywg = gap2 * (double)Y.w[q];
-              vs = match_node_score(co, s, xbb, xb0, xnbf, Y, b >> 16, e >> 24, xwg, ywg, x_nbp,
-                                    (double)ynbp, x_nseq);
-            }
-            M = vs * Hq;
-          }
+      if (k < kused) {
+        const int q = lane + 64 * k;
+        const uint32_t bq = Y.b[q];
+        const int dl = xlen - (int)(bq & 0xffff);
+        const bool inb = q < NLy && (band == 0 || (dl < 0 ? -dl : dl) <= band);
+        const double egy = gp[Y.c[q]];
+        const double Hq = q < nloop_y ? (xloop ? xeg0 : xSL) * egy : H[k];
+        const uint32_t a = ya[q];
+        const float ynbp = Y.nbp[q];
+        double vs = co[xcode + Y.bc[bq >> 16]] * xpf * (double)Y.bp[bq >> 16];
+        const bool fast = x_one && (a >> 24) == 1u && ynbp == 0.0f;
+        if (!fast && inb && Hq != 0.0) {
+          // general bp-frequency lists / gap columns (score_table.cpp:343-380)
+          const double ywg = gap2 * (double)Y.w[q];
+          vs = match_node_score(co, s, xbb, xb0, xnbf, Y, bq >> 16, a >> 24, xwg, ywg, x_nbp,
+                                (double)ynbp, x_nseq);
         }
+        const double M = inb ? vs * Hq : 0.0;
         R[q] = M;
         rowk += M * Y.P[q];
       }
@@ -313,27 +300,33 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
     //         Level bounds are read two levels ahead and edge records one
     //         level ahead, so only the R reads stay on the dependency chain.
     if (Y.nlev > 1) {
+      // IY weight of an edge: node gap score of the parent * g^gaps (the
+      // reference multiplies G1[child]*v_s*e_s, stem_kernel.cpp:96-102)
       int fa = Y.lve[1], fb = Y.lve[2];
       int fc = Y.lve[Y.nlev > 2 ? 3 : 2];
-      uint2 rec = make_uint2(0, 0);
+      uint32_t rec = 0;
       double w = 0.0;
       if (fa + lane < fb) {
         rec = Y.ed[fa + lane];
-        w = yew[fa + lane];
+        w = gap2 * (double)Y.w[(rec >> 11) & 0x7ff] * gp[rec >> 22];
       }
       for (int l = 1; l < Y.nlev; ++l) {
         // next level [fb, fc); level after next ends at fd
         const int fd = (l + 3 <= Y.nlev) ? Y.lve[l + 3] : fc;
-        uint2 rec2 = make_uint2(0, 0);
+        uint32_t rec2 = 0;
         double w2 = 0.0;
         if (fb + lane < fc) {
           rec2 = Y.ed[fb + lane];
-          w2 = yew[fb + lane];
+          w2 = gap2 * (double)Y.w[(rec2 >> 11) & 0x7ff] * gp[rec2 >> 22];
         }
-        if (fa + lane < fb) atomicAdd(&R[rec.y], R[rec.x & 0xffff] * w);
+        if (fa + lane < fb)
+          __hip_atomic_fetch_add(&R[(rec >> 11) & 0x7ff], R[rec & 0x7ff] * w, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WAVEFRONT);
         for (int f = fa + 64 + lane; f < fb; f += 64) {  // levels with > 64 edges
-          const uint2 rr = Y.ed[f];
-          atomicAdd(&R[rr.y], R[rr.x & 0xffff] * yew[f]);
+          const uint32_t rr = Y.ed[f];
+          const double wr = gap2 * (double)Y.w[(rr >> 11) & 0x7ff] * gp[rr >> 22];
+          __hip_atomic_fetch_add(&R[(rr >> 11) & 0x7ff], R[rr & 0x7ff] * wr, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
         wave_sync();
         fa = fb;
@@ -349,12 +342,10 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
     // Every later read of element q of this row is by the same lane (q =
     // lane + 64k), so per-thread program order makes it visible: no fence.
     if (pslot != 0xffffu) {
-      double* __restrict__ orow = slab + (size_t)pslot * NLy;
+      double* __restrict__ orow = slab + (size_t)pslot * stride + lane;
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k) {
-        const int q = lane + 64 * k;
-        if (q < NLy) orow[q] = R[q] + xwg * S[k];
-      }
+      for (int k = 0; k < MAXK; ++k)
+        if (k < kused) orow[64 * k] = R[lane + 64 * k] + xwg * S[k];
     }
     wave_sync();
     STAMP(5);
@@ -371,35 +362,42 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, const uint32_t 
   return kacc;
 }
 
+// Workgroup size bound per register template: MAXK <= 16 keeps <= 168 VGPRs,
+// so 12 waves (3 per SIMD) fit; the wider templates need up to 256.
 template <int MAXK>
-__global__ void __launch_bounds__(512) sk_dag_stem_kernel(StemLaunch P) {
+struct StemWaves {
+  static constexpr int value = MAXK <= 16 ? 12 : 8;
+};
+
+template <int MAXK>
+__global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kernel(StemLaunch P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const DevSet& s = P.yset;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
-  const int maxnl = P.lds_max_nl;
+  const int maxnl = P.lds_max_nl;  // multiple of 64
 
   // LDS carve (every region a multiple of 16 bytes)
-  double* co = reinterpret_cast<double*>(smem);             // 256
-  double* gp = co + 256;                                     // n_gpow_pad
-  double* yP = gp + P.n_gpow_pad;                            // maxnl
-  double* Rall = yP + maxnl;                                 // nwaves*maxnl
-  double* yew = Rall + (size_t)nwaves * maxnl;               // lds_max_edges
-  uint2* yed = reinterpret_cast<uint2*>(yew + P.lds_max_edges);  // lds_max_edges
-  uint32_t* yb = reinterpret_cast<uint32_t*>(yed + P.lds_max_edges);
-  uint32_t* yc = yb + maxnl;
-  float* yw = reinterpret_cast<float*>(yc + maxnl);
-  float* ynbp = yw + maxnl;
-  uint32_t* ybc = reinterpret_cast<uint32_t*>(ynbp + maxnl);  // lds_max_bpf
-  float* ybp = reinterpret_cast<float*>(ybc + P.lds_max_bpf);
-  int32_t* ylv = reinterpret_cast<int32_t*>(ybp + P.lds_max_bpf);  // lds_max_nlev_pad
-  int32_t* ylve = ylv + P.lds_max_nlev_pad;                   // lds_max_nlev_pad
-  int32_t* ctl = ylve + P.lds_max_nlev_pad;                   // 4 ints
+  lds_f64* co = (lds_f64*)(smem);                             // 256
+  lds_f64* gp = co + 256;                                     // n_gpow_pad
+  lds_f64* yP = gp + P.n_gpow_pad;                            // maxnl
+  lds_f64* Rall = yP + maxnl;                                 // nwaves*maxnl
+  lds_u32* yed = (lds_u32*)(Rall + (size_t)nwaves * maxnl);   // lds_max_edges (mult. of 4)
+  lds_u32* ya = yed + P.lds_max_edges;                        // maxnl
+  lds_u32* yb = ya + maxnl;
+  lds_u32* yc = yb + maxnl;
+  lds_f32* yw = (lds_f32*)(yc + maxnl);
+  lds_f32* ynbp = yw + maxnl;
+  lds_u32* ybc = (lds_u32*)(ynbp + maxnl);                    // lds_max_bpf
+  lds_f32* ybp = (lds_f32*)(ybc + P.lds_max_bpf);
+  lds_i32* ylv = (lds_i32*)(ybp + P.lds_max_bpf);             // lds_max_nlev_pad
+  lds_i32* ylve = ylv + P.lds_max_nlev_pad;                   // lds_max_nlev_pad
+  lds_i32* ctl = ylve + P.lds_max_nlev_pad;                   // 4 ints
 
   for (int k = threadIdx.x; k < 256; k += blockDim.x) co[k] = P.co_subst[k];
   for (int k = threadIdx.x; k < P.n_gpow; k += blockDim.x) gp[k] = P.gpow[k];
 
-  double* R = Rall + (size_t)wave * maxnl;
+  lds_f64* R = Rall + (size_t)wave * maxnl;
   double* slab = P.scratch + (size_t)(blockIdx.x * nwaves + wave) * P.slab_doubles;
   const double gap2 = P.gap2;
 
@@ -418,26 +416,33 @@ __global__ void __launch_bounds__(512) sk_dag_stem_kernel(StemLaunch P) {
     Y.nlev = s.ex_nlev[y];
     Y.nseqs = s.ex_nseqs[y];
     const int nb = s.ex_node_base[y], eb = s.ex_edge_base[y], bb = s.ex_bpf_base[y];
+    const int kused = (Y.nl + 63) >> 6;
+    const int stride = kused * 64;
     {
       const int ne = s.ex_edge_base[y + 1] - eb, nbf = s.ex_bpf_base[y + 1] - bb;
       const int lb = s.ex_lvl_base[y];
-      for (int k = threadIdx.x; k < Y.nl; k += blockDim.x) {
-        yb[k] = s.nd_b[nb + k];
-        yc[k] = s.nd_c[nb + k];
-        yw[k] = s.nd_w[nb + k];
-        ynbp[k] = s.nd_nbp[nb + k];
-        yP[k] = s.nd_P[nb + k];
+      // node fields, zero padded to a multiple of 64 (padded q: no edges)
+      for (int k = threadIdx.x; k < stride; k += blockDim.x) {
+        const bool v = k < Y.nl;
+        ya[k] = v ? s.nd_a[nb + k] : 0u;
+        yb[k] = v ? s.nd_b[nb + k] : 0u;
+        yc[k] = v ? s.nd_c[nb + k] : 0u;
+        yw[k] = v ? s.nd_w[nb + k] : 0.0f;
+        ynbp[k] = v ? s.nd_nbp[nb + k] : 0.0f;
+        yP[k] = v ? s.nd_P[nb + k] : 0.0;
       }
-      for (int k = threadIdx.x; k < ne; k += blockDim.x) {
-        const uint2 rec = s.ed[eb + k];
-        yed[k] = rec;
-        // IY weight of the edge: node gap score of the parent * g^gaps (the
-        // reference multiplies G1[child]*v_s*e_s, stem_kernel.cpp:96-102)
-        yew[k] = gap2 * (double)s.nd_w[nb + rec.y] * gp[rec.x >> 16];
+      // edges (+4 padding records: the predicated gather reads past the end)
+      for (int k = threadIdx.x; k < ne + 4; k += blockDim.x) {
+        if (k < ne) {
+          const uint2 rec = s.ed[eb + k];  // {child | gaps<<16, parent}
+          yed[k] = (rec.x & 0x7ffu) | ((rec.y & 0x7ffu) << 11) | ((rec.x >> 16) << 22);
+        } else {
+          yed[k] = 0u;
+        }
       }
-      for (int k = threadIdx.x; k < nbf; k += blockDim.x) {
-        ybc[k] = s.bpf_code[bb + k];
-        ybp[k] = s.bpf_p[bb + k];
+      for (int k = threadIdx.x; k < nbf + 1; k += blockDim.x) {
+        ybc[k] = k < nbf ? s.bpf_code[bb + k] : 0u;
+        ybp[k] = k < nbf ? s.bpf_p[bb + k] : 0.0f;
       }
       for (int k = threadIdx.x; k <= Y.nlev; k += blockDim.x) {
         const int q = s.lvl[lb + k];
@@ -448,21 +453,12 @@ __global__ void __launch_bounds__(512) sk_dag_stem_kernel(StemLaunch P) {
     }
     Y.b = yb; Y.c = yc; Y.w = yw; Y.nbp = ynbp; Y.P = yP;
     Y.ed = yed; Y.bc = ybc; Y.bp = ybp; Y.lv = ylv; Y.lve = ylve;
-    uint32_t qe[MAXK], ql[MAXK / 2];
-#pragma unroll
-    for (int k = 0; k < MAXK / 2; ++k) ql[k] = 0;
-#pragma unroll
-    for (int k = 0; k < MAXK; ++k) {
-      const int q = lane + 64 * k;
-      qe[k] = q < Y.nl ? s.nd_a[nb + q] : 0xffffffffu;
-      if (q < Y.nl) ql[k >> 1] |= (s.nd_b[nb + q] & 0xffffu) << (16 * (k & 1));
-    }
     __syncthreads();
 
     // static round-robin of the item's pairs over the waves (uniform loop)
     for (int t = wave_u; t < item.z; t += nwaves) {
       const int x = P.xs[item.y + t];
-      const double k = stem_pair<MAXK>(P, Y, qe, ql, R, yew, co, gp, slab, x, lane);
+      const double k = stem_pair<MAXK>(P, Y, R, co, gp, ya, slab, x, lane, kused, stride);
       if (lane == 0) P.out[P.oidx[item.y + t]] = k;
     }
   }
@@ -484,8 +480,8 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += (size_t)P.n_gpow_pad * 8;
   b += (size_t)P.lds_max_nl * 8;                   // yP
   b += (size_t)nwaves * P.lds_max_nl * 8;          // one row per wave
-  b += (size_t)P.lds_max_edges * 16;               // yew + yed
-  b += (size_t)P.lds_max_nl * 16;                  // yb,yc,yw,ynbp
+  b += (size_t)P.lds_max_edges * 4;                // packed edges
+  b += (size_t)P.lds_max_nl * 20;                  // ya,yb,yc,yw,ynbp
   b += (size_t)P.lds_max_bpf * 8;
   b += (size_t)P.lds_max_nlev_pad * 8;
   b += 16;
@@ -525,7 +521,7 @@ hipError_t launch_stem(const StemLaunch& P, int grid, int nwaves, hipStream_t st
   return hipGetLastError();
 }
 
-hipError_t stem_kernel_attr(int max_nl, int* max_dyn_lds, int* vgprs) {
+hipError_t stem_kernel_attr(int max_nl, int* max_dyn_lds, int* vgprs, int* max_waves) {
   hipFuncAttributes attr;
   const int maxk = stem_maxk(max_nl);
   if (maxk < 0) return hipErrorInvalidValue;
@@ -533,6 +529,7 @@ hipError_t stem_kernel_attr(int max_nl, int* max_dyn_lds, int* vgprs) {
   if (e != hipSuccess) return e;
   *max_dyn_lds = 163840 - (int)attr.sharedSizeBytes;
   *vgprs = attr.numRegs;
+  *max_waves = std::max(1, attr.maxThreadsPerBlock / 64);
   return hipSuccess;
 }
 

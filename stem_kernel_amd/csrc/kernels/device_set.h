@@ -12,6 +12,18 @@
 namespace sk {
 
 
+// x-role row header (post-order row r of an example)
+struct XRow {
+  uint32_t a;    // n_ch:8 | n_bpf:8 | loop leaf-edge gaps:16
+  uint32_t b;    // len:16 | out slot:16 (0xffff = row never read)
+  uint32_t c;    // bpf_beg_local:16 | code of first bp entry:8
+  float w;       // node weight
+  float nbp;     // profile gap count at node.first
+  float bp0;     // p of the first bp entry
+  double P;      // root->node path count
+};
+static_assert(sizeof(XRow) == 32, "XRow is one 32-byte scalar load");
+
 struct DevSet {
   int32_t n_examples = 0;
   // per example (n_examples entries; *_base are absolute indices)
@@ -50,14 +62,8 @@ struct DevSet {
   // its children are xr_ch[ex_xch_base[e] + sum of earlier rows' n_ch ...].
   const int32_t* ex_nslots = nullptr;   // recycled HBM row slots this example needs
   const int32_t* ex_xch_base = nullptr; // into xr_ch
-  const uint32_t* xr_a = nullptr;  // n_ch:8 | n_bpf:8 | loop leaf-edge gaps:16
-  const uint32_t* xr_b = nullptr;  // len:16 | out slot:16 (0xffff = row never read)
-  const uint32_t* xr_c = nullptr;  // bpf_beg_local:16 | code of first bp entry:8
+  const XRow* xrow = nullptr;       // one 32-B record per row (wave-uniform scalar load)
   const uint32_t* xr_node = nullptr;  // level-order node id (for nd_SL)
-  const float* xr_w = nullptr;
-  const float* xr_nbp = nullptr;
-  const float* xr_bp0 = nullptr;   // p of the first bp entry
-  const double* xr_P = nullptr;
   const uint32_t* xr_ch = nullptr;  // per child edge: child slot:16 | gaps:16
   // maxima over the set
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;

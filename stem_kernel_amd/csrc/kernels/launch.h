@@ -107,7 +107,7 @@ hipError_t launch_prep(const DevSet& s, const DevParamNodes& pn, const double* g
                        hipStream_t st);
 size_t stem_lds_bytes(const StemLaunch& P, int nwaves);
 hipError_t launch_stem(const StemLaunch& P, int grid, int nwaves, hipStream_t st);
-hipError_t stem_kernel_attr(int max_nl, int* max_dyn_lds, int* vgprs);
+hipError_t stem_kernel_attr(int max_nl, int* max_dyn_lds, int* vgprs, int* max_waves);
 int stem_maxk(int max_nl);
 
 size_t str_lds_bytes(const StrLaunch& P, int nwaves);

@@ -80,9 +80,8 @@ struct HostPack {
   std::vector<uint8_t> pos_chr;
   std::vector<float4> pos_lru;
   std::vector<int32_t> ex_nslots, ex_xch_base;
-  std::vector<uint32_t> xr_a, xr_b, xr_c, xr_node, xr_ch;
-  std::vector<float> xr_w, xr_nbp, xr_bp0;
-  std::vector<double> xr_P;
+  std::vector<sk::XRow> xrow;
+  std::vector<uint32_t> xr_node, xr_ch;
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
 };
 
@@ -210,8 +209,9 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       if (!loop) {
         for (uint32_t t = e0; t < e1; ++t) {
           const int c = nid[X.edge_to[t]];
-          if (c < 0 || X.edge_gaps[t] > 0xffff) {
-            err = c < 0 ? "unexpected DAG shape: stem with a leaf child" : "gap count exceeds 16 bits";
+          if (c < 0 || X.edge_gaps[t] > 1023) {
+            // the stem kernel packs an edge as child:11 | parent:11 | gaps:10
+            err = c < 0 ? "unexpected DAG shape: stem with a leaf child" : "gap count exceeds 1023";
             return SK_ERR_UNSUPPORTED;
           }
           P.ed.push_back(make_uint2((uint32_t)c | (X.edge_gaps[t] << 16), (uint32_t)k));
@@ -266,18 +266,18 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
           }
           slot[v] = (uint32_t)sl;
         }
-        const uint32_t bloc = (uint32_t)nid[v];  // placeholder, fixed below
-        (void)bloc;
-        P.xr_a.push_back(nch | ((b1 - b0) << 8) | ((loop ? X.edge_gaps[e0] : 0u) << 16));
-        P.xr_b.push_back((X.last[v] - X.first[v]) | (slot[v] << 16));
-        P.xr_node.push_back((uint32_t)nid[v]);
-        P.xr_w.push_back(X.weight[v]);
-        P.xr_nbp.push_back(X.prof5[(size_t)X.first[v] * 5 + 4]);
-        P.xr_bp0.push_back(b1 > b0 ? X.bpf_p[b0] : 0.0f);
-        P.xr_P.push_back(Pw[v]);
+        sk::XRow xr;
+        xr.a = nch | ((b1 - b0) << 8) | ((loop ? X.edge_gaps[e0] : 0u) << 16);
+        xr.b = (X.last[v] - X.first[v]) | (slot[v] << 16);
+        xr.w = X.weight[v];
+        xr.nbp = X.prof5[(size_t)X.first[v] * 5 + 4];
+        xr.bp0 = b1 > b0 ? X.bpf_p[b0] : 0.0f;
+        xr.P = Pw[v];
         // bpf_beg in the level-order bpf array of this example (see nd_b)
-        P.xr_c.push_back((P.nd_b[P.ex_node_base.back() + nid[v]] >> 16) |
-                         ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16));
+        xr.c = (P.nd_b[P.ex_node_base.back() + nid[v]] >> 16) |
+               ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16);
+        P.xrow.push_back(xr);
+        P.xr_node.push_back((uint32_t)nid[v]);
       }
       if (nslots >= 0xffff) {
         err = "too many live DAG rows";
@@ -665,13 +665,20 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   const HostPack& PY = ys_->pack;
 
   // ---- host-side work lists
-  // stem items: pairs grouped by y, chunks, largest first
+  // stem items: pairs grouped by y, chunks, largest first, in classes by the
+  // y example's register template (MAXK = 64-node slots per lane): one
+  // launch per class, each sized (LDS, waves) for its own largest y
+  struct StemClass {
+    int maxk = 0;
+    int max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0;
+    int nwaves = 1, grid = 1;
+    size_t item_off = 0, n_items = 0;
+  };
+  std::vector<StemClass> classes;
   std::vector<int4> items;
   std::vector<int32_t> ixs;
   std::vector<int64_t> ioidx;
   const int max_len = std::max(PX.max_len, PY.max_len);
-  int nwaves = 1, grid = 1;
-  sk::StemLaunch SL;
   if (stem) {
     std::vector<int64_t> cnt(ny + 1, 0);
     for (int64_t k = 0; k < n; ++k) cnt[y[k] + 1]++;
@@ -681,57 +688,72 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
       for (int64_t k = 0; k < n; ++k) byy[pos[y[k]]++] = k;
     }
-    // LDS need and wave count
-    SL.lds_max_nl = std::max(PY.max_nl, 1);
-    SL.lds_max_nl = (SL.lds_max_nl + 1) & ~1;
-    SL.lds_max_edges = (std::max(PY.max_edges, 1) + 1) & ~1;
-    SL.lds_max_nl = (SL.lds_max_nl + 3) & ~3;
-    SL.lds_max_bpf = (std::max(PY.max_bpf, 1) + 3) & ~3;
-    SL.lds_max_nlev_pad = (PY.max_nlev + 1 + 3) & ~3;
-    SL.n_gpow = max_len + 2;
-    SL.n_gpow_pad = (SL.n_gpow + 1) & ~1;
-    if (sk::stem_maxk(SL.lds_max_nl) < 0)
-      return fail(ctx, SK_ERR_UNSUPPORTED, "y example has more than 2048 non-leaf DAG nodes");
-    int max_dyn = 0, vgprs = 0;
-    SK_HIP(ctx, sk::stem_kernel_attr(SL.lds_max_nl, &max_dyn, &vgprs));
-    const int valloc = ((std::max(vgprs, 1) + 7) / 8) * 8;
-    const int waves_cu_vgpr = 4 * std::min(8, 512 / valloc);
-    int best = 0, per_cu = 1;
-    for (int w = 8; w >= 1; --w) {  // __launch_bounds__(512)
-      const size_t lds = sk::stem_lds_bytes(SL, w);
-      if (lds > (size_t)max_dyn) continue;
-      const int pc = std::min<int>((int)(163840 / lds), std::min(32, waves_cu_vgpr) / w);
-      if (pc * w > best) {
-        best = pc * w;
-        nwaves = w;
-        per_cu = pc;
-      }
-    }
-    if (best == 0) return fail(ctx, SK_ERR_UNSUPPORTED, "y example too large for LDS");
-    grid = ctx->n_cu * per_cu;
-    const int chunk = 2 * nwaves;
-    struct It {
-      int4 v;
-      double cost;
-    };
-    std::vector<It> tmp;
-    for (int j = 0; j < ny; ++j) {
-      for (int64_t b = cnt[j]; b < cnt[j + 1]; b += chunk) {
-        const int64_t e = std::min<int64_t>(cnt[j + 1], b + chunk);
-        double cost = 0.0;
-        for (int64_t t = b; t < e; ++t)
-          cost += (double)PX.ex_nl[x[byy[t]]] * (double)PY.ex_nl[j];
-        tmp.push_back({make_int4(j, (int)b, (int)(e - b), 0), cost});
-      }
-    }
-    std::stable_sort(tmp.begin(), tmp.end(), [](const It& a, const It& b) { return a.cost > b.cost; });
-    items.reserve(tmp.size());
-    for (auto& t : tmp) items.push_back(t.v);
     ixs.resize(n);
     ioidx.resize(n);
     for (int64_t t = 0; t < n; ++t) {
       ixs[t] = x[byy[t]];
       ioidx[t] = byy[t];
+    }
+    for (int maxk : {32, 24, 16, 8}) {
+      StemClass C;
+      C.maxk = maxk;
+      bool any = false;
+      for (int j = 0; j < ny; ++j) {
+        if (cnt[j + 1] == cnt[j] || sk::stem_maxk(std::max(PY.ex_nl[j], 1)) != maxk) continue;
+        any = true;
+        C.max_nl = std::max(C.max_nl, PY.ex_nl[j]);
+        C.max_edges = std::max(C.max_edges, PY.ex_edge_base[j + 1] - PY.ex_edge_base[j]);
+        C.max_bpf = std::max(C.max_bpf, PY.ex_bpf_base[j + 1] - PY.ex_bpf_base[j]);
+        C.max_nlev = std::max(C.max_nlev, PY.ex_nlev[j]);
+      }
+      if (!any) continue;
+      sk::StemLaunch L;
+      L.lds_max_nl = (std::max(C.max_nl, 1) + 63) & ~63;
+      L.lds_max_edges = (C.max_edges + 4 + 3) & ~3;
+      L.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
+      L.lds_max_nlev_pad = (C.max_nlev + 1 + 3) & ~3;
+      L.n_gpow = max_len + 2;
+      L.n_gpow_pad = (L.n_gpow + 1) & ~1;
+      int max_dyn = 0, vgprs = 0, max_w = 8;
+      SK_HIP(ctx, sk::stem_kernel_attr(L.lds_max_nl, &max_dyn, &vgprs, &max_w));
+      const int valloc = ((std::max(vgprs, 1) + 7) / 8) * 8;
+      const int waves_cu_vgpr = 4 * std::min(8, 512 / valloc);
+      int best = 0, per_cu = 1;
+      for (int w = max_w; w >= 1; --w) {  // the template's __launch_bounds__
+        const size_t lds = sk::stem_lds_bytes(L, w);
+        if (lds > (size_t)max_dyn) continue;
+        const int pc = std::min<int>((int)(163840 / lds), std::min(32, waves_cu_vgpr) / w);
+        if (pc * w > best) {
+          best = pc * w;
+          C.nwaves = w;
+          per_cu = pc;
+        }
+      }
+      if (best == 0) return fail(ctx, SK_ERR_UNSUPPORTED, "y example too large for LDS");
+      C.grid = ctx->n_cu * per_cu;
+      const int chunk = 2 * C.nwaves;
+      struct It {
+        int4 v;
+        double cost;
+      };
+      std::vector<It> tmp;
+      for (int j = 0; j < ny; ++j) {
+        if (sk::stem_maxk(std::max(PY.ex_nl[j], 1)) != maxk) continue;
+        for (int64_t b = cnt[j]; b < cnt[j + 1]; b += chunk) {
+          const int64_t e = std::min<int64_t>(cnt[j + 1], b + chunk);
+          double cost = 0.0;
+          for (int64_t t = b; t < e; ++t)
+            cost += (double)PX.ex_nl[x[byy[t]]] * (double)PY.ex_nl[j];
+          tmp.push_back({make_int4(j, (int)b, (int)(e - b), 0), cost});
+        }
+      }
+      std::stable_sort(tmp.begin(), tmp.end(),
+                       [](const It& a, const It& b) { return a.cost > b.cost; });
+      C.item_off = items.size();
+      C.n_items = tmp.size();
+      for (auto& t : tmp) items.push_back(t.v);
+      C.grid = (int)std::min<int64_t>(C.grid, std::max<int64_t>(1, (int64_t)C.n_items));
+      classes.push_back(C);
     }
     double cells = 0.0;
     for (int64_t k = 0; k < n; ++k) cells += (double)PX.ex_nl[x[k]] * (double)PY.ex_nl[y[k]];
@@ -793,33 +815,49 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     sk::DevParamNodes pn{d_L, d_SL, d_xSL};
     const double gap2 = kp->loop_gap * kp->loop_gap;
     SK_HIP(ctx, sk::launch_prep(xs_->dev, pn, d_gp_loop, gap2, S));
-    SL.xset = xs_->dev;
-    SL.yset = ys_->dev;
-    SL.pn = pn;
-    SL.co_subst = d_co;
-    SL.gpow = d_gp_loop;
-    SL.gap2 = gap2;
-    SL.band = kp->len_band;
-    SL.items = d_items;
-    SL.n_items = (int32_t)items.size();
-    SL.xs = d_ixs;
-    SL.oidx = d_oidx;
-    SL.out = stem_out;
-    SL.item_counter = d_ctr;
-    SL.slab_doubles = (int64_t)std::max(PX.max_slots, 1) * std::max(PY.max_nl, 1);
-    SL.slab_doubles = (SL.slab_doubles + 31) & ~int64_t(31);
-    grid = std::min<int64_t>(grid, std::max<int64_t>(1, (int64_t)items.size()));
-    rc = ensure_scratch(ctx, (size_t)grid * nwaves * SL.slab_doubles * sizeof(double));
+    // one scratch buffer serves the class launches in turn (same stream)
+    size_t scratch_need = 0;
+    for (const StemClass& C : classes) {
+      const int64_t slab = (int64_t)std::max(PX.max_slots, 1) * ((C.max_nl + 63) & ~63);
+      scratch_need = std::max(scratch_need, (size_t)C.grid * C.nwaves * slab * sizeof(double));
+    }
+    rc = ensure_scratch(ctx, std::max<size_t>(scratch_need, 64));
     if (rc) return rc;
-    SL.scratch = ctx->scratch;
 #ifdef SK_STAMPS
     unsigned long long* d_stamps = nullptr;
     SK_HIP(ctx, hipMalloc(&d_stamps, 8 * sizeof(unsigned long long)));
     SK_HIP(ctx, hipMemsetAsync(d_stamps, 0, 8 * sizeof(unsigned long long), S));
-    SL.stamps = d_stamps;
 #endif
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
-    SK_HIP(ctx, sk::launch_stem(SL, grid, nwaves, S));
+    for (size_t c = 0; c < classes.size(); ++c) {
+      const StemClass& C = classes[c];
+      sk::StemLaunch SL;
+      SL.xset = xs_->dev;
+      SL.yset = ys_->dev;
+      SL.pn = pn;
+      SL.co_subst = d_co;
+      SL.gpow = d_gp_loop;
+      SL.n_gpow = max_len + 2;
+      SL.n_gpow_pad = (SL.n_gpow + 1) & ~1;
+      SL.gap2 = gap2;
+      SL.band = kp->len_band;
+      SL.lds_max_nl = (std::max(C.max_nl, 1) + 63) & ~63;
+      SL.lds_max_edges = (C.max_edges + 4 + 3) & ~3;
+      SL.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
+      SL.lds_max_nlev_pad = (C.max_nlev + 1 + 3) & ~3;
+      SL.items = d_items + C.item_off;
+      SL.n_items = (int32_t)C.n_items;
+      SL.xs = d_ixs;
+      SL.oidx = d_oidx;
+      SL.out = stem_out;
+      SL.item_counter = d_ctr + 16 + (int)c;
+      SL.slab_doubles = (int64_t)std::max(PX.max_slots, 1) * SL.lds_max_nl;
+      SL.scratch = ctx->scratch;
+#ifdef SK_STAMPS
+      SL.stamps = d_stamps;
+#endif
+      SK_HIP(ctx, sk::launch_stem(SL, C.grid, C.nwaves, S));
+    }
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
 #ifdef SK_STAMPS
     {
@@ -828,14 +866,17 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SK_HIP(ctx, hipStreamSynchronize(S));
       (void)hipFree(d_stamps);
       const double rows = (double)h[6];
-      std::fprintf(stderr, "[stamps] grid=%d waves/wg=%d pairs=%llu rows=%.0f cycles/row:", grid,
-                   nwaves, h[7], rows);
+      std::fprintf(stderr, "[stamps] classes=%zu pairs=%llu rows=%.0f cycles/row:", classes.size(),
+                   h[7], rows);
       const char* nm[6] = {"hdr", "load", "gather", "match", "sweep", "store"};
       for (int i = 0; i < 6; ++i) std::fprintf(stderr, " %s=%.0f", nm[i], h[i] / rows);
       std::fprintf(stderr, "\n");
+      for (const StemClass& C : classes)
+        std::fprintf(stderr, "[stamps] class maxk=%d max_nl=%d waves/wg=%d grid=%d items=%zu\n",
+                     C.maxk, C.max_nl, C.nwaves, C.grid, C.n_items);
     }
 #endif
-    ctx->last_launches = 1;
+    ctx->last_launches = (int32_t)classes.size();
   }
   if (str) {
     SK_HIP(ctx, hipMemcpyAsync(d_px, x, nb * 4, hipMemcpyHostToDevice, S));
@@ -1184,14 +1225,8 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.pos_lru, &D.pos_lru));
   SK_HIP(ctx, upload(B, P.ex_nslots, &D.ex_nslots));
   SK_HIP(ctx, upload(B, P.ex_xch_base, &D.ex_xch_base));
-  SK_HIP(ctx, upload(B, P.xr_a, &D.xr_a));
-  SK_HIP(ctx, upload(B, P.xr_b, &D.xr_b));
-  SK_HIP(ctx, upload(B, P.xr_c, &D.xr_c));
+  SK_HIP(ctx, upload(B, P.xrow, &D.xrow));
   SK_HIP(ctx, upload(B, P.xr_node, &D.xr_node));
-  SK_HIP(ctx, upload(B, P.xr_w, &D.xr_w));
-  SK_HIP(ctx, upload(B, P.xr_nbp, &D.xr_nbp));
-  SK_HIP(ctx, upload(B, P.xr_bp0, &D.xr_bp0));
-  SK_HIP(ctx, upload(B, P.xr_P, &D.xr_P));
   SK_HIP(ctx, upload(B, P.xr_ch, &D.xr_ch));
   D.max_nl = P.max_nl;
   D.max_edges = P.max_edges;
