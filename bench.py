@@ -339,6 +339,7 @@ def main():
                 "algorithmic_per_launch": alg / n_launch, "model": model,
             },
             "cpu_baseline": cpu,
+            "cells_per_step": float(np.mean(cells)),
         }
         print(json.dumps(line), flush=True)
     if dist_on:
