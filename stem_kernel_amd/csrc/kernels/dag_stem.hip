@@ -69,17 +69,34 @@ typedef __attribute__((address_space(3))) float lds_f32;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 
+// One y node in LDS (16 B, one ds_read_b128 when all fields are needed):
+//   a   = edge_beg:16 | n_edges:8 | n_bpf:8; loop nodes (no non-leaf edges)
+//         carry the gaps of their leaf edge in the low 16 bits instead
+//   b   = len:16 | bpf_beg:16
+//   w   = node weight, nbp = profile gap count at node.first
+struct __attribute__((aligned(16))) NodeRec {
+  uint32_t a, b;
+  float w, nbp;
+};
+typedef __attribute__((address_space(3))) NodeRec lds_nr;
+
+__device__ __forceinline__ NodeRec load_nr(const lds_nr* p) {
+  NodeRec r;
+  r.a = p->a;
+  r.b = p->b;
+  r.w = p->w;
+  r.nbp = p->nbp;
+  return r;
+}
+
 struct YView {  // the y example staged in LDS
-  const lds_u32* b;   // len:16 | bpf_beg:16
-  const lds_u32* c;   // loop gaps
-  const lds_f32* w;
-  const lds_f32* nbp;
+  const lds_nr* nr;
   const lds_f64* P;
   const lds_u32* ed;  // child:11 | parent:11 | gaps:10
   const lds_u32* bc;
   const lds_f32* bp;
-  const lds_i32* lv;   // level -> first node
   const lds_i32* lve;  // level -> first edge
+  const lds_i32* xe;   // per slot k: largest edge count among its 64 nodes
   int nl, nlev;
   float nseqs;
 };
@@ -91,6 +108,10 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// scheduling fence: keeps the compiler from hoisting every slot's memory ops
+// to the top of a phase (which would exceed the register budget)
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 #ifdef SK_STAMPS
 #define STAMP(i)                                                  \
@@ -129,10 +150,11 @@ __device__ __forceinline__ double match_node_score(const lds_f64* co, const DevS
 //
 // Rows p of G0 (x non-leaf nodes) are produced in the reference's post-order,
 // each into a recycled HBM row slot (0xffff = never read, not stored).  Lane
-// l owns the y nodes q = l + 64k, k < kused = ceil(|Vy|/64) (wave-uniform);
-// rows are padded to a multiple of 64 in LDS and in the slab, so the per-k
-// loops need no lane predicates (padded q are masked by selects only where
-// they could reach a valid value).
+// l owns the y nodes q = l + 64k, k < MAXK (the launch's register class: the
+// y example has at most 64*MAXK non-leaf nodes).  LDS node data and the slab
+// rows are padded to 64*MAXK, and every per-slot loop is straight-line code
+// (no branches on k or on the lane), so the compiler can overlap the memory
+// round trips of all slots; padded nodes are masked by selects.
 //
 // Both x-child sums of the reference are linear in the child rows, so one
 // weighted row suffices:   S[q] = sum_{c in ch(p)} g^gaps(p,c) * G0[c][q]
@@ -144,12 +166,13 @@ __device__ __forceinline__ double match_node_score(const lds_f64* co, const DevS
 //   B. M[q] = node_score(p,q) * H (closed forms for loop nodes) -> R (G1);
 //      K += P_x[p] * sum_q M[q] P_y[q];
 //   C. IY sweep over the y levels, edge-parallel: G1[q] += G1[cy]*w(q,cy)
-//      with w = gap^2*w_y(q)*g^gaps precomputed per item (LDS f64 atomics);
+//      with w = gap^2*w_y(q)*g^gaps (LDS f64 atomics);
 //   D. G0[p][q] = G1[q] + v_s(p)*S[k] -> slot of p.
 template <int MAXK>
 __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
-                            const lds_f64* co, const lds_f64* gp, const lds_u32* ya,
-                            double* __restrict__ slab, int x, int lane, int kused, int stride) {
+                            const lds_f64* co, const lds_f64* gp, double* __restrict__ slab, int x,
+                            int lane, int lve_lo, int lve_hi) {
+  constexpr int stride = 64 * MAXK;
   const DevSet& s = P.xset;
   const int nlx = s.ex_nl[x];
   const int NLy = Y.nl;
@@ -157,12 +180,20 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
   const int xnb = s.ex_node_base[x], xbb = s.ex_bpf_base[x];
   int chp = s.ex_xch_base[x];
   const double x_nseq = (double)s.ex_nseqs[x];
-  const int nloop_y = Y.lv[1];  // level 0 = loop nodes
+  const int nlev = Y.nlev;
   const double gap2 = P.gap2;
   const int band = (int)P.band;
   const XRow* __restrict__ xrows = s.xrow + xnb;
   const double* __restrict__ xsl = P.pn.xr_SL + xnb;
   const uint32_t* __restrict__ xch = s.xr_ch;
+  // first edge of level l (levels are contiguous edge ranges), from registers
+  auto lve = [&](int l) -> int {
+    return l < 64 ? __builtin_amdgcn_readlane(lve_lo, l) : __builtin_amdgcn_readlane(lve_hi, l - 64);
+  };
+  const int emax_g = lve(nlev) + 3;  // last padded edge record
+  // slot index clamped to the last valid node: padded lanes re-read a line
+  // other lanes already fetch (no extra HBM traffic)
+  const int qlast = NLy - 1;
   double kacc = 0.0;
 #ifdef SK_STAMPS
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -212,11 +243,14 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
       const bool two = t + 1 < xne;
       const uint32_t c1 = two ? (t + 1 < 4 ? ch[t + 1] : xch[chp_r + t + 1]) : c0;
       const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
-      const double* __restrict__ r0 = slab + (size_t)(c0 & 0xffff) * stride + lane;
-      const double* __restrict__ r1 = slab + (size_t)(c1 & 0xffff) * stride + lane;
+      const double* __restrict__ r0 = slab + (size_t)(c0 & 0xffff) * stride;
+      const double* __restrict__ r1 = slab + (size_t)(c1 & 0xffff) * stride;
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k)
-        if (k < kused) S[k] += eg0 * r0[64 * k] + eg1 * r1[64 * k];
+      for (int k = 0; k < MAXK; ++k) {
+        const int qi = min(lane + 64 * k, qlast);
+        S[k] += eg0 * r0[qi] + eg1 * r1[qi];
+        if ((k & 7) == 7) SCHED_FENCE();  // bound the loads in flight (VGPRs)
+      }
     }
     STAMP(1);
     double H[MAXK];
@@ -224,72 +258,72 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     for (int k = 0; k < MAXK; ++k) H[k] = 0.0;
     if (!xloop) {
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k)
-        if (k < kused) R[lane + 64 * k] = S[k];
-      wave_sync();
+      for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = S[k];
       // MATCH sums over y-children: up to 4 edges per node in one pass with
       // selects (reads past a node's edges stay inside the padded edge
-      // array), longer edge lists after it
-      bool more = false;
+      // array; loop and padded nodes have none), longer lists after it.
+      // (R was written above by this wave: LDS ops of a wave run in order.)
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) {
-        if (k < kused) {
-          const uint32_t a = ya[lane + 64 * k];
-          const int e0 = a & 0xffff, ne = (a >> 16) & 0xff;
-          double acc = 0.0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t f = Y.ed[e0 + j];
-            const double v = gp[f >> 22] * R[f & 0x7ff];
-            acc += j < ne ? v : 0.0;
-          }
-          H[k] = acc;
-          more |= ne > 4;
+        const uint32_t a = Y.nr[lane + 64 * k].a;
+        const int ne = (a >> 16) & 0xff;
+        const int e0 = ne ? (int)(a & 0xffff) : 0;
+        // uniform trip count: the slot's largest edge count (nodes are
+        // sorted by edge count, so the 64 lanes of a slot agree closely);
+        // lanes with fewer edges select 0
+        const int cnt = __builtin_amdgcn_readfirstlane(Y.xe[k]);
+        double acc = 0.0;
+        for (int j = 0; j < cnt; ++j) {
+          const uint32_t f = Y.ed[min(e0 + j, emax_g)];
+          const double v = gp[f >> 22] * R[f & 0x7ff];
+          acc += j < ne ? v : 0.0;
         }
-      }
-      if (__any(more)) {
-#pragma unroll
-        for (int k = 0; k < MAXK; ++k) {
-          if (k < kused) {
-            const uint32_t a = ya[lane + 64 * k];
-            const int e0 = a & 0xffff, ne = (a >> 16) & 0xff;
-            double acc = H[k];
-            for (int j = 4; j < ne; ++j) {
-              const uint32_t f = Y.ed[e0 + j];
-              acc += gp[f >> 22] * R[f & 0x7ff];
-            }
-            H[k] = acc;
-          }
-        }
+        H[k] = acc;
+        if ((k & 3) == 3) SCHED_FENCE();
       }
       wave_sync();
     }
     STAMP(2);
 
-    // ---- B: MATCH term (node score, closed forms for loops) -> R, K part
+    // ---- B: MATCH term (node score, closed forms for loops) -> R, K part.
+    //         Fast node score (one bp entry each side) for every slot first;
+    //         the general bp lists only where some lane needs them.
     double rowk = 0.0;
+    uint32_t slow = 0;
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) {
-      if (k < kused) {
-        const int q = lane + 64 * k;
-        const uint32_t bq = Y.b[q];
-        const int dl = xlen - (int)(bq & 0xffff);
-        const bool inb = q < NLy && (band == 0 || (dl < 0 ? -dl : dl) <= band);
-        const double egy = gp[Y.c[q]];
-        const double Hq = q < nloop_y ? (xloop ? xeg0 : xSL) * egy : H[k];
-        const uint32_t a = ya[q];
-        const float ynbp = Y.nbp[q];
-        double vs = co[xcode + Y.bc[bq >> 16]] * xpf * (double)Y.bp[bq >> 16];
-        const bool fast = x_one && (a >> 24) == 1u && ynbp == 0.0f;
-        if (!fast && inb && Hq != 0.0) {
-          // general bp-frequency lists / gap columns (score_table.cpp:343-380)
-          const double ywg = gap2 * (double)Y.w[q];
-          vs = match_node_score(co, s, xbb, xb0, xnbf, Y, bq >> 16, a >> 24, xwg, ywg, x_nbp,
-                                (double)ynbp, x_nseq);
+      const int q = lane + 64 * k;
+      const NodeRec nd = load_nr(&Y.nr[q]);
+      const uint32_t bq = nd.b;
+      const int dl = xlen - (int)(bq & 0xffff);
+      const bool inb = q < NLy && (band == 0 || (dl < 0 ? -dl : dl) <= band);
+      const bool qloop = q < NLy && ((nd.a >> 16) & 0xff) == 0;  // loop node
+      const double egy = gp[qloop ? (nd.a & 0xffff) : 0];
+      const double Hq = qloop ? (xloop ? xeg0 : xSL) * egy : H[k];
+      const double vs = co[xcode + Y.bc[bq >> 16]] * xpf * (double)Y.bp[bq >> 16];
+      const bool fast = x_one && (nd.a >> 24) == 1u && nd.nbp == 0.0f;
+      const double Hm = inb ? Hq : 0.0;  // masked MATCH sum
+      const bool sl = !fast && Hm != 0.0;
+      slow |= (uint32_t)sl << k;
+      const double M = vs * Hm;
+      // slow slots park their MATCH sum in R for the general pass below
+      R[q] = sl ? Hm : M;
+      rowk += sl ? 0.0 : M * Y.P[q];
+      if ((k & 3) == 3) SCHED_FENCE();
+    }
+    if (__any(slow != 0)) {
+      // general bp-frequency lists / gap columns (score_table.cpp:343-380)
+#pragma unroll 1
+      for (int k = 0; k < MAXK; ++k) {
+        if (slow >> k & 1u) {
+          const int q = lane + 64 * k;
+          const NodeRec nd = load_nr(&Y.nr[q]);
+          const double vs = match_node_score(co, s, xbb, xb0, xnbf, Y, nd.b >> 16, nd.a >> 24, xwg,
+                                             gap2 * (double)nd.w, x_nbp, (double)nd.nbp, x_nseq);
+          const double M = vs * R[q];
+          R[q] = M;
+          rowk += M * Y.P[q];
         }
-        const double M = inb ? vs * Hq : 0.0;
-        R[q] = M;
-        rowk += M * Y.P[q];
       }
     }
     kacc += xP * rowk;
@@ -297,43 +331,47 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     STAMP(3);
 
     // ---- C: IY recurrence, level by level, edge-parallel (levels >= 1).
-    //         Level bounds are read two levels ahead and edge records one
-    //         level ahead, so only the R reads stay on the dependency chain.
-    if (Y.nlev > 1) {
-      // IY weight of an edge: node gap score of the parent * g^gaps (the
-      // reference multiplies G1[child]*v_s*e_s, stem_kernel.cpp:96-102)
-      int fa = Y.lve[1], fb = Y.lve[2];
-      int fc = Y.lve[Y.nlev > 2 ? 3 : 2];
-      uint32_t rec = 0;
-      double w = 0.0;
-      if (fa + lane < fb) {
-        rec = Y.ed[fa + lane];
-        w = gap2 * (double)Y.w[(rec >> 11) & 0x7ff] * gp[rec >> 22];
-      }
-      for (int l = 1; l < Y.nlev; ++l) {
-        // next level [fb, fc); level after next ends at fd
-        const int fd = (l + 3 <= Y.nlev) ? Y.lve[l + 3] : fc;
-        uint32_t rec2 = 0;
-        double w2 = 0.0;
-        if (fb + lane < fc) {
-          rec2 = Y.ed[fb + lane];
-          w2 = gap2 * (double)Y.w[(rec2 >> 11) & 0x7ff] * gp[rec2 >> 22];
-        }
+    //         Edge records are read two levels ahead and their weights one
+    //         level ahead, so only R[child] -> atomic stays on the chain.
+    //         Lanes past a level's edges use record 0 with weight 0.
+    if (nlev > 1) {
+      int fa = lve(1), fb = lve(2);
+      const int emax = lve(nlev) + 3;  // 4 zero records pad the edge array
+      auto rec_at = [&](int f, int lim) -> uint32_t {
+        const uint32_t e = Y.ed[min(f, emax)];
+        return f < lim ? e : 0u;
+      };
+      auto wt = [&](uint32_t e, bool on) -> double {
+        const double w = gap2 * (double)Y.nr[(e >> 11) & 0x7ff].w * gp[e >> 22];
+        return on ? w : 0.0;
+      };
+      uint32_t rec = rec_at(fa + lane, fb);
+      double w = wt(rec, fa + lane < fb);
+      int fc = nlev > 2 ? lve(3) : fb;
+      uint32_t rec1 = rec_at(fb + lane, fc);
+      for (int l = 1; l < nlev; ++l) {
+        // level l: edges [fa, fb); level l+1: [fb, fc); level l+2: [fc, fd)
+        const int fd = l + 3 <= nlev ? lve(l + 3) : fc;
+        const uint32_t rec2 = rec_at(fc + lane, fd);
+        const double w1 = wt(rec1, fb + lane < fc);
+        const double add = R[rec & 0x7ff] * w;
         if (fa + lane < fb)
-          __hip_atomic_fetch_add(&R[(rec >> 11) & 0x7ff], R[rec & 0x7ff] * w, __ATOMIC_RELAXED,
+          __hip_atomic_fetch_add(&R[(rec >> 11) & 0x7ff], add, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
-        for (int f = fa + 64 + lane; f < fb; f += 64) {  // levels with > 64 edges
-          const uint32_t rr = Y.ed[f];
-          const double wr = gap2 * (double)Y.w[(rr >> 11) & 0x7ff] * gp[rr >> 22];
-          __hip_atomic_fetch_add(&R[(rr >> 11) & 0x7ff], R[rr & 0x7ff] * wr, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WAVEFRONT);
+        if (fb - fa > 64) {  // levels with more than 64 edges
+          for (int f = fa + 64 + lane; f < fb; f += 64) {
+            const uint32_t rr = Y.ed[f];
+            __hip_atomic_fetch_add(&R[(rr >> 11) & 0x7ff], R[rr & 0x7ff] * wt(rr, true),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+          }
         }
         wave_sync();
         fa = fb;
         fb = fc;
         fc = fd;
-        rec = rec2;
-        w = w2;
+        rec = rec1;
+        w = w1;
+        rec1 = rec2;
       }
     }
     STAMP(4);
@@ -344,8 +382,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     if (pslot != 0xffffu) {
       double* __restrict__ orow = slab + (size_t)pslot * stride + lane;
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k)
-        if (k < kused) orow[64 * k] = R[lane + 64 * k] + xwg * S[k];
+      for (int k = 0; k < MAXK; ++k) orow[64 * k] = R[lane + 64 * k] + xwg * S[k];
     }
     wave_sync();
     STAMP(5);
@@ -362,8 +399,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
   return kacc;
 }
 
-// Workgroup size bound per register template: MAXK <= 16 keeps <= 168 VGPRs,
-// so 12 waves (3 per SIMD) fit; the wider templates need up to 256.
 template <int MAXK>
 struct StemWaves {
   static constexpr int value = MAXK <= 16 ? 12 : 8;
@@ -383,16 +418,12 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   lds_f64* yP = gp + P.n_gpow_pad;                            // maxnl
   lds_f64* Rall = yP + maxnl;                                 // nwaves*maxnl
   lds_u32* yed = (lds_u32*)(Rall + (size_t)nwaves * maxnl);   // lds_max_edges (mult. of 4)
-  lds_u32* ya = yed + P.lds_max_edges;                        // maxnl
-  lds_u32* yb = ya + maxnl;
-  lds_u32* yc = yb + maxnl;
-  lds_f32* yw = (lds_f32*)(yc + maxnl);
-  lds_f32* ynbp = yw + maxnl;
-  lds_u32* ybc = (lds_u32*)(ynbp + maxnl);                    // lds_max_bpf
+  lds_nr* ynr = (lds_nr*)(yed + P.lds_max_edges);             // maxnl node records
+  lds_u32* ybc = (lds_u32*)(ynr + maxnl);                     // lds_max_bpf
   lds_f32* ybp = (lds_f32*)(ybc + P.lds_max_bpf);
-  lds_i32* ylv = (lds_i32*)(ybp + P.lds_max_bpf);             // lds_max_nlev_pad
-  lds_i32* ylve = ylv + P.lds_max_nlev_pad;                   // lds_max_nlev_pad
-  lds_i32* ctl = ylve + P.lds_max_nlev_pad;                   // 4 ints
+  lds_i32* ylve = (lds_i32*)(ybp + P.lds_max_bpf);            // lds_max_nlev_pad
+  lds_i32* yxe = ylve + P.lds_max_nlev_pad;                   // 32 ints
+  lds_i32* ctl = yxe + 32;                                    // 4 ints
 
   for (int k = threadIdx.x; k < 256; k += blockDim.x) co[k] = P.co_subst[k];
   for (int k = threadIdx.x; k < P.n_gpow; k += blockDim.x) gp[k] = P.gpow[k];
@@ -416,49 +447,44 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     Y.nlev = s.ex_nlev[y];
     Y.nseqs = s.ex_nseqs[y];
     const int nb = s.ex_node_base[y], eb = s.ex_edge_base[y], bb = s.ex_bpf_base[y];
-    const int kused = (Y.nl + 63) >> 6;
-    const int stride = kused * 64;
     {
       const int ne = s.ex_edge_base[y + 1] - eb, nbf = s.ex_bpf_base[y + 1] - bb;
-      const int lb = s.ex_lvl_base[y];
-      // node fields, zero padded to a multiple of 64 (padded q: no edges)
-      for (int k = threadIdx.x; k < stride; k += blockDim.x) {
+      const int lb = s.ex_ylve_base[y];
+      // node records in slot order, zero padded to 64*MAXK (padded q: no
+      // edges, out of band)
+      for (int k = threadIdx.x; k < 64 * MAXK; k += blockDim.x) {
         const bool v = k < Y.nl;
-        ya[k] = v ? s.nd_a[nb + k] : 0u;
-        yb[k] = v ? s.nd_b[nb + k] : 0u;
-        yc[k] = v ? s.nd_c[nb + k] : 0u;
-        yw[k] = v ? s.nd_w[nb + k] : 0.0f;
-        ynbp[k] = v ? s.nd_nbp[nb + k] : 0.0f;
-        yP[k] = v ? s.nd_P[nb + k] : 0.0;
+        ynr[k].a = v ? s.yn_a[nb + k] : 0u;
+        ynr[k].b = v ? s.yn_b[nb + k] : 0u;
+        ynr[k].w = v ? s.yn_w[nb + k] : 0.0f;
+        ynr[k].nbp = v ? s.yn_nbp[nb + k] : 0.0f;
+        yP[k] = v ? s.yn_P[nb + k] : 0.0;
       }
-      // edges (+4 padding records: the predicated gather reads past the end)
-      for (int k = threadIdx.x; k < ne + 4; k += blockDim.x) {
-        if (k < ne) {
-          const uint2 rec = s.ed[eb + k];  // {child | gaps<<16, parent}
-          yed[k] = (rec.x & 0x7ffu) | ((rec.y & 0x7ffu) << 11) | ((rec.x >> 16) << 22);
-        } else {
-          yed[k] = 0u;
-        }
-      }
+      // edges (+4 zero records: reads past the end stay in the array)
+      for (int k = threadIdx.x; k < ne + 4; k += blockDim.x) yed[k] = k < ne ? s.ye[eb + k] : 0u;
       for (int k = threadIdx.x; k < nbf + 1; k += blockDim.x) {
         ybc[k] = k < nbf ? s.bpf_code[bb + k] : 0u;
         ybp[k] = k < nbf ? s.bpf_p[bb + k] : 0.0f;
       }
-      for (int k = threadIdx.x; k <= Y.nlev; k += blockDim.x) {
-        const int q = s.lvl[lb + k];
-        ylv[k] = q;
-        // first edge of level k (levels are contiguous node and edge ranges)
-        ylve[k] = q < Y.nl ? (int)(s.nd_a[nb + q] & 0xffff) : ne;
-      }
+      // first edge of each level (levels >= 1 are contiguous edge ranges)
+      for (int k = threadIdx.x; k < P.lds_max_nlev_pad; k += blockDim.x)
+        ylve[k] = k <= Y.nlev ? s.ylve[lb + k] : ne;
     }
-    Y.b = yb; Y.c = yc; Y.w = yw; Y.nbp = ynbp; Y.P = yP;
-    Y.ed = yed; Y.bc = ybc; Y.bp = ybp; Y.lv = ylv; Y.lve = ylve;
+    Y.nr = ynr; Y.P = yP;
+    Y.ed = yed; Y.bc = ybc; Y.bp = ybp; Y.lve = ylve; Y.xe = yxe;
     __syncthreads();
+    if (threadIdx.x < MAXK) {  // per slot: largest edge count (slots are sorted)
+      int m = 0;
+      for (int l = 0; l < 64; ++l) m = max(m, (int)((ynr[64 * threadIdx.x + l].a >> 16) & 0xff));
+      yxe[threadIdx.x] = m;
+    }
+    __syncthreads();
+    const int lve_lo = ylve[lane], lve_hi = ylve[64 + lane];  // level -> first edge
 
     // static round-robin of the item's pairs over the waves (uniform loop)
     for (int t = wave_u; t < item.z; t += nwaves) {
       const int x = P.xs[item.y + t];
-      const double k = stem_pair<MAXK>(P, Y, R, co, gp, ya, slab, x, lane, kused, stride);
+      const double k = stem_pair<MAXK>(P, Y, R, co, gp, slab, x, lane, lve_lo, lve_hi);
       if (lane == 0) P.out[P.oidx[item.y + t]] = k;
     }
   }
@@ -481,42 +507,45 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += (size_t)P.lds_max_nl * 8;                   // yP
   b += (size_t)nwaves * P.lds_max_nl * 8;          // one row per wave
   b += (size_t)P.lds_max_edges * 4;                // packed edges
-  b += (size_t)P.lds_max_nl * 20;                  // ya,yb,yc,yw,ynbp
+  b += (size_t)P.lds_max_nl * 16;                  // node records
   b += (size_t)P.lds_max_bpf * 8;
-  b += (size_t)P.lds_max_nlev_pad * 8;
-  b += 16;
+  b += (size_t)P.lds_max_nlev_pad * 4;
+  b += 32 * 4 + 16;
   return b;
 }
 
+#define SK_STEM_CLASSES(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32)
+
 static const void* stem_kernel_ptr(int maxk) {
   switch (maxk) {
-    case 8: return reinterpret_cast<const void*>(sk_dag_stem_kernel<8>);
-    case 16: return reinterpret_cast<const void*>(sk_dag_stem_kernel<16>);
-    case 24: return reinterpret_cast<const void*>(sk_dag_stem_kernel<24>);
-    default: return reinterpret_cast<const void*>(sk_dag_stem_kernel<32>);
+#define SK_CASE(K) \
+  case K: return reinterpret_cast<const void*>(sk_dag_stem_kernel<K>);
+    SK_STEM_CLASSES(SK_CASE)
+#undef SK_CASE
+    default: return nullptr;
   }
 }
 
 int stem_maxk(int max_nl) {
-  const int k = (max_nl + 63) / 64;
-  if (k <= 8) return 8;
-  if (k <= 16) return 16;
-  if (k <= 24) return 24;
-  if (k <= 32) return 32;
-  return -1;
+  const int k = ((std::max(max_nl, 1) + 63) / 64 + 3) & ~3;
+  return k <= 32 ? k : -1;
 }
 
 hipError_t launch_stem(const StemLaunch& P, int grid, int nwaves, hipStream_t st) {
   const size_t lds = stem_lds_bytes(P, nwaves);
   const int maxk = stem_maxk(P.lds_max_nl);
   const void* fn = stem_kernel_ptr(maxk);
+  if (!fn) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   switch (maxk) {
-    case 8: hipLaunchKernelGGL(sk_dag_stem_kernel<8>, dim3(grid), dim3(64 * nwaves), lds, st, P); break;
-    case 16: hipLaunchKernelGGL(sk_dag_stem_kernel<16>, dim3(grid), dim3(64 * nwaves), lds, st, P); break;
-    case 24: hipLaunchKernelGGL(sk_dag_stem_kernel<24>, dim3(grid), dim3(64 * nwaves), lds, st, P); break;
-    default: hipLaunchKernelGGL(sk_dag_stem_kernel<32>, dim3(grid), dim3(64 * nwaves), lds, st, P); break;
+#define SK_CASE(K)                                                                          \
+  case K:                                                                                  \
+    hipLaunchKernelGGL(sk_dag_stem_kernel<K>, dim3(grid), dim3(64 * nwaves), lds, st, P); \
+    break;
+    SK_STEM_CLASSES(SK_CASE)
+#undef SK_CASE
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

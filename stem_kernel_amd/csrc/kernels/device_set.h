@@ -65,6 +65,16 @@ struct DevSet {
   const XRow* xrow = nullptr;       // one 32-B record per row (wave-uniform scalar load)
   const uint32_t* xr_node = nullptr;  // level-order node id (for nd_SL)
   const uint32_t* xr_ch = nullptr;  // per child edge: child slot:16 | gaps:16
+  // y role of the stem kernel: non-leaf nodes sorted by edge count (slot
+  // order), edges grouped by parent level, packed child:11|parent:11|gaps:10
+  const uint32_t* yn_a = nullptr;   // e0:16 (loops: leaf-edge gaps) | n_edges:8 | n_bpf:8
+  const uint32_t* yn_b = nullptr;   // len:16 | bpf_beg:16
+  const float* yn_w = nullptr;
+  const float* yn_nbp = nullptr;
+  const double* yn_P = nullptr;
+  const uint32_t* ye = nullptr;     // edges (local ids), ex_edge_base[e] per example
+  const int32_t* ylve = nullptr;    // per level: first edge (nlev+1 entries)
+  const int32_t* ex_ylve_base = nullptr;
   // maxima over the set
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
   int64_t total_nodes = 0;

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <memory>
 #include <new>
 #include <numeric>
@@ -81,6 +82,10 @@ struct HostPack {
   std::vector<float4> pos_lru;
   std::vector<int32_t> ex_nslots, ex_xch_base;
   std::vector<sk::XRow> xrow;
+  std::vector<uint32_t> yn_a, yn_b, ye;
+  std::vector<float> yn_w, yn_nbp;
+  std::vector<double> yn_P;
+  std::vector<int32_t> ylve, ex_ylve_base;
   std::vector<uint32_t> xr_node, xr_ch;
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
 };
@@ -226,6 +231,49 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     for (int k = 0; k < nl; ++k) lv[level[order[k]] + 1]++;
     for (int l = 0; l < nlev; ++l) lv[l + 1] += lv[l];
     P.lvl.insert(P.lvl.end(), lv.begin(), lv.end());
+
+    // y-role numbering for the stem kernel: nodes sorted by non-leaf edge
+    // count (descending, loops last), so that the 64 nodes of one register
+    // slot need about the same number of MATCH-sum iterations; edges grouped
+    // by parent level (the IY sweep walks levels) and contiguous per parent,
+    // packed child:11 | parent:11 | gaps:10 in sorted ids.
+    {
+      std::vector<int> srt(nl);
+      std::iota(srt.begin(), srt.end(), 0);
+      auto ne_of = [&](int k) { return (P.nd_a[P.ex_node_base.back() + k] >> 16) & 0xff; };
+      std::stable_sort(srt.begin(), srt.end(), [&](int a, int b) { return ne_of(a) > ne_of(b); });
+      std::vector<int> pos(nl);
+      for (int i = 0; i < nl; ++i) pos[srt[i]] = i;
+      const int nb0 = P.ex_node_base.back();
+      std::vector<uint32_t> e0_of(nl, 0);
+      const int ye_base = (int)P.ye.size();
+      P.ex_ylve_base.push_back((int32_t)P.ylve.size());
+      for (int l = 0; l < nlev; ++l) {
+        P.ylve.push_back((int32_t)P.ye.size() - ye_base);
+        for (int k = lv[l]; k < lv[l + 1]; ++k) {  // level-order ids of level l
+          const uint32_t a = P.nd_a[nb0 + k];
+          const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
+          e0_of[k] = (uint32_t)P.ye.size() - ye_base;
+          for (uint32_t t = 0; t < ne; ++t) {
+            const uint2 rec = P.ed[ebase + el + t];  // {child | gaps<<16, parent}
+            P.ye.push_back((uint32_t)pos[rec.x & 0xffff] | ((uint32_t)pos[k] << 11) |
+                           ((rec.x >> 16) << 22));
+          }
+        }
+      }
+      P.ylve.push_back((int32_t)P.ye.size() - ye_base);
+      for (int i = 0; i < nl; ++i) {
+        const int k = srt[i];
+        const uint32_t a = P.nd_a[nb0 + k];
+        const uint32_t ne = (a >> 16) & 0xff;
+        // loops carry their leaf-edge gaps where stems keep their first edge
+        P.yn_a.push_back((ne ? e0_of[k] : P.nd_c[nb0 + k]) | (a & 0xffff0000u));
+        P.yn_b.push_back(P.nd_b[nb0 + k]);
+        P.yn_w.push_back(P.nd_w[nb0 + k]);
+        P.yn_nbp.push_back(P.nd_nbp[nb0 + k]);
+        P.yn_P.push_back(P.nd_P[nb0 + k]);
+      }
+    }
 
     // x-role schedule: rows in reference (post-)order; a row's HBM slot is
     // recycled once its last parent has been produced (LIFO free list keeps
@@ -694,7 +742,10 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       ixs[t] = x[byy[t]];
       ioidx[t] = byy[t];
     }
-    for (int maxk : {32, 24, 16, 8}) {
+    for (int j = 0; j < ny; ++j)
+      if (cnt[j + 1] > cnt[j] && sk::stem_maxk(std::max(PY.ex_nl[j], 1)) < 0)
+        return fail(ctx, SK_ERR_UNSUPPORTED, "y example has more than 2048 non-leaf DAG nodes");
+    for (int maxk : {32, 28, 24, 20, 16, 12, 8, 4}) {
       StemClass C;
       C.maxk = maxk;
       bool any = false;
@@ -707,11 +758,13 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
         C.max_nlev = std::max(C.max_nlev, PY.ex_nlev[j]);
       }
       if (!any) continue;
+      if (C.max_nlev > 127)
+        return fail(ctx, SK_ERR_UNSUPPORTED, "y example has more than 127 DAG levels");
       sk::StemLaunch L;
-      L.lds_max_nl = (std::max(C.max_nl, 1) + 63) & ~63;
+      L.lds_max_nl = 64 * maxk;
       L.lds_max_edges = (C.max_edges + 4 + 3) & ~3;
       L.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
-      L.lds_max_nlev_pad = (C.max_nlev + 1 + 3) & ~3;
+      L.lds_max_nlev_pad = 128;
       L.n_gpow = max_len + 2;
       L.n_gpow_pad = (L.n_gpow + 1) & ~1;
       int max_dyn = 0, vgprs = 0, max_w = 8;
@@ -730,6 +783,16 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
         }
       }
       if (best == 0) return fail(ctx, SK_ERR_UNSUPPORTED, "y example too large for LDS");
+#ifdef SK_STAMPS
+      // diagnostics: SK_FORCE_WAVES=w,p -> w waves per workgroup, p workgroups per CU
+      if (const char* fw = std::getenv("SK_FORCE_WAVES")) {
+        int w = 0, pc = 0;
+        if (std::sscanf(fw, "%d,%d", &w, &pc) == 2 && w >= 1 && w <= C.nwaves && pc >= 1) {
+          C.nwaves = w;
+          per_cu = pc;
+        }
+      }
+#endif
       C.grid = ctx->n_cu * per_cu;
       const int chunk = 2 * C.nwaves;
       struct It {
@@ -818,7 +881,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     // one scratch buffer serves the class launches in turn (same stream)
     size_t scratch_need = 0;
     for (const StemClass& C : classes) {
-      const int64_t slab = (int64_t)std::max(PX.max_slots, 1) * ((C.max_nl + 63) & ~63);
+      const int64_t slab = (int64_t)std::max(PX.max_slots, 1) * 64 * C.maxk;
       scratch_need = std::max(scratch_need, (size_t)C.grid * C.nwaves * slab * sizeof(double));
     }
     rc = ensure_scratch(ctx, std::max<size_t>(scratch_need, 64));
@@ -841,10 +904,10 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.n_gpow_pad = (SL.n_gpow + 1) & ~1;
       SL.gap2 = gap2;
       SL.band = kp->len_band;
-      SL.lds_max_nl = (std::max(C.max_nl, 1) + 63) & ~63;
+      SL.lds_max_nl = 64 * C.maxk;
       SL.lds_max_edges = (C.max_edges + 4 + 3) & ~3;
       SL.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
-      SL.lds_max_nlev_pad = (C.max_nlev + 1 + 3) & ~3;
+      SL.lds_max_nlev_pad = 128;
       SL.items = d_items + C.item_off;
       SL.n_items = (int32_t)C.n_items;
       SL.xs = d_ixs;
@@ -1226,6 +1289,14 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.ex_nslots, &D.ex_nslots));
   SK_HIP(ctx, upload(B, P.ex_xch_base, &D.ex_xch_base));
   SK_HIP(ctx, upload(B, P.xrow, &D.xrow));
+  SK_HIP(ctx, upload(B, P.yn_a, &D.yn_a));
+  SK_HIP(ctx, upload(B, P.yn_b, &D.yn_b));
+  SK_HIP(ctx, upload(B, P.yn_w, &D.yn_w));
+  SK_HIP(ctx, upload(B, P.yn_nbp, &D.yn_nbp));
+  SK_HIP(ctx, upload(B, P.yn_P, &D.yn_P));
+  SK_HIP(ctx, upload(B, P.ye, &D.ye));
+  SK_HIP(ctx, upload(B, P.ylve, &D.ylve));
+  SK_HIP(ctx, upload(B, P.ex_ylve_base, &D.ex_ylve_base));
   SK_HIP(ctx, upload(B, P.xr_node, &D.xr_node));
   SK_HIP(ctx, upload(B, P.xr_ch, &D.xr_ch));
   D.max_nl = P.max_nl;
