@@ -112,6 +112,15 @@ __device__ __forceinline__ void wave_sync() {
 // scheduling fence: keeps the compiler from hoisting every slot's memory ops
 // to the top of a phase (which would exceed the register budget)
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#ifndef SK_CHUNK_A
+#define SK_CHUNK_A 8
+#endif
+#ifndef SK_CHUNK_G
+#define SK_CHUNK_G 4
+#endif
+#ifndef SK_CHUNK_M
+#define SK_CHUNK_M 4
+#endif
 
 #ifdef SK_STAMPS
 #define STAMP(i)                                                  \
@@ -188,7 +197,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
   const uint32_t* __restrict__ xch = s.xr_ch;
   // first edge of level l (levels are contiguous edge ranges), from registers
   auto lve = [&](int l) -> int {
-    return l < 64 ? __builtin_amdgcn_readlane(lve_lo, l) : __builtin_amdgcn_readlane(lve_hi, l - 64);
+    return __builtin_amdgcn_readlane(l < 64 ? lve_lo : lve_hi, l & 63);
   };
   const int emax_g = lve(nlev) + 3;  // last padded edge record
   // slot index clamped to the last valid node: padded lanes re-read a line
@@ -249,7 +258,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
       for (int k = 0; k < MAXK; ++k) {
         const int qi = min(lane + 64 * k, qlast);
         S[k] += eg0 * r0[qi] + eg1 * r1[qi];
-        if ((k & 7) == 7) SCHED_FENCE();  // bound the loads in flight (VGPRs)
+        if ((k % SK_CHUNK_A) == SK_CHUNK_A - 1) SCHED_FENCE();  // bound loads in flight (VGPRs)
       }
     }
     STAMP(1);
@@ -279,7 +288,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
           acc += j < ne ? v : 0.0;
         }
         H[k] = acc;
-        if ((k & 3) == 3) SCHED_FENCE();
+        if ((k % SK_CHUNK_G) == SK_CHUNK_G - 1) SCHED_FENCE();
       }
       wave_sync();
     }
@@ -309,7 +318,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
       // slow slots park their MATCH sum in R for the general pass below
       R[q] = sl ? Hm : M;
       rowk += sl ? 0.0 : M * Y.P[q];
-      if ((k & 3) == 3) SCHED_FENCE();
+      if ((k % SK_CHUNK_M) == SK_CHUNK_M - 1) SCHED_FENCE();
     }
     if (__any(slow != 0)) {
       // general bp-frequency lists / gap columns (score_table.cpp:343-380)
@@ -351,10 +360,12 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
       uint32_t rec1 = rec_at(fb + lane, fc);
       for (int l = 1; l < nlev; ++l) {
         // level l: edges [fa, fb); level l+1: [fb, fc); level l+2: [fc, fd)
+        // the level's R reads go first, so waiting for them does not wait
+        // for the prefetches behind them (LDS ops complete in order)
+        const double add = R[rec & 0x7ff] * w;
         const int fd = l + 3 <= nlev ? lve(l + 3) : fc;
         const uint32_t rec2 = rec_at(fc + lane, fd);
         const double w1 = wt(rec1, fb + lane < fc);
-        const double add = R[rec & 0x7ff] * w;
         if (fa + lane < fb)
           __hip_atomic_fetch_add(&R[(rec >> 11) & 0x7ff], add, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
