@@ -216,6 +216,11 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
 #pragma unroll
   for (int j = 0; j < 4; ++j) nch[j] = xch[chp + j];
 
+  double S[MAXK];  // this row's weighted child sum (carried over rows)
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) S[k] = 0.0;
+  uint32_t done = 0;  // first-four children already in S
+
   for (int r = 0; r < nlx; ++r) {
     const uint32_t xa = nx.a, xb = nx.b, xc = nx.c;
     const double xwg = gap2 * (double)nx.w;
@@ -243,14 +248,43 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     const uint32_t xcode = (xc >> 16) * 16u;
     STAMP(0);
 
-    // ---- A: S = sum_c g^gaps G0[c][*]  (coalesced HBM row streams)
-    double S[MAXK];
+    // ---- A: S = sum_c g^gaps G0[c][*]  (coalesced HBM row streams).
+    //      S arrives partly filled: the previous row added the child rows it
+    //      prefetched during its sweep and itself (a distance-1 child) from
+    //      registers; `done` marks those among the first four children.
+    {
+      uint32_t c[4] = {0u, 0u, 0u, 0u};
+      int na = 0;
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) S[k] = 0.0;
-    for (int t = 0; t < xne; t += 2) {
-      const uint32_t c0 = t < 4 ? ch[t] : xch[chp_r + t];
+      for (int j = 0; j < 4; ++j) {
+        const bool take = j < xne && !(done >> j & 1u);
+        c[0] = (take && na == 0) ? ch[j] : c[0];
+        c[1] = (take && na == 1) ? ch[j] : c[1];
+        c[2] = (take && na == 2) ? ch[j] : c[2];
+        c[3] = (take && na == 3) ? ch[j] : c[3];
+        na += take ? 1 : 0;
+      }
+#pragma unroll
+      for (int h = 0; h < 4; h += 2) {
+        if (na > h) {
+          const bool two = na > h + 1;
+          const uint32_t c0 = c[h], c1 = two ? c[h + 1] : c[h];
+          const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
+          const double* __restrict__ r0 = slab + (size_t)(c0 & 0xffff) * stride;
+          const double* __restrict__ r1 = slab + (size_t)(c1 & 0xffff) * stride;
+#pragma unroll
+          for (int k = 0; k < MAXK; ++k) {
+            const int qi = min(lane + 64 * k, qlast);
+            S[k] += eg0 * r0[qi] + eg1 * r1[qi];
+            if ((k % SK_CHUNK_A) == SK_CHUNK_A - 1) SCHED_FENCE();
+          }
+        }
+      }
+    }
+    for (int t = 4; t < xne; t += 2) {  // children past the fourth
+      const uint32_t c0 = xch[chp_r + t];
       const bool two = t + 1 < xne;
-      const uint32_t c1 = two ? (t + 1 < 4 ? ch[t + 1] : xch[chp_r + t + 1]) : c0;
+      const uint32_t c1 = two ? xch[chp_r + t + 1] : c0;
       const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
       const double* __restrict__ r0 = slab + (size_t)(c0 & 0xffff) * stride;
       const double* __restrict__ r1 = slab + (size_t)(c1 & 0xffff) * stride;
@@ -258,7 +292,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
       for (int k = 0; k < MAXK; ++k) {
         const int qi = min(lane + 64 * k, qlast);
         S[k] += eg0 * r0[qi] + eg1 * r1[qi];
-        if ((k % SK_CHUNK_A) == SK_CHUNK_A - 1) SCHED_FENCE();  // bound loads in flight (VGPRs)
+        if ((k % SK_CHUNK_A) == SK_CHUNK_A - 1) SCHED_FENCE();
       }
     }
     STAMP(1);
@@ -339,6 +373,54 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     wave_sync();
     STAMP(3);
 
+    // ---- next row's children: the ones this row cannot produce are loaded
+    //      now (two at most, into registers the MATCH sums have freed) and
+    //      land during the sweep; this row itself, when a child of the next,
+    //      is added from registers in D.
+    // rows prefetched per row: two where the register budget allows
+    constexpr int NPF = (MAXK <= 12 || MAXK == 20) ? 2 : 1;
+    uint32_t nxt_done = 0;
+    double egd = 0.0, egt0 = 0.0, egt1 = 0.0;
+    double T0[MAXK], T1[MAXK];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) T0[k] = T1[k] = 0.0;
+    if (r + 1 < nlx) {
+      const int nne = nx.a & 0xff;
+      uint32_t pf0 = 0, pf1 = 0;
+      int npf = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < nne) {
+          const uint32_t c = nch[j];
+          const double g = gp[c >> 16];
+          if ((c & 0xffff) == pslot) {
+            egd += g;
+            nxt_done |= 1u << j;
+          } else if (npf < NPF) {
+            if (npf == 0) {
+              pf0 = c;
+              egt0 = g;
+            } else {
+              pf1 = c;
+              egt1 = g;
+            }
+            ++npf;
+            nxt_done |= 1u << j;
+          }
+        }
+      }
+      if (npf >= 1) {
+        const double* __restrict__ r0 = slab + (size_t)(pf0 & 0xffff) * stride;
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k) T0[k] = r0[min(lane + 64 * k, qlast)];
+      }
+      if (NPF >= 2 && npf >= 2) {
+        const double* __restrict__ r1 = slab + (size_t)(pf1 & 0xffff) * stride;
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k) T1[k] = r1[min(lane + 64 * k, qlast)];
+      }
+    }
+
     // ---- C: IY recurrence, level by level, edge-parallel (levels >= 1).
     //         Edge records are read two levels ahead and their weights one
     //         level ahead, so only R[child] -> atomic stays on the chain.
@@ -390,11 +472,17 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     // ---- D: G0 row p = G1 + v_s*S, to p's slot (roots are never read).
     // Every later read of element q of this row is by the same lane (q =
     // lane + 64k), so per-thread program order makes it visible: no fence.
-    if (pslot != 0xffffu) {
-      double* __restrict__ orow = slab + (size_t)pslot * stride + lane;
+    {
+      double* __restrict__ orow = slab + (size_t)(pslot == 0xffffu ? 0u : pslot) * stride + lane;
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k) orow[64 * k] = R[lane + 64 * k] + xwg * S[k];
+      for (int k = 0; k < MAXK; ++k) {
+        const double o = R[lane + 64 * k] + xwg * S[k];
+        if (pslot != 0xffffu) orow[64 * k] = o;
+        // the next row's partial sum: itself (distance-1) + prefetched rows
+        S[k] = egd * o + egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
+      }
     }
+    done = nxt_done;
     wave_sync();
     STAMP(5);
   }
