@@ -1017,3 +1017,120 @@ double orc_stem4d(const char *x, const double *bpx, const char *y, const double 
   free(col[1]);
   return result;
 }
+
+/* Band constraints of StemKernel::alignment_constraints without alignment
+ * posteriors (ali_bound == 0, band > 0; stem_kernel/stem_kernel.cpp:66-72). */
+void orc_stem4d_band(int n, int m, unsigned band, unsigned *c_low, unsigned *c_high) {
+  for (int i = 0; i <= n; ++i) {
+    const unsigned j = (unsigned)((double)i / n * m + 0.5);
+    c_low[i] = j < band ? 0u : j - band;
+    c_high[i] = j + band > (unsigned)m ? (unsigned)m : j + band;
+  }
+}
+
+/* StemKernel<double,BPMat>::partial_dp (stem_kernel/stem_kernel.cpp:113-280)
+ * with band constraints only: cells outside the band stay at the planes'
+ * zero fill; K0 past c_high[j-1] and K1 below c_low[i+1] use the
+ * reference's boundary approximations. */
+double orc_stem4d_banded(const char *x, const double *bpx, const char *y, const double *bpy,
+                         double gap, double stack, double subst, float bp_bound, int model,
+                         unsigned loop, unsigned band) {
+  const int n = (int)strlen(x), m = (int)strlen(y);
+  if (n == 0) return 1.0; /* K0(0,0,0,m) of the fully initialised plane (0,0) */
+  const double g = gap;
+  bp4 BX = {x, bpx, n, model, loop}, BY = {y, bpy, m, model, loop};
+  unsigned *cl = (unsigned *)malloc(sizeof(unsigned) * (n + 1));
+  unsigned *chh = (unsigned *)malloc(sizeof(unsigned) * (n + 1));
+  orc_stem4d_band(n, m, band, cl, chh);
+  double *gpw = (double *)malloc(sizeof(double) * (m + 1));
+  gpw[0] = 1.0;
+  for (int i = 1; i <= m; ++i) gpw[i] = gpw[i - 1] * g;
+  const size_t cells = (size_t)(m + 1) * (m + 2) / 2;
+  const size_t plane = cells * 8;
+#define CELL(k, l) ((size_t)(l) * ((l) + 1) / 2 + (size_t)(k))
+  double *col[2];
+  col[0] = (double *)calloc((size_t)(n + 1) * plane, sizeof(double));
+  col[1] = (double *)calloc((size_t)(n + 1) * plane, sizeof(double));
+  double result = 0.0;
+  for (int j = 0; j <= n; ++j) {
+    double *cur = col[j & 1], *prv = col[(j + 1) & 1];
+#define DP(C, s, i, k, l) ((C)[(size_t)(i) * plane + (size_t)(s) * cells + CELL(k, l)])
+    memset(&cur[(size_t)j * plane], 0, plane * sizeof(double));
+    for (size_t c = 0; c < cells; ++c) cur[(size_t)j * plane + S_K0 * cells + c] = 1.0;
+    for (int l = 0; l <= m; ++l) {
+      DP(cur, S_G0, j, l, l) = 1.0;
+      for (int k = l - 1; k >= 0; --k) DP(cur, S_G0, j, k, l) = DP(cur, S_G0, j, k + 1, l) * g;
+    }
+    for (int i = j - 1; i >= 0; --i) {
+      const float bp_ij = bp4_prob(&BX, i, j - 1);
+      memset(&cur[(size_t)i * plane], 0, plane * sizeof(double));
+      for (int l = (int)cl[j]; l <= (int)chh[j]; ++l) {
+        DP(cur, S_K0, i, l, l) = 1.0;
+        DP(cur, S_G0, i, l, l) = DP(cur, S_G0, i + 1, l, l) * g;
+        if (l == 0) continue;
+        const int kt = (l - 1) < (int)chh[i] ? (l - 1) : (int)chh[i];
+        for (int k = kt; k >= (int)cl[i]; --k) {
+          if (l <= (int)chh[j - 1]) {
+            DP(cur, S_K0, i, k, l) = DP(prv, S_K0, i, k, l);
+            DP(cur, S_G0, i, k, l) = DP(prv, S_G0, i, k, l) * g;
+          } else { /* approximation (:183-186) */
+            DP(cur, S_K0, i, k, l) = DP(prv, S_K0, i, k, chh[j - 1]);
+            DP(cur, S_G0, i, k, l) = DP(prv, S_G0, i, k, chh[j - 1]) * g * g;
+          }
+          if (k >= (int)cl[i + 1]) {
+            DP(cur, S_K1, i, k, l) = DP(cur, S_K1, i + 1, k, l);
+            DP(cur, S_G1, i, k, l) = DP(cur, S_G1, i + 1, k, l) * g;
+          } else { /* approximation (:193-196) */
+            DP(cur, S_K1, i, k, l) = DP(cur, S_K1, i + 1, cl[i + 1], l);
+            DP(cur, S_G1, i, k, l) = DP(cur, S_G1, i + 1, cl[i + 1], l) * g * g;
+          }
+          if (l - 1 >= (int)cl[j] || k == l - 1) {
+            DP(cur, S_K2, i, k, l) = DP(cur, S_K2, i, k, l - 1);
+            DP(cur, S_G2, i, k, l) = DP(cur, S_G2, i, k, l - 1) * g;
+          } else { /* :221-227 */
+            DP(cur, S_K2, i, k, l) = 0.0;
+            DP(cur, S_G2, i, k, l) = 0.0;
+            for (int ll = k; ll != l; ++ll) {
+              DP(cur, S_K2, i, k, l) += DP(cur, S_K3, i, ll, ll);
+              DP(cur, S_G2, i, k, l) += DP(cur, S_G3, i, ll, ll) * gpw[l - k];
+            }
+          }
+          if (k + 1 <= (int)chh[i]) {
+            DP(cur, S_K3, i, k, l) = DP(cur, S_K3, i, k + 1, l);
+            DP(cur, S_G3, i, k, l) = DP(cur, S_G3, i, k + 1, l) * g;
+          } else { /* :233-235 */
+            DP(cur, S_K3, i, k, l) = DP(cur, S_K3, i, l, l);
+            DP(cur, S_G3, i, k, l) = DP(cur, S_G3, i, l, l) * gpw[l - k];
+          }
+          if (bp_ij > bp_bound) {
+            const float bp_kl = bp4_prob(&BY, k, l - 1);
+            if (bp_kl > bp_bound) {
+              const double g0 = DP(prv, S_G0, i + 1, k + 1, l - 1);
+              if (x[i] == y[k] && x[j - 1] == y[l - 1]) {
+                DP(cur, S_K3, i, k, l) += g0 * stack * bp_ij * bp_kl;
+                DP(cur, S_G3, i, k, l) += g0;
+              } else {
+                DP(cur, S_K3, i, k, l) += g0 * stack * subst * bp_ij * bp_kl;
+              }
+            }
+          }
+          DP(cur, S_K2, i, k, l) += DP(cur, S_K3, i, k, l);
+          DP(cur, S_G2, i, k, l) += DP(cur, S_G3, i, k, l);
+          DP(cur, S_K1, i, k, l) += DP(cur, S_K2, i, k, l);
+          DP(cur, S_G1, i, k, l) += DP(cur, S_G2, i, k, l);
+          DP(cur, S_K0, i, k, l) += DP(cur, S_K1, i, k, l);
+          DP(cur, S_G0, i, k, l) += DP(cur, S_G1, i, k, l);
+        }
+      }
+    }
+    if (j == n) result = DP(cur, S_K0, 0, 0, m);
+#undef DP
+  }
+#undef CELL
+  free(col[0]);
+  free(col[1]);
+  free(cl);
+  free(chh);
+  free(gpw);
+  return result;
+}

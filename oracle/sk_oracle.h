@@ -106,6 +106,12 @@ void orc_bpla_weights(const orc_mdata *d, float *p_left, float *p_right, float *
 double orc_stem4d(const char *x, const double *bpx, const char *y, const double *bpy,
                   double gap, double stack, double subst, float bp_bound, int model,
                   unsigned loop);
+/* Banded variant: partial_dp (stem_kernel.cpp:113-280) with the -b band
+ * constraints of alignment_constraints (ali_bound == 0, :66-72). */
+double orc_stem4d_banded(const char *x, const double *bpx, const char *y, const double *bpy,
+                         double gap, double stack, double subst, float bp_bound, int model,
+                         unsigned loop, unsigned band);
+void orc_stem4d_band(int n, int m, unsigned band, unsigned *c_low, unsigned *c_high);
 
 #ifdef __cplusplus
 }

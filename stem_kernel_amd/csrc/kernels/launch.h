@@ -76,6 +76,7 @@ struct Stem4dPair {
   int64_t x_bp = 0, y_bp = 0;    // into bpdiag
   int64_t x_chr = 0, y_chr = 0;  // into chars
   int64_t out_index = 0;
+  int64_t band_off = 0;          // into band_lo/band_hi (n+1 entries)
 };
 
 struct Stem4dLaunch {
@@ -90,6 +91,8 @@ struct Stem4dLaunch {
   double gap = 0.0, stack = 0.0, subst = 0.0;
   float bp_bound = 0.0f;
   double* out = nullptr;
+  const int32_t* band_lo = nullptr;  // partial_dp band (nullptr: full_dp)
+  const int32_t* band_hi = nullptr;
 };
 
 int stem4d_cpl(int m);

@@ -38,7 +38,18 @@ __device__ __forceinline__ double wave_shl1(double v, double high) {
 
 __device__ __forceinline__ int pad4(int v) { return (v + 3) & ~3; }
 
-template <int CPL>
+// offset of row d2 in a plane: sum_{e<d2} pad4(m+1-e)
+__device__ __forceinline__ int row_off(int m, int d2) {
+  const int q = d2 >> 2;
+  int r = 4 * q * (m + 1) - (4 * q) * (4 * q - 1) / 2 + 6 * q;  // whole groups of four rows
+  for (int e = 4 * q; e < d2; ++e) r += pad4(m + 1 - e);
+  return r;
+}
+
+// BAND: partial_dp (stem_kernel.cpp:113-280) with the -b band constraints:
+// cells outside the band stay zero, K0 past c_high[j-1] and K1 below
+// c_low[i+1] take the reference's boundary approximations.
+template <int CPL, bool BAND>
 __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -92,6 +103,17 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
   const bool stack_on = bp_ij > bound;
   const uint8_t xi = xs[i], xj = xs[j - 1];
   const double stk = P.stack, sub = P.subst;
+  int clj = 0, chj = m, cli = 0, chi = m, chjm1 = m, cli1 = 0;
+  if (BAND) {
+    const int32_t* cl = P.band_lo + pr.band_off;
+    const int32_t* ch = P.band_hi + pr.band_off;
+    clj = cl[j];
+    chj = ch[j];
+    cli = cl[i];
+    chi = ch[i];
+    chjm1 = ch[j - 1];
+    cli1 = cl[i + 1];
+  }
 
   double K2[CPL], G2[CPL], K3[CPL], G3[CPL];
   uint8_t yk[CPL];
@@ -107,8 +129,9 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
   for (int c = 0; c < CPL; ++c) {
     const int k = k0 + c;
     if (k <= m) {
-      cur[k] = 1.0;
-      cur[cp + k] = B[cp + k] * g;
+      const bool on = !BAND || (k >= clj && k <= chj);
+      cur[k] = on ? 1.0 : 0.0;
+      cur[cp + k] = on ? B[cp + k] * g : 0.0;
       cur[2 * cp + k] = 0.0;
       cur[3 * cp + k] = 0.0;
     }
@@ -174,14 +197,30 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + c;
       if (k <= kmax) {
-        // dp_init (:85-96)
+        const int l = k + d2;
+        const bool on = !BAND || (l >= clj && l <= chj && k >= cli && k <= chi);
+        // dp_init (:85-96); banded: partial_dp's boundary cases (:179-236)
         double K0 = cK0[c];
         double G0 = cG0[c] * g;
         double K1 = cK1[c];
         double G1 = cG1[c] * g;
         double k2 = K2[c], g2 = G2[c] * g;
         double k3 = K3n[c], g3 = G3n[c] * g;
-        if (stack_on) {  // :327-340
+        if (BAND && on) {
+          if (l > chjm1) {  // K0(i,j-1,k,c_high[j-1]), G0 * g * g
+            const int o = row_off(m, chjm1 - k) + k;
+            K0 = A[o];
+            G0 = A[cp + o] * g * g;
+          }
+          if (k < cli1) {  // K1(i+1,j,c_low[i+1],l), G1 * g * g
+            const int o = row_off(m, l - cli1) + cli1;
+            K1 = B[2 * cp + o];
+            G1 = B[3 * cp + o] * g * g;
+          }
+          if (!(l - 1 >= clj || k == l - 1)) k2 = g2 = 0.0;  // diagonal K3/G3 are zero
+          if (!(k + 1 <= chi)) k3 = g3 = 0.0;
+        }
+        if (stack_on && on) {  // :327-340
           const float bp_kl = cbp[c];
           if (bp_kl > bound) {
             const double g0 = cGs[c];
@@ -200,6 +239,7 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
         G1 += g2;
         K0 += K1;
         G0 += G1;
+        if (BAND && !on) K0 = G0 = K1 = G1 = k2 = g2 = k3 = g3 = 0.0;  // zero fill
         cur[R + k] = K0;
         cur[cp + R + k] = G0;
         cur[2 * cp + R + k] = K1;
@@ -230,12 +270,19 @@ hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st) {
   if (P.n_items == 0) return hipSuccess;
   const int wpb = 4;
   const dim3 grid((unsigned)((P.n_items + wpb - 1) / wpb)), block(64 * wpb);
+  const bool band = P.band_lo != nullptr;
+#define SK_L(C)                                                                      \
+  if (band)                                                                          \
+    hipLaunchKernelGGL((sk_stem4d_kernel<C, true>), grid, block, 0, st, P);         \
+  else                                                                               \
+    hipLaunchKernelGGL((sk_stem4d_kernel<C, false>), grid, block, 0, st, P);
   switch (cpl) {
-    case 1: hipLaunchKernelGGL(sk_stem4d_kernel<1>, grid, block, 0, st, P); break;
-    case 2: hipLaunchKernelGGL(sk_stem4d_kernel<2>, grid, block, 0, st, P); break;
-    case 4: hipLaunchKernelGGL(sk_stem4d_kernel<4>, grid, block, 0, st, P); break;
-    default: hipLaunchKernelGGL(sk_stem4d_kernel<8>, grid, block, 0, st, P); break;
+    case 1: SK_L(1) break;
+    case 2: SK_L(2) break;
+    case 4: SK_L(4) break;
+    default: SK_L(8) break;
   }
+#undef SK_L
   return hipGetLastError();
 }
 

@@ -107,7 +107,8 @@ struct sk_dataset {
 struct Stem4dBatch {
   sk::Stem4dPair* pairs = nullptr;
   int2* items = nullptr;
-  size_t cap_pairs = 0, cap_items = 0;
+  int32_t* band = nullptr;  // c_low | c_high (cap_band each)
+  size_t cap_pairs = 0, cap_items = 0, cap_band = 0;
 };
 
 struct sk_context {
@@ -544,8 +545,6 @@ int64_t stem4d_plane_doubles(int m) {
 
 int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
                const int32_t* x, const int32_t* y, int64_t n, double* out_dev) {
-  if (kp->len_band != 0)
-    return fail(ctx, SK_ERR_UNSUPPORTED, "4-D stem kernel: banded partial_dp is not implemented");
   if (kp->bp_model < 0 || kp->bp_model > 2 || !(kp->bp_bound >= 0.0))
     return fail(ctx, SK_ERR_INVALID, "4-D stem kernel: bp_model 0..2 and bp_bound >= 0");
   // per-example tables of the examples this call touches
@@ -633,6 +632,19 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       prs.push_back(p);
       ++b1;
     }
+    // partial_dp band constraints per pair (alignment_constraints with
+    // ali_bound 0, stem_kernel.cpp:66-72): x position -> [c_low, c_high]
+    std::vector<int32_t> blo, bhi;
+    if (kp->len_band > 0) {
+      for (auto& p : prs) {
+        p.band_off = (int64_t)blo.size();
+        for (int i = 0; i <= p.n; ++i) {
+          const unsigned jj = p.n ? (unsigned)((double)i / p.n * p.m + 0.5) : 0u;
+          blo.push_back((int32_t)(jj < kp->len_band ? 0u : jj - kp->len_band));
+          bhi.push_back((int32_t)(jj + kp->len_band > (unsigned)p.m ? (unsigned)p.m : jj + kp->len_band));
+        }
+      }
+    }
     // work items {pair, i} per span d1, concatenated
     std::vector<int2> items;
     std::vector<int64_t> ioff(maxn + 2, 0);
@@ -656,6 +668,16 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
                                hipMemcpyHostToDevice, S));
     SK_HIP(ctx, hipMemcpyAsync(Bt.items, items.data(), items.size() * sizeof(int2),
                                hipMemcpyHostToDevice, S));
+    if (!blo.empty()) {
+      if (Bt.cap_band < blo.size()) {
+        if (Bt.band) (void)hipFree(Bt.band);
+        Bt.cap_band = std::max<size_t>(blo.size(), 4096);
+        SK_HIP(ctx, hipMalloc(&Bt.band, 2 * Bt.cap_band * sizeof(int32_t)));
+      }
+      SK_HIP(ctx, hipMemcpyAsync(Bt.band, blo.data(), blo.size() * 4, hipMemcpyHostToDevice, S));
+      SK_HIP(ctx, hipMemcpyAsync(Bt.band + Bt.cap_band, bhi.data(), bhi.size() * 4,
+                                 hipMemcpyHostToDevice, S));
+    }
     sk::Stem4dLaunch L;
     L.pairs = Bt.pairs;
     L.scratch = ctx->scratch;
@@ -667,6 +689,8 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     L.subst = kp->subst;
     L.bp_bound = (float)kp->bp_bound;
     L.out = out_dev;
+    L.band_lo = blo.empty() ? nullptr : Bt.band;
+    L.band_hi = blo.empty() ? nullptr : Bt.band + Bt.cap_band;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     for (int d1 = 0; d1 <= maxn; ++d1) {
       L.d1 = d1;
@@ -1089,6 +1113,7 @@ int sk_close(sk_context* ctx) {
   if (ctx->work) (void)hipFree(ctx->work);
   if (ctx->s4d.pairs) (void)hipFree(ctx->s4d.pairs);
   if (ctx->s4d.items) (void)hipFree(ctx->s4d.items);
+  if (ctx->s4d.band) (void)hipFree(ctx->s4d.band);
   for (hipEvent_t e : {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3})
     if (e) (void)hipEventDestroy(e);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -152,11 +152,13 @@ class StemKernel4D(_Kernel):
     to float32 here like the CLI would."""
     kind = _lib.STEM4D
 
-    def __init__(self, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0, bp_model=0, loop=3,
+    def __init__(self, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0, bp_model=0, loop=3, band=0,
                  cli_float=True):
+        """band > 0 selects partial_dp with the -b band constraints
+        (stem_kernel.cpp:51-75, 113-280); 0 is full_dp."""
         f = (lambda v: float(np.float32(v))) if cli_float else float
         super().__init__(gap=f(gap), stack=f(stack), subst=f(subst), bp_bound=f(bp_bound),
-                         bp_model=int(bp_model), loop=int(loop), len_band=0)
+                         bp_model=int(bp_model), loop=int(loop), len_band=int(band))
 
 
 class SiStemStrKernel(_Kernel):

@@ -29,7 +29,7 @@ def _oracle(seqs, kern, pairs):
     for a, b in pairs:
         xa, xb = seqs[a], seqs[b]
         out.append(po.stem4d(xa.lower(), ska.fold(xa), xb.lower(), ska.fold(xb), p.gap, p.stack,
-                             p.subst, p.bp_bound, p.bp_model, p.loop))
+                             p.subst, p.bp_bound, p.bp_model, p.loop, p.len_band))
     return np.array(out)
 
 
@@ -78,13 +78,39 @@ def test_stem4d_params_and_predict(gpu_ctx):
     assert rel_err(row, ref) < TOL
 
 
+def test_oracle_band_wide_equals_full_dp():
+    """partial_dp with a band wider than both sequences computes every cell."""
+    s = ska.random_sequences(3, 24, 21) + ska.random_sequences(1, 17, 22)
+    for a in range(4):
+        for b in range(4):
+            x, y = s[a], s[b]
+            full = po.stem4d(x.lower(), ska.fold(x), y.lower(), ska.fold(y))
+            wide = po.stem4d(x.lower(), ska.fold(x), y.lower(), ska.fold(y), band=64)
+            assert wide == full
+
+
 @pytest.mark.gpu
-def test_stem4d_rejects_alignments_and_band(gpu_ctx):
+@pytest.mark.parametrize("band", [1, 3, 8, 100])
+def test_stem4d_banded_matches_oracle(gpu_ctx, band):
+    """partial_dp (-b): band constraints and the boundary approximations."""
+    seqs = ska.random_sequences(3, 40, 0x5EED0043) + ska.random_sequences(2, 27, 9)
+    seqs += ska.random_sequences(1, 70, 10) + ["GGGAAACCC", "A"]
+    ds, _ = make_examples(seqs)
+    kern = ska.StemKernel4D(band=band)
+    n = len(seqs)
+    iu = list(zip(*np.triu_indices(n)))
+    got = gpu_ctx.gram(ds, kern)
+    ref = _oracle(seqs, kern, iu)
+    assert rel_err(got[tuple(np.array(iu).T)], ref) < TOL
+    # asymmetric lengths in both orders
+    x = np.array([3, 0, 5, 6], np.int32)
+    y = np.array([0, 3, 1, 2], np.int32)
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    assert rel_err(got, _oracle(seqs, kern, list(zip(x, y)))) < TOL
+
+
+@pytest.mark.gpu
+def test_stem4d_rejects_alignments(gpu_ctx):
     ds, _ = make_examples([["ACGUACGU", "ACG-ACGU"], "ACGUAC"])
     with pytest.raises(ska.StemKernelError):
         gpu_ctx.gram(ds, ska.StemKernel4D())
-    ds2, _ = make_examples(["ACGUACGUAA", "ACGUAC"])
-    k = ska.StemKernel4D()
-    k.params.len_band = 5  # partial_dp (banded) is not implemented
-    with pytest.raises(ska.StemKernelError):
-        gpu_ctx.gram(ds2, k)
