@@ -38,6 +38,12 @@ __device__ __forceinline__ double wave_shl1(double v, double high) {
 
 __device__ __forceinline__ int pad4(int v) { return (v + 3) & ~3; }
 
+__device__ __forceinline__ double bcast_lane0(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
 // offset of row d2 in a plane: sum_{e<d2} pad4(m+1-e)
 __device__ __forceinline__ int row_off(int m, int d2) {
   const int q = d2 >> 2;
@@ -63,7 +69,9 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
   double* span_cur = P.scratch + pr.scratch_off + (int64_t)(d1 % 3) * (n + 1) * 4 * cp;
   double* __restrict__ cur = span_cur + (int64_t)i * 4 * cp;
   const double g = P.gap;
-  const int k0 = lane * CPL;
+  // lane owns k = lane + 64c: every state access of a wave instruction is
+  // 512 contiguous bytes
+  const int k0 = lane;
 
   if (d1 == 0) {  // plane (j,j): K0 = 1, G0 = g^(l-k), K1 = G1 = 0  (:297-309)
     int R = 0;
@@ -71,7 +79,7 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
       const double gd = P.gpow[d2];
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
-        const int k = k0 + c;
+        const int k = k0 + 64 * c;
         if (k <= m - d2) {
           cur[R + k] = 1.0;
           cur[cp + R + k] = gd;
@@ -120,14 +128,14 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     K2[c] = G2[c] = K3[c] = G3[c] = 0.0;
-    const int k = k0 + c;
+    const int k = k0 + 64 * c;
     yk[c] = k < m ? ys[k] : 0;
   }
 
   // d2 = 0: cells (l,l): K0 = 1, G0 = G0(i+1,j,l,l)*g, K1 = G1 = 0  (:313-316)
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
-    const int k = k0 + c;
+    const int k = k0 + 64 * c;
     if (k <= m) {
       const bool on = !BAND || (k >= clj && k <= chj);
       cur[k] = on ? 1.0 : 0.0;
@@ -149,7 +157,7 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
     const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      const int k = k0 + c;
+      const int k = k0 + 64 * c;
       pbp[c] = 0.0f;
       pGs[c] = 0.0;
       pyl[c] = 0;
@@ -186,16 +194,17 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
     // K3/G3 of (k+1, l): my next cell, or the next lane's first (span d2-1)
     double K3n[CPL], G3n[CPL];
 #pragma unroll
-    for (int c = 0; c < CPL - 1; ++c) {
-      K3n[c] = K3[c + 1];
-      G3n[c] = G3[c + 1];
+    for (int c = 0; c < CPL; ++c) {
+      // lane 63's neighbour k+1 is lane 0 of the next slot
+      const double hk = c + 1 < CPL ? bcast_lane0(K3[c + 1 < CPL ? c + 1 : c]) : 0.0;
+      const double hg = c + 1 < CPL ? bcast_lane0(G3[c + 1 < CPL ? c + 1 : c]) : 0.0;
+      K3n[c] = wave_shl1(K3[c], hk);
+      G3n[c] = wave_shl1(G3[c], hg);
     }
-    K3n[CPL - 1] = wave_shl1(K3[0], 0.0);
-    G3n[CPL - 1] = wave_shl1(G3[0], 0.0);
     const int kmax = m - d2;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      const int k = k0 + c;
+      const int k = k0 + 64 * c;
       if (k <= kmax) {
         const int l = k + d2;
         const bool on = !BAND || (l >= clj && l <= chj && k >= cli && k <= chi);
