@@ -180,7 +180,7 @@ __device__ __forceinline__ double match_node_score(const lds_f64* co, const DevS
 template <int MAXK>
 __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
                             const lds_f64* co, const lds_f64* gp, double* __restrict__ slab, int x,
-                            int lane, int lve_lo, int lve_hi) {
+                            int lane, int lve_lo, int lve_hi, int lcm_lo, int lcm_hi) {
   constexpr int stride = 64 * MAXK;
   const DevSet& s = P.xset;
   const int nlx = s.ex_nl[x];
@@ -425,8 +425,20 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     //         Edge records are read two levels ahead and their weights one
     //         level ahead, so only R[child] -> atomic stays on the chain.
     //         Lanes past a level's edges use record 0 with weight 0.
-    if (nlev > 1) {
-      int fa = lve(1), fb = lve(2);
+    // With a length band, every y node shorter than xlen - band has G1 = 0
+    // exactly (its MATCH terms are masked and so are all its descendants'),
+    // so sweep levels whose children are all that short add only zeros:
+    // start at the first level whose running maximum child length reaches
+    // the threshold (lcm = per-level prefix maximum, staged per item).
+    int l0 = 1;
+    if (band > 0) {
+      const int thr = xlen - band;
+      const uint64_t blo = __ballot(lane >= 1 && lane < nlev && lcm_lo >= thr);
+      const uint64_t bhi = __ballot(lane + 64 < nlev && lcm_hi >= thr);
+      l0 = blo ? (int)__builtin_ctzll(blo) : (bhi ? 64 + (int)__builtin_ctzll(bhi) : nlev);
+    }
+    if (l0 < nlev) {
+      int fa = lve(l0), fb = lve(l0 + 1);
       const int emax = lve(nlev) + 3;  // 4 zero records pad the edge array
       auto rec_at = [&](int f, int lim) -> uint32_t {
         const uint32_t e = Y.ed[min(f, emax)];
@@ -438,9 +450,9 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
       };
       uint32_t rec = rec_at(fa + lane, fb);
       double w = wt(rec, fa + lane < fb);
-      int fc = nlev > 2 ? lve(3) : fb;
+      int fc = l0 + 2 <= nlev ? lve(l0 + 2) : fb;
       uint32_t rec1 = rec_at(fb + lane, fc);
-      for (int l = 1; l < nlev; ++l) {
+      for (int l = l0; l < nlev; ++l) {
         // level l: edges [fa, fb); level l+1: [fb, fc); level l+2: [fc, fd)
         // the level's R reads go first, so waiting for them does not wait
         // for the prefetches behind them (LDS ops complete in order)
@@ -521,7 +533,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   lds_u32* ybc = (lds_u32*)(ynr + maxnl);                     // lds_max_bpf
   lds_f32* ybp = (lds_f32*)(ybc + P.lds_max_bpf);
   lds_i32* ylve = (lds_i32*)(ybp + P.lds_max_bpf);            // lds_max_nlev_pad
-  lds_i32* yxe = ylve + P.lds_max_nlev_pad;                   // 32 ints
+  lds_i32* ylcm = ylve + P.lds_max_nlev_pad;                  // lds_max_nlev_pad
+  lds_i32* yxe = ylcm + P.lds_max_nlev_pad;                   // 32 ints
   lds_i32* ctl = yxe + 32;                                    // 4 ints
 
   for (int k = threadIdx.x; k < 256; k += blockDim.x) co[k] = P.co_subst[k];
@@ -566,8 +579,10 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
         ybp[k] = k < nbf ? s.bpf_p[bb + k] : 0.0f;
       }
       // first edge of each level (levels >= 1 are contiguous edge ranges)
-      for (int k = threadIdx.x; k < P.lds_max_nlev_pad; k += blockDim.x)
+      for (int k = threadIdx.x; k < P.lds_max_nlev_pad; k += blockDim.x) {
         ylve[k] = k <= Y.nlev ? s.ylve[lb + k] : ne;
+        ylcm[k] = k <= Y.nlev ? s.ylcm[lb + k] : 0x7fffffff;
+      }
     }
     Y.nr = ynr; Y.P = yP;
     Y.ed = yed; Y.bc = ybc; Y.bp = ybp; Y.lve = ylve; Y.xe = yxe;
@@ -579,11 +594,13 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     }
     __syncthreads();
     const int lve_lo = ylve[lane], lve_hi = ylve[64 + lane];  // level -> first edge
+    const int lcm_lo = ylcm[lane], lcm_hi = ylcm[64 + lane];  // prefix max child length
 
     // static round-robin of the item's pairs over the waves (uniform loop)
     for (int t = wave_u; t < item.z; t += nwaves) {
       const int x = P.xs[item.y + t];
-      const double k = stem_pair<MAXK>(P, Y, R, co, gp, slab, x, lane, lve_lo, lve_hi);
+      const double k =
+          stem_pair<MAXK>(P, Y, R, co, gp, slab, x, lane, lve_lo, lve_hi, lcm_lo, lcm_hi);
       if (lane == 0) P.out[P.oidx[item.y + t]] = k;
     }
   }
@@ -608,7 +625,7 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += (size_t)P.lds_max_edges * 4;                // packed edges
   b += (size_t)P.lds_max_nl * 16;                  // node records
   b += (size_t)P.lds_max_bpf * 8;
-  b += (size_t)P.lds_max_nlev_pad * 4;
+  b += (size_t)P.lds_max_nlev_pad * 8;
   b += 32 * 4 + 16;
   return b;
 }

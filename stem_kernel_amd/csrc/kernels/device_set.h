@@ -74,6 +74,7 @@ struct DevSet {
   const double* yn_P = nullptr;
   const uint32_t* ye = nullptr;     // edges (local ids), ex_edge_base[e] per example
   const int32_t* ylve = nullptr;    // per level: first edge (nlev+1 entries)
+  const int32_t* ylcm = nullptr;    // per level: max child length over levels 1..l (same base)
   const int32_t* ex_ylve_base = nullptr;
   // maxima over the set
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;

@@ -85,7 +85,7 @@ struct HostPack {
   std::vector<uint32_t> yn_a, yn_b, ye;
   std::vector<float> yn_w, yn_nbp;
   std::vector<double> yn_P;
-  std::vector<int32_t> ylve, ex_ylve_base;
+  std::vector<int32_t> ylve, ylcm, ex_ylve_base;
   std::vector<uint32_t> xr_node, xr_ch;
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
 };
@@ -263,6 +263,24 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         }
       }
       P.ylve.push_back((int32_t)P.ye.size() - ye_base);
+      // prefix maximum over levels 1..l of the children's lengths (level 0
+      // has no edges): lets a row skip sweep levels that only carry zeros
+      {
+        int32_t run = -1;
+        P.ylcm.push_back(-1);  // level 0
+        for (int l = 1; l < nlev; ++l) {
+          for (int k = lv[l]; k < lv[l + 1]; ++k) {
+            const uint32_t a = P.nd_a[nb0 + k];
+            const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
+            for (uint32_t t = 0; t < ne; ++t) {
+              const uint32_t c = P.ed[ebase + el + t].x & 0xffff;
+              run = std::max<int32_t>(run, (int32_t)(P.nd_b[nb0 + c] & 0xffff));
+            }
+          }
+          P.ylcm.push_back(run);
+        }
+        P.ylcm.push_back(run);  // entry nlev (unused)
+      }
       for (int i = 0; i < nl; ++i) {
         const int k = srt[i];
         const uint32_t a = P.nd_a[nb0 + k];
@@ -1321,6 +1339,7 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.yn_P, &D.yn_P));
   SK_HIP(ctx, upload(B, P.ye, &D.ye));
   SK_HIP(ctx, upload(B, P.ylve, &D.ylve));
+  SK_HIP(ctx, upload(B, P.ylcm, &D.ylcm));
   SK_HIP(ctx, upload(B, P.ex_ylve_base, &D.ex_ylve_base));
   SK_HIP(ctx, upload(B, P.xr_node, &D.xr_node));
   SK_HIP(ctx, upload(B, P.xr_ch, &D.xr_ch));
