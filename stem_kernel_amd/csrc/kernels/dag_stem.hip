@@ -96,7 +96,8 @@ struct YView {  // the y example staged in LDS
   const lds_u32* bc;
   const lds_f32* bp;
   const lds_i32* lve;  // level -> first edge
-  const lds_i32* xe;   // per slot k: largest edge count among its 64 nodes
+  const lds_i32* lfirst;  // length v -> first node (nodes sorted by length), v <= lmax+1
+  int lmax;               // largest node length of the example
   int nl, nlev;
   float nseqs;
 };
@@ -199,7 +200,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
   auto lve = [&](int l) -> int {
     return __builtin_amdgcn_readlane(l < 64 ? lve_lo : lve_hi, l & 63);
   };
-  const int emax_g = lve(nlev) + 3;  // last padded edge record
   // slot index clamped to the last valid node: padded lanes re-read a line
   // other lanes already fetch (no extra HBM traffic)
   const int qlast = NLy - 1;
@@ -296,79 +296,67 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
       }
     }
     STAMP(1);
-    double H[MAXK];
-#pragma unroll
-    for (int k = 0; k < MAXK; ++k) H[k] = 0.0;
-    if (!xloop) {
-#pragma unroll
-      for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = S[k];
-      // MATCH sums over y-children: up to 4 edges per node in one pass with
-      // selects (reads past a node's edges stay inside the padded edge
-      // array; loop and padded nodes have none), longer lists after it.
-      // (R was written above by this wave: LDS ops of a wave run in order.)
-#pragma unroll
-      for (int k = 0; k < MAXK; ++k) {
-        const uint32_t a = Y.nr[lane + 64 * k].a;
-        const int ne = (a >> 16) & 0xff;
-        const int e0 = ne ? (int)(a & 0xffff) : 0;
-        // uniform trip count: the slot's largest edge count (nodes are
-        // sorted by edge count, so the 64 lanes of a slot agree closely);
-        // lanes with fewer edges select 0
-        const int cnt = __builtin_amdgcn_readfirstlane(Y.xe[k]);
-        double acc = 0.0;
-        for (int j = 0; j < cnt; ++j) {
-          const uint32_t f = Y.ed[min(e0 + j, emax_g)];
-          const double v = gp[f >> 22] * R[f & 0x7ff];
-          acc += j < ne ? v : 0.0;
-        }
-        H[k] = acc;
-        if ((k % SK_CHUNK_G) == SK_CHUNK_G - 1) SCHED_FENCE();
-      }
-      wave_sync();
-    }
-    STAMP(2);
 
-    // ---- B: MATCH term (node score, closed forms for loops) -> R, K part.
-    //         Fast node score (one bp entry each side) for every slot first;
-    //         the general bp lists only where some lane needs them.
+    // ---- MATCH term, only where it can be non-zero.  y nodes are numbered
+    //      by length, so the nodes inside the length band [xlen-band,
+    //      xlen+band] are one index range [qa, qb) (looked up per row).  They
+    //      are processed longest first, 64 per pass: a node's MATCH sum reads
+    //      S of its children, which are strictly shorter, so a pass may
+    //      overwrite R (S -> M) for the nodes it finished without affecting a
+    //      later pass.  Everything outside the range gets M = 0 afterwards.
+    //      (LDS ops of a wave complete in issue order.)
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = S[k];
+    int qa = 0, qb = NLy;
+    if (band > 0) {
+      qa = Y.lfirst[min(max(xlen - band, 0), Y.lmax + 1)];
+      qb = Y.lfirst[min(max(xlen + band + 1, 0), Y.lmax + 1)];
+    }
+    qa = __builtin_amdgcn_readfirstlane(qa);
+    qb = __builtin_amdgcn_readfirstlane(qb);
     double rowk = 0.0;
-    uint32_t slow = 0;
+    for (int top = qb - 1; top >= qa; top -= 64) {
+      const int q = top - lane;
+      const bool on = q >= qa;
+      const int qq = on ? q : qa;
+      const NodeRec nd = load_nr(&Y.nr[qq]);
+      const int ne = (nd.a >> 16) & 0xff;
+      double Hq;
+      if (ne == 0) {  // loop node: closed form over the two leaf children
+        Hq = (xloop ? xeg0 : xSL) * gp[nd.a & 0xffff];
+      } else if (xloop) {  // x leaf child against a y stem: G0[leaf][*] = 0
+        Hq = 0.0;
+      } else {  // sum_{cy in ch(q)} g^gy S[cy]
+        const int e0 = nd.a & 0xffff;
+        Hq = 0.0;
+        for (int j = 0; j < ne; ++j) {
+          const uint32_t f = Y.ed[e0 + j];
+          Hq += gp[f >> 22] * R[f & 0x7ff];
+        }
+      }
+      double vs;
+      if (x_one && (nd.a >> 24) == 1u && nd.nbp == 0.0f) {
+        // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:350-364)
+        vs = co[xcode + Y.bc[nd.b >> 16]] * xpf * (double)Y.bp[nd.b >> 16];
+      } else {
+        // general bp-frequency lists / gap columns (score_table.cpp:343-380)
+        vs = Hq != 0.0 ? match_node_score(co, s, xbb, xb0, xnbf, Y, nd.b >> 16, nd.a >> 24, xwg,
+                                           gap2 * (double)nd.w, x_nbp, (double)nd.nbp, x_nseq)
+                       : 0.0;
+      }
+      const double M = vs * Hq;
+      if (on) {
+        R[q] = M;
+        rowk += M * Y.P[q];
+      }
+    }
+    // outside the band: M = 0
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) {
       const int q = lane + 64 * k;
-      const NodeRec nd = load_nr(&Y.nr[q]);
-      const uint32_t bq = nd.b;
-      const int dl = xlen - (int)(bq & 0xffff);
-      const bool inb = q < NLy && (band == 0 || (dl < 0 ? -dl : dl) <= band);
-      const bool qloop = q < NLy && ((nd.a >> 16) & 0xff) == 0;  // loop node
-      const double egy = gp[qloop ? (nd.a & 0xffff) : 0];
-      const double Hq = qloop ? (xloop ? xeg0 : xSL) * egy : H[k];
-      const double vs = co[xcode + Y.bc[bq >> 16]] * xpf * (double)Y.bp[bq >> 16];
-      const bool fast = x_one && (nd.a >> 24) == 1u && nd.nbp == 0.0f;
-      const double Hm = inb ? Hq : 0.0;  // masked MATCH sum
-      const bool sl = !fast && Hm != 0.0;
-      slow |= (uint32_t)sl << k;
-      const double M = vs * Hm;
-      // slow slots park their MATCH sum in R for the general pass below
-      R[q] = sl ? Hm : M;
-      rowk += sl ? 0.0 : M * Y.P[q];
-      if ((k % SK_CHUNK_M) == SK_CHUNK_M - 1) SCHED_FENCE();
+      if (q < qa || q >= qb) R[q] = 0.0;
     }
-    if (__any(slow != 0)) {
-      // general bp-frequency lists / gap columns (score_table.cpp:343-380)
-#pragma unroll 1
-      for (int k = 0; k < MAXK; ++k) {
-        if (slow >> k & 1u) {
-          const int q = lane + 64 * k;
-          const NodeRec nd = load_nr(&Y.nr[q]);
-          const double vs = match_node_score(co, s, xbb, xb0, xnbf, Y, nd.b >> 16, nd.a >> 24, xwg,
-                                             gap2 * (double)nd.w, x_nbp, (double)nd.nbp, x_nseq);
-          const double M = vs * R[q];
-          R[q] = M;
-          rowk += M * Y.P[q];
-        }
-      }
-    }
+    STAMP(2);
     kacc += xP * rowk;
     wave_sync();
     STAMP(3);
@@ -534,8 +522,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   lds_f32* ybp = (lds_f32*)(ybc + P.lds_max_bpf);
   lds_i32* ylve = (lds_i32*)(ybp + P.lds_max_bpf);            // lds_max_nlev_pad
   lds_i32* ylcm = ylve + P.lds_max_nlev_pad;                  // lds_max_nlev_pad
-  lds_i32* yxe = ylcm + P.lds_max_nlev_pad;                   // 32 ints
-  lds_i32* ctl = yxe + 32;                                    // 4 ints
+  lds_i32* ylf = ylcm + P.lds_max_nlev_pad;                   // lds_max_len_pad
+  lds_i32* ctl = ylf + P.lds_max_len_pad;                     // 4 ints
 
   for (int k = threadIdx.x; k < 256; k += blockDim.x) co[k] = P.co_subst[k];
   for (int k = threadIdx.x; k < P.n_gpow; k += blockDim.x) gp[k] = P.gpow[k];
@@ -585,12 +573,17 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
       }
     }
     Y.nr = ynr; Y.P = yP;
-    Y.ed = yed; Y.bc = ybc; Y.bp = ybp; Y.lve = ylve; Y.xe = yxe;
+    Y.ed = yed; Y.bc = ybc; Y.bp = ybp; Y.lve = ylve; Y.lfirst = ylf;
+    Y.lmax = Y.nl ? (int)(s.yn_b[nb + Y.nl - 1] & 0xffff) : 0;
     __syncthreads();
-    if (threadIdx.x < MAXK) {  // per slot: largest edge count (slots are sorted)
-      int m = 0;
-      for (int l = 0; l < 64; ++l) m = max(m, (int)((ynr[64 * threadIdx.x + l].a >> 16) & 0xff));
-      yxe[threadIdx.x] = m;
+    // length -> first node index (nodes are sorted by length)
+    for (int v = threadIdx.x; v <= Y.lmax + 1; v += blockDim.x) {
+      int lo = 0, hi = Y.nl;  // first q with len(q) >= v
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int)(ynr[mid].b & 0xffff) < v) lo = mid + 1; else hi = mid;
+      }
+      ylf[v] = lo;
     }
     __syncthreads();
     const int lve_lo = ylve[lane], lve_hi = ylve[64 + lane];  // level -> first edge
@@ -626,7 +619,7 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += (size_t)P.lds_max_nl * 16;                  // node records
   b += (size_t)P.lds_max_bpf * 8;
   b += (size_t)P.lds_max_nlev_pad * 8;
-  b += 32 * 4 + 16;
+  b += (size_t)P.lds_max_len_pad * 4 + 16;
   return b;
 }
 

@@ -233,16 +233,16 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     for (int l = 0; l < nlev; ++l) lv[l + 1] += lv[l];
     P.lvl.insert(P.lvl.end(), lv.begin(), lv.end());
 
-    // y-role numbering for the stem kernel: nodes sorted by non-leaf edge
-    // count (descending, loops last), so that the 64 nodes of one register
-    // slot need about the same number of MATCH-sum iterations; edges grouped
-    // by parent level (the IY sweep walks levels) and contiguous per parent,
-    // packed child:11 | parent:11 | gaps:10 in sorted ids.
+    // y-role numbering for the stem kernel: nodes sorted by length (span
+    // last - first), so the nodes inside a row's length band are one index
+    // range and a node's children (strictly shorter) come before it; edges
+    // grouped by parent level (the IY sweep walks levels) and contiguous per
+    // parent, packed child:11 | parent:11 | gaps:10 in sorted ids.
     {
       std::vector<int> srt(nl);
       std::iota(srt.begin(), srt.end(), 0);
-      auto ne_of = [&](int k) { return (P.nd_a[P.ex_node_base.back() + k] >> 16) & 0xff; };
-      std::stable_sort(srt.begin(), srt.end(), [&](int a, int b) { return ne_of(a) > ne_of(b); });
+      auto len_of = [&](int k) { return P.nd_b[P.ex_node_base.back() + k] & 0xffff; };
+      std::stable_sort(srt.begin(), srt.end(), [&](int a, int b) { return len_of(a) < len_of(b); });
       std::vector<int> pos(nl);
       for (int i = 0; i < nl; ++i) pos[srt[i]] = i;
       const int nb0 = P.ex_node_base.back();
@@ -807,6 +807,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       L.lds_max_edges = (C.max_edges + 4 + 3) & ~3;
       L.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
       L.lds_max_nlev_pad = 128;
+      L.lds_max_len_pad = (max_len + 2 + 3) & ~3;
       L.n_gpow = max_len + 2;
       L.n_gpow_pad = (L.n_gpow + 1) & ~1;
       int max_dyn = 0, vgprs = 0, max_w = 8;
@@ -950,6 +951,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.lds_max_edges = (C.max_edges + 4 + 3) & ~3;
       SL.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
       SL.lds_max_nlev_pad = 128;
+      SL.lds_max_len_pad = (max_len + 2 + 3) & ~3;
       SL.items = d_items + C.item_off;
       SL.n_items = (int32_t)C.n_items;
       SL.xs = d_ixs;
