@@ -52,3 +52,11 @@ stamps:
 	$(HIPCC) $(CXXFLAGS) -DSK_STAMPS -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/stamps/sk_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o -Wl,-rpath,/opt/rocm/lib
 .PHONY: stamps
+
+# experiment build: make variant NAME=x DEFS="-DSK_CHUNK_A=32 [-DSK_STAMPS]" -> build/libsk_x.so
+variant:
+	@mkdir -p $(BUILD)/var/$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip -o $(BUILD)/var/$(NAME)/dag_stem.o
+	$(HIPCC) $(CXXFLAGS) $(DEFS) -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/var/$(NAME)/sk_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/var/$(NAME)/sk_api.o $(BUILD)/var/$(NAME)/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o -Wl,-rpath,/opt/rocm/lib
+.PHONY: variant

@@ -366,7 +366,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     //      land during the sweep; this row itself, when a child of the next,
     //      is added from registers in D.
     // rows prefetched per row: two where the register budget allows
-    constexpr int NPF = (MAXK <= 12 || MAXK == 20) ? 2 : 1;
+    constexpr int NPF = (MAXK <= 12 || (MAXK == 20 && SK_W20 == 8)) ? 2 : 1;
     uint32_t nxt_done = 0;
     double egd = 0.0, egt0 = 0.0, egt1 = 0.0;
     double T0[MAXK], T1[MAXK];
@@ -427,7 +427,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     }
     if (l0 < nlev) {
       int fa = lve(l0), fb = lve(l0 + 1);
-      const int emax = lve(nlev) + 3;  // 4 zero records pad the edge array
+      const int emax = lve(nlev) + 63;  // 64 zero records pad the edge array
       auto rec_at = [&](int f, int lim) -> uint32_t {
         const uint32_t e = Y.ed[min(f, emax)];
         return f < lim ? e : 0u;
@@ -472,12 +472,16 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     // ---- D: G0 row p = G1 + v_s*S, to p's slot (roots are never read).
     // Every later read of element q of this row is by the same lane (q =
     // lane + 64k), so per-thread program order makes it visible: no fence.
+    // Rows never read (pslot 0xffff) go to the slab's last (junk) row, so
+    // the store is unconditional and the R reads of all slots issue back to
+    // back.
     {
-      double* __restrict__ orow = slab + (size_t)(pslot == 0xffffu ? 0u : pslot) * stride + lane;
+      const uint32_t oslot = pslot == 0xffffu ? (uint32_t)(P.slab_doubles / stride - 1) : pslot;
+      double* __restrict__ orow = slab + (size_t)oslot * stride + lane;
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) {
         const double o = R[lane + 64 * k] + xwg * S[k];
-        if (pslot != 0xffffu) orow[64 * k] = o;
+        orow[64 * k] = o;
         // the next row's partial sum: itself (distance-1) + prefetched rows
         S[k] = egd * o + egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
       }
@@ -498,9 +502,12 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
   return kacc;
 }
 
+#ifndef SK_W20
+#define SK_W20 8
+#endif
 template <int MAXK>
 struct StemWaves {
-  static constexpr int value = MAXK <= 16 ? 12 : 8;
+  static constexpr int value = MAXK <= 16 ? 12 : MAXK <= 20 ? SK_W20 : 8;
 };
 
 template <int MAXK>
@@ -560,8 +567,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
         ynr[k].nbp = v ? s.yn_nbp[nb + k] : 0.0f;
         yP[k] = v ? s.yn_P[nb + k] : 0.0;
       }
-      // edges (+4 zero records: reads past the end stay in the array)
-      for (int k = threadIdx.x; k < ne + 4; k += blockDim.x) yed[k] = k < ne ? s.ye[eb + k] : 0u;
+      // edges + 64 zero pad records (reads past the end stay in the array)
+      for (int k = threadIdx.x; k < ne + 64; k += blockDim.x) yed[k] = k < ne ? s.ye[eb + k] : 0u;
       for (int k = threadIdx.x; k < nbf + 1; k += blockDim.x) {
         ybc[k] = k < nbf ? s.bpf_code[bb + k] : 0u;
         ybp[k] = k < nbf ? s.bpf_p[bb + k] : 0.0f;

@@ -804,7 +804,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
         return fail(ctx, SK_ERR_UNSUPPORTED, "y example has more than 127 DAG levels");
       sk::StemLaunch L;
       L.lds_max_nl = 64 * maxk;
-      L.lds_max_edges = (C.max_edges + 4 + 3) & ~3;
+      L.lds_max_edges = C.max_edges + 64;  // + 64 pad records (dag_stem.hip)
       L.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
       L.lds_max_nlev_pad = 128;
       L.lds_max_len_pad = (max_len + 2 + 3) & ~3;
@@ -924,7 +924,8 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     // one scratch buffer serves the class launches in turn (same stream)
     size_t scratch_need = 0;
     for (const StemClass& C : classes) {
-      const int64_t slab = (int64_t)std::max(PX.max_slots, 1) * 64 * C.maxk;
+      // + one junk row: root rows are stored there (never read)
+      const int64_t slab = (int64_t)(PX.max_slots + 1) * 64 * C.maxk;
       scratch_need = std::max(scratch_need, (size_t)C.grid * C.nwaves * slab * sizeof(double));
     }
     rc = ensure_scratch(ctx, std::max<size_t>(scratch_need, 64));
@@ -948,7 +949,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.gap2 = gap2;
       SL.band = kp->len_band;
       SL.lds_max_nl = 64 * C.maxk;
-      SL.lds_max_edges = (C.max_edges + 4 + 3) & ~3;
+      SL.lds_max_edges = C.max_edges + 64;  // + 64 pad records (dag_stem.hip)
       SL.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
       SL.lds_max_nlev_pad = 128;
       SL.lds_max_len_pad = (max_len + 2 + 3) & ~3;
@@ -958,7 +959,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.oidx = d_oidx;
       SL.out = stem_out;
       SL.item_counter = d_ctr + 16 + (int)c;
-      SL.slab_doubles = (int64_t)std::max(PX.max_slots, 1) * SL.lds_max_nl;
+      SL.slab_doubles = (int64_t)(PX.max_slots + 1) * SL.lds_max_nl;
       SL.scratch = ctx->scratch;
 #ifdef SK_STAMPS
       SL.stamps = d_stamps;
