@@ -113,6 +113,10 @@ __device__ __forceinline__ void wave_sync() {
 // scheduling fence: keeps the compiler from hoisting every slot's memory ops
 // to the top of a phase (which would exceed the register budget)
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// waves per workgroup of the MAXK 20 class (8: two prefetched rows; 12: one)
+#ifndef SK_W20
+#define SK_W20 8
+#endif
 #ifndef SK_CHUNK_A
 #define SK_CHUNK_A 8
 #endif
@@ -502,9 +506,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
   return kacc;
 }
 
-#ifndef SK_W20
-#define SK_W20 8
-#endif
 template <int MAXK>
 struct StemWaves {
   static constexpr int value = MAXK <= 16 ? 12 : MAXK <= 20 ? SK_W20 : 8;
