@@ -70,36 +70,37 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 
 // One y node in LDS (16 B, one ds_read_b128 when all fields are needed):
-//   a   = edge_beg:16 | n_edges:8 | n_bpf:8; loop nodes (no non-leaf edges)
-//         carry the gaps of their leaf edge in the low 16 bits instead
-//   b   = len:16 | bpf_beg:16
-//   w   = node weight, nbp = profile gap count at node.first
+//   a   = first edge in the node-major edge array:16 | n_edges:8 | n_bpf:8
+//         (padded nodes: the edge count of the example, no edges)
+//   c   = loop leaf-edge gaps:16 | code of the first bp-freq entry:4 @16 |
+//         single-entry flag @24 (one bp-freq entry and no gap column)
+//   w   = node weight, p0 = probability of the first bp-freq entry
 struct __attribute__((aligned(16))) NodeRec {
-  uint32_t a, b;
-  float w, nbp;
+  uint32_t a, c;
+  float w, p0;
 };
 typedef __attribute__((address_space(3))) NodeRec lds_nr;
 
 __device__ __forceinline__ NodeRec load_nr(const lds_nr* p) {
   NodeRec r;
   r.a = p->a;
-  r.b = p->b;
+  r.c = p->c;
   r.w = p->w;
-  r.nbp = p->nbp;
+  r.p0 = p->p0;
   return r;
 }
 
 struct YView {  // the y example staged in LDS
   const lds_nr* nr;
-  const lds_f64* P;
-  const lds_u32* ed;  // child:11 | parent:11 | gaps:10
-  const lds_u32* bc;
-  const lds_f32* bp;
+  const lds_u32* ed;   // by parent level: child:11 | parent:11 | gaps:10
+  const lds_u32* ed2;  // the same edges node-major (sorted ids)
   const lds_i32* lve;  // level -> first edge
+  const lds_i32* lcm;  // level -> prefix maximum of the children's lengths
   const lds_i32* lfirst;  // length v -> first node (nodes sorted by length), v <= lmax+1
   int lmax;               // largest node length of the example
   int nl, nlev;
   float nseqs;
+  int nb, bb;             // node / bp-freq base of the example in the y set (HBM)
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -142,17 +143,19 @@ __device__ __forceinline__ void wave_sync() {
 
 // node_score(xx,yy,i,j): score_table.cpp:343-380 (Subst) / 193-232 (Simple);
 // co[] holds exp(beta*ribosum) or the match/mismatch table.
+// General case (several bp-freq entries or gap columns; rare): the y
+// entries are read from HBM.
 __device__ __forceinline__ double match_node_score(const lds_f64* co, const DevSet& s, int xbb,
-                                                int xb0, int xnb, const YView& Y, int yb0, int ynb,
-                                                double xwg, double ywg, double x_nbp, double y_nbp,
-                                                double x_nseq) {
+                                                int xb0, int xnb, const DevSet& ys, const YView& Y,
+                                                int yb0, int ynb, double xwg, double ywg,
+                                                double x_nbp, double y_nbp, double x_nseq) {
   double v = 0.0;
   for (int a = 0; a < xnb; ++a) {
     const double cx = (double)s.bpf_p[xbb + xb0 + a];
     const uint32_t ca = s.bpf_code[xbb + xb0 + a] * 16u;
     for (int b = 0; b < ynb; ++b) {
-      const double cy = (double)Y.bp[yb0 + b];
-      v += co[ca + Y.bc[yb0 + b]] * cx * cy;
+      const double cy = (double)ys.bpf_p[Y.bb + yb0 + b];
+      v += co[ca + ys.bpf_code[Y.bb + yb0 + b]] * cx * cy;
     }
   }
   v += ywg * x_nbp / x_nseq;
@@ -183,11 +186,13 @@ __device__ __forceinline__ double match_node_score(const lds_f64* co, const DevS
 //      with w = gap^2*w_y(q)*g^gaps (LDS f64 atomics);
 //   D. G0[p][q] = G1[q] + v_s(p)*S[k] -> slot of p.
 template <int MAXK>
-__device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
+__device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds_f64* hb,
                             const lds_f64* co, const lds_f64* gp, double* __restrict__ slab, int x,
-                            int lane, int lve_lo, int lve_hi, int lcm_lo, int lcm_hi) {
+                            int lane) {
   constexpr int stride = 64 * MAXK;
   const DevSet& s = P.xset;
+  const DevSet& ys = P.yset;
+  const double* __restrict__ yPg = ys.yn_P + Y.nb;  // path counts of y (HBM, L2-resident)
   const int nlx = s.ex_nl[x];
   const int NLy = Y.nl;
   if (nlx == 0 || NLy == 0) return 0.0;
@@ -200,16 +205,13 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
   const XRow* __restrict__ xrows = s.xrow + xnb;
   const double* __restrict__ xsl = P.pn.xr_SL + xnb;
   const uint32_t* __restrict__ xch = s.xr_ch;
-  // first edge of level l (levels are contiguous edge ranges), from registers
-  auto lve = [&](int l) -> int {
-    return __builtin_amdgcn_readlane(l < 64 ? lve_lo : lve_hi, l & 63);
-  };
   // slot index clamped to the last valid node: padded lanes re-read a line
   // other lanes already fetch (no extra HBM traffic)
   const int qlast = NLy - 1;
   double kacc = 0.0;
 #ifdef SK_STAMPS
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long cnt[4] = {0, 0, 0, 0};  // A-loaded rows, levels, passes, band nodes
   unsigned long long tlast = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -285,6 +287,13 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
         }
       }
     }
+#ifdef SK_STAMPS
+    {
+      int nl_ = 0;
+      for (int j = 0; j < 4; ++j) nl_ += (j < xne && !(done >> j & 1u)) ? 1 : 0;
+      cnt[0] += nl_ + (xne > 4 ? xne - 4 : 0);
+    }
+#endif
     for (int t = 4; t < xne; t += 2) {  // children past the fourth
       const uint32_t c0 = xch[chp_r + t];
       const bool two = t + 1 < xne;
@@ -308,6 +317,11 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     //      S of its children, which are strictly shorter, so a pass may
     //      overwrite R (S -> M) for the nodes it finished without affecting a
     //      later pass.  Everything outside the range gets M = 0 afterwards.
+    //      Within a pass the child sums are edge-parallel: the pass's nodes
+    //      own one contiguous range of the node-major edge array, each lane
+    //      takes edges of it and adds g^gy S[child] into the per-wave
+    //      accumulator hb[parent - q0] (LDS atomics), so the cost follows
+    //      the pass's edge count, not its largest node degree.
     //      (LDS ops of a wave complete in issue order.)
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = S[k];
@@ -320,38 +334,46 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     qb = __builtin_amdgcn_readfirstlane(qb);
     double rowk = 0.0;
     for (int top = qb - 1; top >= qa; top -= 64) {
-      const int q = top - lane;
-      const bool on = q >= qa;
-      const int qq = on ? q : qa;
-      const NodeRec nd = load_nr(&Y.nr[qq]);
-      const int ne = (nd.a >> 16) & 0xff;
+      const int q0 = max(top - 63, qa);
+      const int q = q0 + lane;
+      const bool on = q <= top;
+      const NodeRec nd = load_nr(&Y.nr[on ? q : top]);
+      const double Pq = yPg[on ? q : top];
       double Hq;
-      if (ne == 0) {  // loop node: closed form over the two leaf children
-        Hq = (xloop ? xeg0 : xSL) * gp[nd.a & 0xffff];
-      } else if (xloop) {  // x leaf child against a y stem: G0[leaf][*] = 0
-        Hq = 0.0;
-      } else {  // sum_{cy in ch(q)} g^gy S[cy]
-        const int e0 = nd.a & 0xffff;
-        Hq = 0.0;
-        for (int j = 0; j < ne; ++j) {
-          const uint32_t f = Y.ed[e0 + j];
-          Hq += gp[f >> 22] * R[f & 0x7ff];
+      if (!xloop) {
+        // edge range of nodes [q0, top]: E(q0) .. E(top + 1) (padded nodes
+        // carry the total edge count)
+        const int ea = __builtin_amdgcn_readfirstlane(Y.nr[q0].a & 0xffff);
+        const int eb = __builtin_amdgcn_readfirstlane(Y.nr[top + 1].a & 0xffff);
+        for (int f = ea + lane; f < eb; f += 64) {
+          const uint32_t e = Y.ed2[f];
+          __hip_atomic_fetch_add(&hb[((e >> 11) & 0x7ff) - q0], gp[e >> 22] * R[e & 0x7ff],
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
+        Hq = hb[lane];
+        hb[lane] = 0.0;
+      } else {  // x leaf child against a y stem: G0[leaf][*] = 0
+        Hq = 0.0;
       }
+      const int ne = (nd.a >> 16) & 0xff;
+      if (ne == 0)  // loop node: closed form over the two leaf children
+        Hq = (xloop ? xeg0 : xSL) * gp[nd.c & 0xffff];
       double vs;
-      if (x_one && (nd.a >> 24) == 1u && nd.nbp == 0.0f) {
+      if (x_one && (nd.c >> 24) != 0u) {
         // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:350-364)
-        vs = co[xcode + Y.bc[nd.b >> 16]] * xpf * (double)Y.bp[nd.b >> 16];
+        vs = co[xcode + ((nd.c >> 16) & 0xf)] * xpf * (double)nd.p0;
       } else {
         // general bp-frequency lists / gap columns (score_table.cpp:343-380)
-        vs = Hq != 0.0 ? match_node_score(co, s, xbb, xb0, xnbf, Y, nd.b >> 16, nd.a >> 24, xwg,
-                                           gap2 * (double)nd.w, x_nbp, (double)nd.nbp, x_nseq)
+        const int qq = on ? q : top;
+        vs = Hq != 0.0 ? match_node_score(co, s, xbb, xb0, xnbf, ys, Y, ys.yn_b[Y.nb + qq] >> 16,
+                                           nd.a >> 24, xwg, gap2 * (double)nd.w, x_nbp,
+                                           (double)ys.yn_nbp[Y.nb + qq], x_nseq)
                        : 0.0;
       }
       const double M = vs * Hq;
       if (on) {
         R[q] = M;
-        rowk += M * Y.P[q];
+        rowk += M * Pq;
       }
     }
     // outside the band: M = 0
@@ -425,11 +447,20 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     int l0 = 1;
     if (band > 0) {
       const int thr = xlen - band;
-      const uint64_t blo = __ballot(lane >= 1 && lane < nlev && lcm_lo >= thr);
-      const uint64_t bhi = __ballot(lane + 64 < nlev && lcm_hi >= thr);
+      const uint64_t blo = __ballot(lane >= 1 && lane < nlev && Y.lcm[lane] >= thr);
+      const uint64_t bhi = __ballot(lane + 64 < nlev && Y.lcm[64 + lane] >= thr);
       l0 = blo ? (int)__builtin_ctzll(blo) : (bhi ? 64 + (int)__builtin_ctzll(bhi) : nlev);
     }
+#ifdef SK_STAMPS
+    cnt[1] += l0 < nlev ? nlev - l0 : 0;
+#endif
     if (l0 < nlev) {
+      // first edge of level l (levels are contiguous edge ranges): loaded
+      // into two registers per sweep, read with readlane per level
+      const int lve_lo = Y.lve[lane], lve_hi = Y.lve[64 + lane];
+      auto lve = [&](int l) -> int {
+        return __builtin_amdgcn_readlane(l < 64 ? lve_lo : lve_hi, l & 63);
+      };
       int fa = lve(l0), fb = lve(l0 + 1);
       const int emax = lve(nlev) + 63;  // 64 zero records pad the edge array
       auto rec_at = [&](int f, int lim) -> uint32_t {
@@ -499,6 +530,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R,
     for (int i = 0; i < 6; ++i) atomicAdd(&P.stamps[i], tacc[i]);
     atomicAdd(&P.stamps[6], (unsigned long long)nlx);
     atomicAdd(&P.stamps[7], 1ull);
+    for (int i = 0; i < 4; ++i) atomicAdd(&P.stamps[8 + i], cnt[i]);
   }
 #endif
   // wave reduction of the K partial sums (fixed order -> deterministic)
@@ -522,13 +554,12 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   // LDS carve (every region a multiple of 16 bytes)
   lds_f64* co = (lds_f64*)(smem);                             // 256
   lds_f64* gp = co + 256;                                     // n_gpow_pad
-  lds_f64* yP = gp + P.n_gpow_pad;                            // maxnl
-  lds_f64* Rall = yP + maxnl;                                 // nwaves*maxnl
-  lds_u32* yed = (lds_u32*)(Rall + (size_t)nwaves * maxnl);   // lds_max_edges (mult. of 4)
-  lds_nr* ynr = (lds_nr*)(yed + P.lds_max_edges);             // maxnl node records
-  lds_u32* ybc = (lds_u32*)(ynr + maxnl);                     // lds_max_bpf
-  lds_f32* ybp = (lds_f32*)(ybc + P.lds_max_bpf);
-  lds_i32* ylve = (lds_i32*)(ybp + P.lds_max_bpf);            // lds_max_nlev_pad
+  lds_f64* Rall = gp + P.n_gpow_pad;                          // nwaves*maxnl
+  lds_f64* hball = Rall + (size_t)nwaves * maxnl;             // nwaves*64 (MATCH sums)
+  lds_nr* ynr = (lds_nr*)(hball + (size_t)nwaves * 64);       // maxnl+1 node records
+  lds_u32* yed = (lds_u32*)(ynr + maxnl + 1);                 // lds_max_edges (mult. of 4)
+  lds_u32* yed2 = yed + P.lds_max_edges;                      // lds_max_edges
+  lds_i32* ylve = (lds_i32*)(yed2 + P.lds_max_edges);         // lds_max_nlev_pad
   lds_i32* ylcm = ylve + P.lds_max_nlev_pad;                  // lds_max_nlev_pad
   lds_i32* ylf = ylcm + P.lds_max_nlev_pad;                   // lds_max_len_pad
   lds_i32* ctl = ylf + P.lds_max_len_pad;                     // 4 ints
@@ -537,6 +568,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   for (int k = threadIdx.x; k < P.n_gpow; k += blockDim.x) gp[k] = P.gpow[k];
 
   lds_f64* R = Rall + (size_t)wave * maxnl;
+  lds_f64* hb = hball + (size_t)wave * 64;
+  hb[lane] = 0.0;  // kept zero between MATCH passes
   double* slab = P.scratch + (size_t)(blockIdx.x * nwaves + wave) * P.slab_doubles;
   const double gap2 = P.gap2;
 
@@ -556,32 +589,30 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     Y.nseqs = s.ex_nseqs[y];
     const int nb = s.ex_node_base[y], eb = s.ex_edge_base[y], bb = s.ex_bpf_base[y];
     {
-      const int ne = s.ex_edge_base[y + 1] - eb, nbf = s.ex_bpf_base[y + 1] - bb;
+      const int ne = s.ex_edge_base[y + 1] - eb;
       const int lb = s.ex_ylve_base[y];
-      // node records in slot order, zero padded to 64*MAXK (padded q: no
-      // edges, out of band)
-      for (int k = threadIdx.x; k < 64 * MAXK; k += blockDim.x) {
+      // node records in slot order, padded to 64*MAXK+1 (padded q: no
+      // edges, first edge = the edge count, out of band)
+      for (int k = threadIdx.x; k <= 64 * MAXK; k += blockDim.x) {
         const bool v = k < Y.nl;
-        ynr[k].a = v ? s.yn_a[nb + k] : 0u;
-        ynr[k].b = v ? s.yn_b[nb + k] : 0u;
+        ynr[k].a = v ? s.yn_a[nb + k] : (uint32_t)ne;
+        ynr[k].c = v ? s.yn_c[nb + k] : 0u;
         ynr[k].w = v ? s.yn_w[nb + k] : 0.0f;
-        ynr[k].nbp = v ? s.yn_nbp[nb + k] : 0.0f;
-        yP[k] = v ? s.yn_P[nb + k] : 0.0;
+        ynr[k].p0 = v ? s.yn_p0[nb + k] : 0.0f;
       }
-      // edges + 64 zero pad records (reads past the end stay in the array)
+      // edges by level + 64 zero pad records (reads past the end stay in
+      // the array), and node-major
       for (int k = threadIdx.x; k < ne + 64; k += blockDim.x) yed[k] = k < ne ? s.ye[eb + k] : 0u;
-      for (int k = threadIdx.x; k < nbf + 1; k += blockDim.x) {
-        ybc[k] = k < nbf ? s.bpf_code[bb + k] : 0u;
-        ybp[k] = k < nbf ? s.bpf_p[bb + k] : 0.0f;
-      }
+      for (int k = threadIdx.x; k < ne; k += blockDim.x) yed2[k] = s.ye2[eb + k];
       // first edge of each level (levels >= 1 are contiguous edge ranges)
       for (int k = threadIdx.x; k < P.lds_max_nlev_pad; k += blockDim.x) {
         ylve[k] = k <= Y.nlev ? s.ylve[lb + k] : ne;
         ylcm[k] = k <= Y.nlev ? s.ylcm[lb + k] : 0x7fffffff;
       }
     }
-    Y.nr = ynr; Y.P = yP;
-    Y.ed = yed; Y.bc = ybc; Y.bp = ybp; Y.lve = ylve; Y.lfirst = ylf;
+    Y.nr = ynr;
+    Y.ed = yed; Y.ed2 = yed2; Y.lve = ylve; Y.lcm = ylcm; Y.lfirst = ylf;
+    Y.nb = nb; Y.bb = bb;
     Y.lmax = Y.nl ? (int)(s.yn_b[nb + Y.nl - 1] & 0xffff) : 0;
     __syncthreads();
     // length -> first node index (nodes are sorted by length)
@@ -589,19 +620,17 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
       int lo = 0, hi = Y.nl;  // first q with len(q) >= v
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if ((int)(ynr[mid].b & 0xffff) < v) lo = mid + 1; else hi = mid;
+        if ((int)(s.yn_b[nb + mid] & 0xffff) < v) lo = mid + 1; else hi = mid;
       }
       ylf[v] = lo;
     }
     __syncthreads();
-    const int lve_lo = ylve[lane], lve_hi = ylve[64 + lane];  // level -> first edge
-    const int lcm_lo = ylcm[lane], lcm_hi = ylcm[64 + lane];  // prefix max child length
 
     // static round-robin of the item's pairs over the waves (uniform loop)
     for (int t = wave_u; t < item.z; t += nwaves) {
       const int x = P.xs[item.y + t];
       const double k =
-          stem_pair<MAXK>(P, Y, R, co, gp, slab, x, lane, lve_lo, lve_hi, lcm_lo, lcm_hi);
+          stem_pair<MAXK>(P, Y, R, hb, co, gp, slab, x, lane);
       if (lane == 0) P.out[P.oidx[item.y + t]] = k;
     }
   }
@@ -621,11 +650,10 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   size_t b = 0;
   b += 256 * 8;
   b += (size_t)P.n_gpow_pad * 8;
-  b += (size_t)P.lds_max_nl * 8;                   // yP
   b += (size_t)nwaves * P.lds_max_nl * 8;          // one row per wave
-  b += (size_t)P.lds_max_edges * 4;                // packed edges
-  b += (size_t)P.lds_max_nl * 16;                  // node records
-  b += (size_t)P.lds_max_bpf * 8;
+  b += (size_t)nwaves * 64 * 8;                    // MATCH accumulators
+  b += (size_t)(P.lds_max_nl + 1) * 16;            // node records
+  b += (size_t)P.lds_max_edges * 4 * 2;            // edges by level (+ pad), node-major
   b += (size_t)P.lds_max_nlev_pad * 8;
   b += (size_t)P.lds_max_len_pad * 4 + 16;
   return b;

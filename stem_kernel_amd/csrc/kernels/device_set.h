@@ -67,12 +67,15 @@ struct DevSet {
   const uint32_t* xr_ch = nullptr;  // per child edge: child slot:16 | gaps:16
   // y role of the stem kernel: non-leaf nodes sorted by edge count (slot
   // order), edges grouped by parent level, packed child:11|parent:11|gaps:10
-  const uint32_t* yn_a = nullptr;   // e0:16 (loops: leaf-edge gaps) | n_edges:8 | n_bpf:8
+  const uint32_t* yn_a = nullptr;   // first edge in ye2:16 | n_edges:8 | n_bpf:8
   const uint32_t* yn_b = nullptr;   // len:16 | bpf_beg:16
   const float* yn_w = nullptr;
   const float* yn_nbp = nullptr;
   const double* yn_P = nullptr;
-  const uint32_t* ye = nullptr;     // edges (local ids), ex_edge_base[e] per example
+  const uint32_t* yn_c = nullptr;   // loop leaf-edge gaps:16 | bc0:4 | single-entry flag @24
+  const float* yn_p0 = nullptr;     // p of the first bp-freq entry
+  const uint32_t* ye = nullptr;     // edges (local ids) by parent level, ex_edge_base[e] per example
+  const uint32_t* ye2 = nullptr;    // the same edges node-major (sorted ids)
   const int32_t* ylve = nullptr;    // per level: first edge (nlev+1 entries)
   const int32_t* ylcm = nullptr;    // per level: max child length over levels 1..l (same base)
   const int32_t* ex_ylve_base = nullptr;

@@ -82,8 +82,8 @@ struct HostPack {
   std::vector<float4> pos_lru;
   std::vector<int32_t> ex_nslots, ex_xch_base;
   std::vector<sk::XRow> xrow;
-  std::vector<uint32_t> yn_a, yn_b, ye;
-  std::vector<float> yn_w, yn_nbp;
+  std::vector<uint32_t> yn_a, yn_b, yn_c, ye, ye2;
+  std::vector<float> yn_w, yn_nbp, yn_p0;
   std::vector<double> yn_P;
   std::vector<int32_t> ylve, ylcm, ex_ylve_base;
   std::vector<uint32_t> xr_node, xr_ch;
@@ -246,7 +246,6 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       std::vector<int> pos(nl);
       for (int i = 0; i < nl; ++i) pos[srt[i]] = i;
       const int nb0 = P.ex_node_base.back();
-      std::vector<uint32_t> e0_of(nl, 0);
       const int ye_base = (int)P.ye.size();
       P.ex_ylve_base.push_back((int32_t)P.ylve.size());
       for (int l = 0; l < nlev; ++l) {
@@ -254,7 +253,6 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         for (int k = lv[l]; k < lv[l + 1]; ++k) {  // level-order ids of level l
           const uint32_t a = P.nd_a[nb0 + k];
           const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
-          e0_of[k] = (uint32_t)P.ye.size() - ye_base;
           for (uint32_t t = 0; t < ne; ++t) {
             const uint2 rec = P.ed[ebase + el + t];  // {child | gaps<<16, parent}
             P.ye.push_back((uint32_t)pos[rec.x & 0xffff] | ((uint32_t)pos[k] << 11) |
@@ -281,12 +279,27 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         }
         P.ylcm.push_back(run);  // entry nlev (unused)
       }
+      // node-major copy of the edges in sorted order (the MATCH sums of a
+      // run of consecutive nodes read one contiguous edge range); a node's
+      // record keeps its first edge there, E(q) = prefix sum of n_edges
+      const int ye2_base = (int)P.ye2.size();
       for (int i = 0; i < nl; ++i) {
         const int k = srt[i];
         const uint32_t a = P.nd_a[nb0 + k];
-        const uint32_t ne = (a >> 16) & 0xff;
-        // loops carry their leaf-edge gaps where stems keep their first edge
-        P.yn_a.push_back((ne ? e0_of[k] : P.nd_c[nb0 + k]) | (a & 0xffff0000u));
+        const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
+        const uint32_t nbf = a >> 24, bl = P.nd_b[nb0 + k] >> 16;
+        P.yn_a.push_back(((uint32_t)P.ye2.size() - ye2_base) | (a & 0xffff0000u));
+        for (uint32_t t = 0; t < ne; ++t) {
+          const uint2 rec = P.ed[ebase + el + t];
+          P.ye2.push_back((uint32_t)pos[rec.x & 0xffff] | ((uint32_t)i << 11) |
+                          ((rec.x >> 16) << 22));
+        }
+        // c = loop leaf-edge gaps:16 | first bp-freq code:4 | single-entry flag
+        // (one bp-freq entry, no gap column: the closed-form node score)
+        const bool one = nbf == 1 && P.nd_nbp[nb0 + k] == 0.0f;
+        const uint32_t bc0 = nbf ? P.bpf_code[bbase + bl] & 0xf : 0u;
+        P.yn_c.push_back((P.nd_c[nb0 + k] & 0xffff) | (bc0 << 16) | ((one ? 1u : 0u) << 24));
+        P.yn_p0.push_back(nbf ? P.bpf_p[bbase + bl] : 0.0f);
         P.yn_b.push_back(P.nd_b[nb0 + k]);
         P.yn_w.push_back(P.nd_w[nb0 + k]);
         P.yn_nbp.push_back(P.nd_nbp[nb0 + k]);
@@ -932,8 +945,8 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     if (rc) return rc;
 #ifdef SK_STAMPS
     unsigned long long* d_stamps = nullptr;
-    SK_HIP(ctx, hipMalloc(&d_stamps, 8 * sizeof(unsigned long long)));
-    SK_HIP(ctx, hipMemsetAsync(d_stamps, 0, 8 * sizeof(unsigned long long), S));
+    SK_HIP(ctx, hipMalloc(&d_stamps, 16 * sizeof(unsigned long long)));
+    SK_HIP(ctx, hipMemsetAsync(d_stamps, 0, 16 * sizeof(unsigned long long), S));
 #endif
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     for (size_t c = 0; c < classes.size(); ++c) {
@@ -969,7 +982,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
 #ifdef SK_STAMPS
     {
-      unsigned long long h[8];
+      unsigned long long h[16];
       SK_HIP(ctx, hipMemcpyAsync(h, d_stamps, sizeof(h), hipMemcpyDeviceToHost, S));
       SK_HIP(ctx, hipStreamSynchronize(S));
       (void)hipFree(d_stamps);
@@ -978,7 +991,8 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
                    h[7], rows);
       const char* nm[6] = {"hdr", "load", "gather", "match", "sweep", "store"};
       for (int i = 0; i < 6; ++i) std::fprintf(stderr, " %s=%.0f", nm[i], h[i] / rows);
-      std::fprintf(stderr, "\n");
+      std::fprintf(stderr, "\n[stamps] per row: A-loaded rows=%.3f swept levels=%.2f match passes=%.2f band nodes=%.1f\n",
+                   h[8] / rows, h[9] / rows, h[10] / rows, h[11] / rows);
       for (const StemClass& C : classes)
         std::fprintf(stderr, "[stamps] class maxk=%d max_nl=%d waves/wg=%d grid=%d items=%zu\n",
                      C.maxk, C.max_nl, C.nwaves, C.grid, C.n_items);
@@ -1341,6 +1355,9 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.yn_nbp, &D.yn_nbp));
   SK_HIP(ctx, upload(B, P.yn_P, &D.yn_P));
   SK_HIP(ctx, upload(B, P.ye, &D.ye));
+  SK_HIP(ctx, upload(B, P.ye2, &D.ye2));
+  SK_HIP(ctx, upload(B, P.yn_c, &D.yn_c));
+  SK_HIP(ctx, upload(B, P.yn_p0, &D.yn_p0));
   SK_HIP(ctx, upload(B, P.ylve, &D.ylve));
   SK_HIP(ctx, upload(B, P.ylcm, &D.ylcm));
   SK_HIP(ctx, upload(B, P.ex_ylve_base, &D.ex_ylve_base));
