@@ -69,36 +69,20 @@ typedef __attribute__((address_space(3))) float lds_f32;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 
-// One y node in LDS (16 B, one ds_read_b128 when all fields are needed):
-//   a   = first edge in the node-major edge array:16 | n_edges:8 | n_bpf:8
-//         (padded nodes: the edge count of the example, no edges)
-//   c   = loop leaf-edge gaps:16 | code of the first bp-freq entry:4 @16 |
-//         single-entry flag @24 (one bp-freq entry and no gap column)
-//   w   = node weight, p0 = probability of the first bp-freq entry
-struct __attribute__((aligned(16))) NodeRec {
-  uint32_t a, c;
-  float w, p0;
-};
-typedef __attribute__((address_space(3))) NodeRec lds_nr;
-
-__device__ __forceinline__ NodeRec load_nr(const lds_nr* p) {
-  NodeRec r;
-  r.a = p->a;
-  r.c = p->c;
-  r.w = p->w;
-  r.p0 = p->p0;
-  return r;
-}
-
-struct YView {  // the y example staged in LDS
-  const lds_nr* nr;
-  const lds_u32* ed;   // by parent level: child:11 | parent:11 | gaps:10
-  const lds_u32* ed2;  // the same edges node-major (sorted ids)
-  const lds_i32* lve;  // level -> first edge
-  const lds_i32* lcm;  // level -> prefix maximum of the children's lengths
+// One y node record (16 B, one global_load_dwordx4):
+//   a = first edge in the node-major edge array:16 | n_edges:8 | n_bpf:8
+//   c = loop leaf-edge gaps:16 | code of the first bp-freq entry:4 @16 |
+//       single-entry flag @24 (one bp-freq entry and no gap column)
+//   w = node weight, p0 = probability of the first bp-freq entry (float bits)
+struct YView {  // the y example (staged in LDS unless noted)
+  const uint4* __restrict__ nrg;  // node records {a, c, w, p0} (HBM, L2-resident)
+  const lds_u32* sc;   // sweep schedule: (nch + 2) chunks of 64 child:11 | parent:11 | gaps:10
+  const lds_f64* ew;   // their weights gap^2 w(parent) g^gaps (0 for dummies)
+  const lds_u32* ed2;  // edges node-major (sorted ids)
   const lds_i32* lfirst;  // length v -> first node (nodes sorted by length), v <= lmax+1
+  const lds_i32* ycs;     // length v -> first sweep chunk reaching v, v <= lmax+1
   int lmax;               // largest node length of the example
-  int nl, nlev;
+  int nl, nch;
   float nseqs;
   int nb, bb;             // node / bp-freq base of the example in the y set (HBM)
 };
@@ -117,6 +101,9 @@ __device__ __forceinline__ void wave_sync() {
 // waves per workgroup of the MAXK 20 class (8: two prefetched rows; 12: one)
 #ifndef SK_W20
 #define SK_W20 8
+#endif
+#ifndef SK_SW  // IY sweep chunk width in 64-edge groups
+#define SK_SW 2
 #endif
 #ifndef SK_CHUNK_A
 #define SK_CHUNK_A 8
@@ -199,7 +186,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
   const int xnb = s.ex_node_base[x], xbb = s.ex_bpf_base[x];
   int chp = s.ex_xch_base[x];
   const double x_nseq = (double)s.ex_nseqs[x];
-  const int nlev = Y.nlev;
   const double gap2 = P.gap2;
   const int band = (int)P.band;
   const XRow* __restrict__ xrows = s.xrow + xnb;
@@ -333,47 +319,62 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     qa = __builtin_amdgcn_readfirstlane(qa);
     qb = __builtin_amdgcn_readfirstlane(qb);
     double rowk = 0.0;
-    for (int top = qb - 1; top >= qa; top -= 64) {
-      const int q0 = max(top - 63, qa);
-      const int q = q0 + lane;
-      const bool on = q <= top;
-      const NodeRec nd = load_nr(&Y.nr[on ? q : top]);
-      const double Pq = yPg[on ? q : top];
-      double Hq;
-      if (!xloop) {
-        // edge range of nodes [q0, top]: E(q0) .. E(top + 1) (padded nodes
-        // carry the total edge count)
-        const int ea = __builtin_amdgcn_readfirstlane(Y.nr[q0].a & 0xffff);
-        const int eb = __builtin_amdgcn_readfirstlane(Y.nr[top + 1].a & 0xffff);
-        for (int f = ea + lane; f < eb; f += 64) {
-          const uint32_t e = Y.ed2[f];
-          __hip_atomic_fetch_add(&hb[((e >> 11) & 0x7ff) - q0], gp[e >> 22] * R[e & 0x7ff],
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (qa < qb) {
+      // node records and path counts come from HBM (L2-resident per y),
+      // each pass's prefetched during the pass before
+      int top = qb - 1, q0 = max(top - 63, qa);
+      uint4 nd_n = Y.nrg[min(q0 + lane, top)];
+      double Pq_n = yPg[min(q0 + lane, top)];
+      for (;;) {
+        const uint4 nd = nd_n;
+        const double Pq = Pq_n;
+        const int ntop = top - 64, nq0 = max(ntop - 63, qa);
+        if (ntop >= qa) {
+          nd_n = Y.nrg[min(nq0 + lane, ntop)];
+          Pq_n = yPg[min(nq0 + lane, ntop)];
         }
-        Hq = hb[lane];
-        hb[lane] = 0.0;
-      } else {  // x leaf child against a y stem: G0[leaf][*] = 0
-        Hq = 0.0;
-      }
-      const int ne = (nd.a >> 16) & 0xff;
-      if (ne == 0)  // loop node: closed form over the two leaf children
-        Hq = (xloop ? xeg0 : xSL) * gp[nd.c & 0xffff];
-      double vs;
-      if (x_one && (nd.c >> 24) != 0u) {
-        // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:350-364)
-        vs = co[xcode + ((nd.c >> 16) & 0xf)] * xpf * (double)nd.p0;
-      } else {
-        // general bp-frequency lists / gap columns (score_table.cpp:343-380)
-        const int qq = on ? q : top;
-        vs = Hq != 0.0 ? match_node_score(co, s, xbb, xb0, xnbf, ys, Y, ys.yn_b[Y.nb + qq] >> 16,
-                                           nd.a >> 24, xwg, gap2 * (double)nd.w, x_nbp,
-                                           (double)ys.yn_nbp[Y.nb + qq], x_nseq)
-                       : 0.0;
-      }
-      const double M = vs * Hq;
-      if (on) {
-        R[q] = M;
-        rowk += M * Pq;
+        const int q = q0 + lane;
+        const bool on = q <= top;
+        const uint32_t nda = nd.x, ndc = nd.y;
+        double Hq;
+        if (!xloop) {
+          // edge range of nodes [q0, top]: E(q0) .. E(top) + n_edges(top)
+          const int ea = __builtin_amdgcn_readfirstlane(nda & 0xffff);
+          const uint32_t at = __builtin_amdgcn_readlane(nda, top - q0);
+          const int eb = (int)((at & 0xffff) + ((at >> 16) & 0xff));
+          for (int f = ea + lane; f < eb; f += 64) {
+            const uint32_t e = Y.ed2[f];
+            __hip_atomic_fetch_add(&hb[((e >> 11) & 0x7ff) - q0], gp[e >> 22] * R[e & 0x7ff],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+          }
+          Hq = hb[lane];
+          hb[lane] = 0.0;
+        } else {  // x leaf child against a y stem: G0[leaf][*] = 0
+          Hq = 0.0;
+        }
+        const int ne = (nda >> 16) & 0xff;
+        if (ne == 0)  // loop node: closed form over the two leaf children
+          Hq = (xloop ? xeg0 : xSL) * gp[ndc & 0xffff];
+        double vs;
+        if (x_one && (ndc >> 24) != 0u) {
+          // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:350-364)
+          vs = co[xcode + ((ndc >> 16) & 0xf)] * xpf * (double)__uint_as_float(nd.w);
+        } else {
+          // general bp-frequency lists / gap columns (score_table.cpp:343-380)
+          const int qq = on ? q : top;
+          vs = Hq != 0.0 ? match_node_score(co, s, xbb, xb0, xnbf, ys, Y, ys.yn_b[Y.nb + qq] >> 16,
+                                             nda >> 24, xwg, gap2 * (double)__uint_as_float(nd.z),
+                                             x_nbp, (double)ys.yn_nbp[Y.nb + qq], x_nseq)
+                         : 0.0;
+        }
+        const double M = vs * Hq;
+        if (on) {
+          R[q] = M;
+          rowk += M * Pq;
+        }
+        if (ntop < qa) break;
+        top = ntop;
+        q0 = nq0;
       }
     }
     // outside the band: M = 0
@@ -435,72 +436,61 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       }
     }
 
-    // ---- C: IY recurrence, level by level, edge-parallel (levels >= 1).
-    //         Edge records are read two levels ahead and their weights one
-    //         level ahead, so only R[child] -> atomic stays on the chain.
-    //         Lanes past a level's edges use record 0 with weight 0.
-    // With a length band, every y node shorter than xlen - band has G1 = 0
-    // exactly (its MATCH terms are masked and so are all its descendants'),
-    // so sweep levels whose children are all that short add only zeros:
-    // start at the first level whose running maximum child length reaches
-    // the threshold (lcm = per-level prefix maximum, staged per item).
-    int l0 = 1;
-    if (band > 0) {
-      const int thr = xlen - band;
-      const uint64_t blo = __ballot(lane >= 1 && lane < nlev && Y.lcm[lane] >= thr);
-      const uint64_t bhi = __ballot(lane + 64 < nlev && Y.lcm[64 + lane] >= thr);
-      l0 = blo ? (int)__builtin_ctzll(blo) : (bhi ? 64 + (int)__builtin_ctzll(bhi) : nlev);
-    }
+    // ---- C: IY recurrence G1[q] += w(q,cy) G1[cy], w = gap^2 w_y(q) g^gaps,
+    //      over the y example's sweep schedule: chunks of 64 edges, each
+    //      placed after every edge of its children (host list schedule).  A
+    //      chunk's R reads are issued after the previous chunk's atomics and
+    //      a wave's LDS ops execute in issue order, so nothing drains between
+    //      chunks: only the data a lane consumes is waited for.  Records are
+    //      read two chunks ahead, weights one; dummy records (weight 0) pad
+    //      the chunks.
+    //      With a length band, every y node shorter than xlen - band has G1 =
+    //      0 exactly (its MATCH terms are masked and so are all its
+    //      descendants'), so chunks whose children are all that short add
+    //      only zeros: the sweep starts at the first chunk whose running
+    //      maximum child length reaches the threshold.
+    int c0 = 0;
+    if (band > 0) c0 = Y.ycs[min(max(xlen - band, 0), Y.lmax + 1)];
+    c0 = __builtin_amdgcn_readfirstlane(c0);
 #ifdef SK_STAMPS
-    cnt[1] += l0 < nlev ? nlev - l0 : 0;
+    cnt[1] += Y.nch - c0;
 #endif
-    if (l0 < nlev) {
-      // first edge of level l (levels are contiguous edge ranges): loaded
-      // into two registers per sweep, read with readlane per level
-      const int lve_lo = Y.lve[lane], lve_hi = Y.lve[64 + lane];
-      auto lve = [&](int l) -> int {
-        return __builtin_amdgcn_readlane(l < 64 ? lve_lo : lve_hi, l & 63);
+    if (c0 < Y.nch) {
+      const lds_u32* rp = Y.sc + c0 * 64 + lane;
+      const lds_f64* wp = Y.ew + c0 * 64 + lane;
+      // three chunk slots in rotation (the loop is unrolled by three, so no
+      // loaded register is ever copied, which would force a wait for it)
+      struct Ck {
+        uint32_t rec;
+        double w, rv;
       };
-      int fa = lve(l0), fb = lve(l0 + 1);
-      const int emax = lve(nlev) + 63;  // 64 zero records pad the edge array
-      auto rec_at = [&](int f, int lim) -> uint32_t {
-        const uint32_t e = Y.ed[min(f, emax)];
-        return f < lim ? e : 0u;
+      Ck A, B, C;
+      A.rec = rp[0];
+      A.w = wp[0];
+      B.rec = rp[64];
+      B.w = 0.0;
+      C.rec = 0u;
+      C.w = C.rv = B.rv = 0.0;
+      A.rv = R[A.rec & 0x7ff];
+      int c = c0;
+      const int nch = Y.nch;
+      // chunk X now, Y next, Z after: false after the last chunk
+      auto step = [&](Ck& X, Ck& Yc, Ck& Z) __attribute__((always_inline)) -> bool {
+        Z.rec = rp[128];
+        Yc.w = wp[64];
+        __hip_atomic_fetch_add(&R[(X.rec >> 11) & 0x7ff], X.rv * X.w, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+        Yc.rv = R[Yc.rec & 0x7ff];
+        rp += 64;
+        wp += 64;
+        return ++c < nch;
       };
-      auto wt = [&](uint32_t e, bool on) -> double {
-        const double w = gap2 * (double)Y.nr[(e >> 11) & 0x7ff].w * gp[e >> 22];
-        return on ? w : 0.0;
-      };
-      uint32_t rec = rec_at(fa + lane, fb);
-      double w = wt(rec, fa + lane < fb);
-      int fc = l0 + 2 <= nlev ? lve(l0 + 2) : fb;
-      uint32_t rec1 = rec_at(fb + lane, fc);
-      for (int l = l0; l < nlev; ++l) {
-        // level l: edges [fa, fb); level l+1: [fb, fc); level l+2: [fc, fd)
-        // the level's R reads go first, so waiting for them does not wait
-        // for the prefetches behind them (LDS ops complete in order)
-        const double add = R[rec & 0x7ff] * w;
-        const int fd = l + 3 <= nlev ? lve(l + 3) : fc;
-        const uint32_t rec2 = rec_at(fc + lane, fd);
-        const double w1 = wt(rec1, fb + lane < fc);
-        if (fa + lane < fb)
-          __hip_atomic_fetch_add(&R[(rec >> 11) & 0x7ff], add, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WAVEFRONT);
-        if (fb - fa > 64) {  // levels with more than 64 edges
-          for (int f = fa + 64 + lane; f < fb; f += 64) {
-            const uint32_t rr = Y.ed[f];
-            __hip_atomic_fetch_add(&R[(rr >> 11) & 0x7ff], R[rr & 0x7ff] * wt(rr, true),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-          }
-        }
-        wave_sync();
-        fa = fb;
-        fb = fc;
-        fc = fd;
-        rec = rec1;
-        w = w1;
-        rec1 = rec2;
+      for (;;) {
+        if (!step(A, B, C)) break;
+        if (!step(B, C, A)) break;
+        if (!step(C, A, B)) break;
       }
+      wave_sync();
     }
     STAMP(4);
 
@@ -556,13 +546,12 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   lds_f64* gp = co + 256;                                     // n_gpow_pad
   lds_f64* Rall = gp + P.n_gpow_pad;                          // nwaves*maxnl
   lds_f64* hball = Rall + (size_t)nwaves * maxnl;             // nwaves*64 (MATCH sums)
-  lds_nr* ynr = (lds_nr*)(hball + (size_t)nwaves * 64);       // maxnl+1 node records
-  lds_u32* yed = (lds_u32*)(ynr + maxnl + 1);                 // lds_max_edges (mult. of 4)
-  lds_u32* yed2 = yed + P.lds_max_edges;                      // lds_max_edges
-  lds_i32* ylve = (lds_i32*)(yed2 + P.lds_max_edges);         // lds_max_nlev_pad
-  lds_i32* ylcm = ylve + P.lds_max_nlev_pad;                  // lds_max_nlev_pad
-  lds_i32* ylf = ylcm + P.lds_max_nlev_pad;                   // lds_max_len_pad
-  lds_i32* ctl = ylf + P.lds_max_len_pad;                     // 4 ints
+  lds_f64* yew = hball + (size_t)nwaves * 64;                 // lds_max_nch*64 weights
+  lds_u32* ysc = (lds_u32*)(yew + (size_t)P.lds_max_nch * 64);  // lds_max_nch*64 records
+  lds_u32* yed2 = ysc + (size_t)P.lds_max_nch * 64;           // lds_max_edges (mult. of 4)
+  lds_i32* ylf = (lds_i32*)(yed2 + P.lds_max_edges);          // lds_max_len_pad
+  lds_i32* ycs = ylf + P.lds_max_len_pad;                     // lds_max_len_pad
+  lds_i32* ctl = ycs + P.lds_max_len_pad;                     // 4 ints
 
   for (int k = threadIdx.x; k < 256; k += blockDim.x) co[k] = P.co_subst[k];
   for (int k = threadIdx.x; k < P.n_gpow; k += blockDim.x) gp[k] = P.gpow[k];
@@ -585,35 +574,30 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     const int y = item.x;
     YView Y;
     Y.nl = s.ex_nl[y];
-    Y.nlev = s.ex_nlev[y];
+    Y.nch = s.ex_nch[y];
     Y.nseqs = s.ex_nseqs[y];
     const int nb = s.ex_node_base[y], eb = s.ex_edge_base[y], bb = s.ex_bpf_base[y];
+    Y.lmax = Y.nl ? (int)(s.yn_b[nb + Y.nl - 1] & 0xffff) : 0;
     {
       const int ne = s.ex_edge_base[y + 1] - eb;
-      const int lb = s.ex_ylve_base[y];
-      // node records in slot order, padded to 64*MAXK+1 (padded q: no
-      // edges, first edge = the edge count, out of band)
-      for (int k = threadIdx.x; k <= 64 * MAXK; k += blockDim.x) {
-        const bool v = k < Y.nl;
-        ynr[k].a = v ? s.yn_a[nb + k] : (uint32_t)ne;
-        ynr[k].c = v ? s.yn_c[nb + k] : 0u;
-        ynr[k].w = v ? s.yn_w[nb + k] : 0.0f;
-        ynr[k].p0 = v ? s.yn_p0[nb + k] : 0.0f;
+      // sweep schedule + two dummy chunks (read ahead past the end), with
+      // the edge weights; dummy records have child == parent and weight 0
+      const int sb = s.ex_ysc_base[y] * 64, nrec = Y.nch * 64;
+      const int nl1 = max(Y.nl, 1);
+      for (int k = threadIdx.x; k < nrec + 128; k += blockDim.x) {
+        const uint32_t d = (uint32_t)((k & 63) % nl1);
+        const uint32_t r = k < nrec ? s.ysc[sb + k] : (d | (d << 11));
+        const uint32_t ch = r & 0x7ff, pa = (r >> 11) & 0x7ff;
+        ysc[k] = r;
+        yew[k] = ch == pa ? 0.0 : gap2 * (double)s.yn_w[nb + pa] * gp[r >> 22];
       }
-      // edges by level + 64 zero pad records (reads past the end stay in
-      // the array), and node-major
-      for (int k = threadIdx.x; k < ne + 64; k += blockDim.x) yed[k] = k < ne ? s.ye[eb + k] : 0u;
       for (int k = threadIdx.x; k < ne; k += blockDim.x) yed2[k] = s.ye2[eb + k];
-      // first edge of each level (levels >= 1 are contiguous edge ranges)
-      for (int k = threadIdx.x; k < P.lds_max_nlev_pad; k += blockDim.x) {
-        ylve[k] = k <= Y.nlev ? s.ylve[lb + k] : ne;
-        ylcm[k] = k <= Y.nlev ? s.ylcm[lb + k] : 0x7fffffff;
-      }
+      const int cb = s.ex_ycs_base[y];
+      for (int v = threadIdx.x; v <= Y.lmax + 1; v += blockDim.x) ycs[v] = s.ycs[cb + v];
     }
-    Y.nr = ynr;
-    Y.ed = yed; Y.ed2 = yed2; Y.lve = ylve; Y.lcm = ylcm; Y.lfirst = ylf;
+    Y.nrg = s.yrec + nb;
+    Y.sc = ysc; Y.ew = yew; Y.ed2 = yed2; Y.lfirst = ylf; Y.ycs = ycs;
     Y.nb = nb; Y.bb = bb;
-    Y.lmax = Y.nl ? (int)(s.yn_b[nb + Y.nl - 1] & 0xffff) : 0;
     __syncthreads();
     // length -> first node index (nodes are sorted by length)
     for (int v = threadIdx.x; v <= Y.lmax + 1; v += blockDim.x) {
@@ -652,10 +636,9 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += (size_t)P.n_gpow_pad * 8;
   b += (size_t)nwaves * P.lds_max_nl * 8;          // one row per wave
   b += (size_t)nwaves * 64 * 8;                    // MATCH accumulators
-  b += (size_t)(P.lds_max_nl + 1) * 16;            // node records
-  b += (size_t)P.lds_max_edges * 4 * 2;            // edges by level (+ pad), node-major
-  b += (size_t)P.lds_max_nlev_pad * 8;
-  b += (size_t)P.lds_max_len_pad * 4 + 16;
+  b += (size_t)P.lds_max_nch * 64 * 12;            // sweep schedule: weights + records
+  b += (size_t)P.lds_max_edges * 4;                // node-major edges
+  b += (size_t)P.lds_max_len_pad * 4 * 2 + 16;     // length tables, control
   return b;
 }
 

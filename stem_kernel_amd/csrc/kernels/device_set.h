@@ -65,8 +65,8 @@ struct DevSet {
   const XRow* xrow = nullptr;       // one 32-B record per row (wave-uniform scalar load)
   const uint32_t* xr_node = nullptr;  // level-order node id (for nd_SL)
   const uint32_t* xr_ch = nullptr;  // per child edge: child slot:16 | gaps:16
-  // y role of the stem kernel: non-leaf nodes sorted by edge count (slot
-  // order), edges grouped by parent level, packed child:11|parent:11|gaps:10
+  // y role of the stem kernel: non-leaf nodes sorted by length (sorted
+  // ids), edges packed child:11|parent:11|gaps:10 in sorted ids
   const uint32_t* yn_a = nullptr;   // first edge in ye2:16 | n_edges:8 | n_bpf:8
   const uint32_t* yn_b = nullptr;   // len:16 | bpf_beg:16
   const float* yn_w = nullptr;
@@ -74,13 +74,20 @@ struct DevSet {
   const double* yn_P = nullptr;
   const uint32_t* yn_c = nullptr;   // loop leaf-edge gaps:16 | bc0:4 | single-entry flag @24
   const float* yn_p0 = nullptr;     // p of the first bp-freq entry
-  const uint32_t* ye = nullptr;     // edges (local ids) by parent level, ex_edge_base[e] per example
-  const uint32_t* ye2 = nullptr;    // the same edges node-major (sorted ids)
-  const int32_t* ylve = nullptr;    // per level: first edge (nlev+1 entries)
-  const int32_t* ylcm = nullptr;    // per level: max child length over levels 1..l (same base)
-  const int32_t* ex_ylve_base = nullptr;
+  const uint4* yrec = nullptr;      // node record {yn_a, yn_c, w, p0} (16 B)
+  const uint32_t* ye2 = nullptr;    // edges node-major (sorted ids), ex_edge_base[e] per example
+  // IY sweep schedule: ex_nch[e] chunks of 64 records child:11 | parent:11 |
+  // gaps:10 from ysc[64 * ex_ysc_base[e]] (dummy records: child == parent);
+  // ycs[ex_ycs_base[e] + v], v <= max node length + 1: first chunk whose
+  // prefix maximum of the children's lengths reaches v
+  const uint32_t* ysc = nullptr;
+  const int32_t* ex_ysc_base = nullptr;
+  const int32_t* ex_nch = nullptr;
+  const int32_t* ycs = nullptr;
+  const int32_t* ex_ycs_base = nullptr;
   // maxima over the set
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
+  int32_t max_nch = 0;
   int64_t total_nodes = 0;
 };
 

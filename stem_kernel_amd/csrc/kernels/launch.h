@@ -19,7 +19,7 @@ struct StemLaunch {
   double gap2 = 0.0;                 // loop_gap^2
   uint32_t band = 0;                 // --length-band (0 = off)
   // LDS sizing (maxima over the y examples of this launch)
-  int32_t lds_max_nl = 0, lds_max_edges = 0, lds_max_bpf = 0, lds_max_nlev_pad = 0;
+  int32_t lds_max_nl = 0, lds_max_edges = 0, lds_max_bpf = 0, lds_max_nch = 0;
   int32_t lds_max_len_pad = 0;  // length -> first node table (max node length + 2, padded)
   // work: items {y, base, count, 0}; pair t of an item is x = xs[base+t],
   // result -> out[oidx[base+t]]

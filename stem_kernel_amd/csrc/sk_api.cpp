@@ -14,6 +14,7 @@
 #include <memory>
 #include <new>
 #include <numeric>
+#include <queue>
 #include <sstream>
 #include <thread>
 #include <atomic>
@@ -82,12 +83,14 @@ struct HostPack {
   std::vector<float4> pos_lru;
   std::vector<int32_t> ex_nslots, ex_xch_base;
   std::vector<sk::XRow> xrow;
-  std::vector<uint32_t> yn_a, yn_b, yn_c, ye, ye2;
+  std::vector<uint32_t> yn_a, yn_b, yn_c, ye2, ysc;
+  std::vector<uint4> yrec;
   std::vector<float> yn_w, yn_nbp, yn_p0;
   std::vector<double> yn_P;
-  std::vector<int32_t> ylve, ylcm, ex_ylve_base;
+  std::vector<int32_t> ycs, ex_ysc_base, ex_nch, ex_ycs_base;
   std::vector<uint32_t> xr_node, xr_ch;
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
+  int32_t max_nch = 0;
 };
 
 }  // namespace
@@ -246,38 +249,82 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       std::vector<int> pos(nl);
       for (int i = 0; i < nl; ++i) pos[srt[i]] = i;
       const int nb0 = P.ex_node_base.back();
-      const int ye_base = (int)P.ye.size();
-      P.ex_ylve_base.push_back((int32_t)P.ylve.size());
-      for (int l = 0; l < nlev; ++l) {
-        P.ylve.push_back((int32_t)P.ye.size() - ye_base);
-        for (int k = lv[l]; k < lv[l + 1]; ++k) {  // level-order ids of level l
+      // IY sweep schedule.  The sweep is a stream of chunks of 64 edges: a
+      // chunk's R[child] reads are issued after the previous chunk's
+      // atomics, so an edge may go into any chunk after the one holding the
+      // last edge of its child (every node's value is final by then).  List
+      // scheduling, priority = height of the parent (longest path up to a
+      // root; the critical chain first), then the child's length; chunks
+      // are padded with dummy records (child == parent: weight 0).
+      {
+        std::vector<uint32_t> er;       // records child:11 | parent:11 | gaps:10
+        std::vector<int> epar, ech;
+        std::vector<std::vector<int>> by_child(nl), parents(nl);
+        for (int k = 0; k < nl; ++k) {
           const uint32_t a = P.nd_a[nb0 + k];
           const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
           for (uint32_t t = 0; t < ne; ++t) {
             const uint2 rec = P.ed[ebase + el + t];  // {child | gaps<<16, parent}
-            P.ye.push_back((uint32_t)pos[rec.x & 0xffff] | ((uint32_t)pos[k] << 11) |
-                           ((rec.x >> 16) << 22));
+            const int c = pos[rec.x & 0xffff], q = pos[k];
+            by_child[c].push_back((int)er.size());
+            parents[c].push_back(q);
+            epar.push_back(q);
+            ech.push_back(c);
+            er.push_back((uint32_t)c | ((uint32_t)q << 11) | ((rec.x >> 16) << 22));
           }
         }
-      }
-      P.ylve.push_back((int32_t)P.ye.size() - ye_base);
-      // prefix maximum over levels 1..l of the children's lengths (level 0
-      // has no edges): lets a row skip sweep levels that only carry zeros
-      {
-        int32_t run = -1;
-        P.ylcm.push_back(-1);  // level 0
-        for (int l = 1; l < nlev; ++l) {
-          for (int k = lv[l]; k < lv[l + 1]; ++k) {
-            const uint32_t a = P.nd_a[nb0 + k];
-            const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
-            for (uint32_t t = 0; t < ne; ++t) {
-              const uint32_t c = P.ed[ebase + el + t].x & 0xffff;
-              run = std::max<int32_t>(run, (int32_t)(P.nd_b[nb0 + c] & 0xffff));
-            }
+        const int ne_all = (int)er.size();
+        // sorted ids: a parent is strictly longer, so it has a larger id
+        std::vector<int> h(nl, 0), rem(nl, 0);
+        for (int i = nl - 1; i >= 0; --i)
+          for (int q : parents[i]) h[i] = std::max(h[i], h[q] + 1);
+        for (int f = 0; f < ne_all; ++f) rem[epar[f]]++;
+        typedef std::pair<std::pair<int, int>, int> Key;  // {{-height, child len}, edge}
+        std::priority_queue<Key, std::vector<Key>, std::greater<Key>> ready;
+        auto push_edges_of = [&](int c) {
+          for (int f : by_child[c])
+            ready.push({{-h[epar[f]], (int)(P.nd_b[nb0 + srt[c]] & 0xffff)}, f});
+        };
+        for (int c = 0; c < nl; ++c)
+          if (rem[c] == 0) push_edges_of(c);
+        P.ex_ysc_base.push_back((int32_t)(P.ysc.size() / 64));
+        std::vector<int32_t> cm;  // prefix maximum of the children's lengths
+        int32_t run = -1, placed = 0;
+        std::vector<int> take, done;
+        while (!ready.empty()) {
+          take.clear();
+          done.clear();
+          while (!ready.empty() && (int)take.size() < 64) {
+            take.push_back(ready.top().second);
+            ready.pop();
           }
-          P.ylcm.push_back(run);
+          for (int f : take) {
+            P.ysc.push_back(er[f]);
+            run = std::max<int32_t>(run, (int32_t)(P.nd_b[nb0 + srt[ech[f]]] & 0xffff));
+            if (--rem[epar[f]] == 0) done.push_back(epar[f]);
+          }
+          for (int j = (int)take.size(); j < 64; ++j) {
+            const uint32_t d = (uint32_t)(j % std::max(nl, 1));
+            P.ysc.push_back(d | (d << 11));
+          }
+          placed += (int)take.size();
+          cm.push_back(run);
+          for (int q : done) push_edges_of(q);  // ready from the next chunk on
         }
-        P.ylcm.push_back(run);  // entry nlev (unused)
+        if (placed != ne_all) {
+          err = "IY sweep schedule: DAG has a cycle";
+          return SK_ERR_INVALID;
+        }
+        const int nch = (int)cm.size();
+        // first chunk whose prefix maximum reaches v, v = 0 .. lmax+1
+        const int lmax = nl ? (int)(P.nd_b[nb0 + srt[nl - 1]] & 0xffff) : 0;
+        P.ex_ycs_base.push_back((int32_t)P.ycs.size());
+        for (int v = 0, c = 0; v <= lmax + 1; ++v) {
+          while (c < nch && cm[c] < v) ++c;
+          P.ycs.push_back(c);
+        }
+        P.ex_nch.push_back(nch);
+        P.max_nch = std::max(P.max_nch, nch);
       }
       // node-major copy of the edges in sorted order (the MATCH sums of a
       // run of consecutive nodes read one contiguous edge range); a node's
@@ -300,6 +347,14 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         const uint32_t bc0 = nbf ? P.bpf_code[bbase + bl] & 0xf : 0u;
         P.yn_c.push_back((P.nd_c[nb0 + k] & 0xffff) | (bc0 << 16) | ((one ? 1u : 0u) << 24));
         P.yn_p0.push_back(nbf ? P.bpf_p[bbase + bl] : 0.0f);
+        {
+          uint4 r;
+          r.x = P.yn_a.back();
+          r.y = P.yn_c.back();
+          std::memcpy(&r.z, &P.nd_w[nb0 + k], 4);
+          std::memcpy(&r.w, &P.yn_p0.back(), 4);
+          P.yrec.push_back(r);
+        }
         P.yn_b.push_back(P.nd_b[nb0 + k]);
         P.yn_w.push_back(P.nd_w[nb0 + k]);
         P.yn_nbp.push_back(P.nd_nbp[nb0 + k]);
@@ -773,7 +828,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   // launch per class, each sized (LDS, waves) for its own largest y
   struct StemClass {
     int maxk = 0;
-    int max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0;
+    int max_nl = 0, max_edges = 0, max_bpf = 0, max_nch = 0;
     int nwaves = 1, grid = 1;
     size_t item_off = 0, n_items = 0;
   };
@@ -810,16 +865,14 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
         C.max_nl = std::max(C.max_nl, PY.ex_nl[j]);
         C.max_edges = std::max(C.max_edges, PY.ex_edge_base[j + 1] - PY.ex_edge_base[j]);
         C.max_bpf = std::max(C.max_bpf, PY.ex_bpf_base[j + 1] - PY.ex_bpf_base[j]);
-        C.max_nlev = std::max(C.max_nlev, PY.ex_nlev[j]);
+        C.max_nch = std::max(C.max_nch, PY.ex_nch[j]);
       }
       if (!any) continue;
-      if (C.max_nlev > 127)
-        return fail(ctx, SK_ERR_UNSUPPORTED, "y example has more than 127 DAG levels");
       sk::StemLaunch L;
       L.lds_max_nl = 64 * maxk;
-      L.lds_max_edges = C.max_edges + 64;  // + 64 pad records (dag_stem.hip)
+      L.lds_max_edges = (C.max_edges + 3) & ~3;
       L.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
-      L.lds_max_nlev_pad = 128;
+      L.lds_max_nch = C.max_nch + 2;  // + 2 dummy chunks read past the end (dag_stem.hip)
       L.lds_max_len_pad = (max_len + 2 + 3) & ~3;
       L.n_gpow = max_len + 2;
       L.n_gpow_pad = (L.n_gpow + 1) & ~1;
@@ -962,9 +1015,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.gap2 = gap2;
       SL.band = kp->len_band;
       SL.lds_max_nl = 64 * C.maxk;
-      SL.lds_max_edges = C.max_edges + 64;  // + 64 pad records (dag_stem.hip)
+      SL.lds_max_edges = (C.max_edges + 3) & ~3;
       SL.lds_max_bpf = (C.max_bpf + 1 + 3) & ~3;
-      SL.lds_max_nlev_pad = 128;
+      SL.lds_max_nch = C.max_nch + 2;  // + 2 dummy chunks read past the end (dag_stem.hip)
       SL.lds_max_len_pad = (max_len + 2 + 3) & ~3;
       SL.items = d_items + C.item_off;
       SL.n_items = (int32_t)C.n_items;
@@ -1354,19 +1407,22 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.yn_w, &D.yn_w));
   SK_HIP(ctx, upload(B, P.yn_nbp, &D.yn_nbp));
   SK_HIP(ctx, upload(B, P.yn_P, &D.yn_P));
-  SK_HIP(ctx, upload(B, P.ye, &D.ye));
+  SK_HIP(ctx, upload(B, P.ysc, &D.ysc));
   SK_HIP(ctx, upload(B, P.ye2, &D.ye2));
   SK_HIP(ctx, upload(B, P.yn_c, &D.yn_c));
   SK_HIP(ctx, upload(B, P.yn_p0, &D.yn_p0));
-  SK_HIP(ctx, upload(B, P.ylve, &D.ylve));
-  SK_HIP(ctx, upload(B, P.ylcm, &D.ylcm));
-  SK_HIP(ctx, upload(B, P.ex_ylve_base, &D.ex_ylve_base));
+  SK_HIP(ctx, upload(B, P.ycs, &D.ycs));
+  SK_HIP(ctx, upload(B, P.yrec, &D.yrec));
+  SK_HIP(ctx, upload(B, P.ex_ysc_base, &D.ex_ysc_base));
+  SK_HIP(ctx, upload(B, P.ex_nch, &D.ex_nch));
+  SK_HIP(ctx, upload(B, P.ex_ycs_base, &D.ex_ycs_base));
   SK_HIP(ctx, upload(B, P.xr_node, &D.xr_node));
   SK_HIP(ctx, upload(B, P.xr_ch, &D.xr_ch));
   D.max_nl = P.max_nl;
   D.max_edges = P.max_edges;
   D.max_bpf = P.max_bpf;
   D.max_nlev = P.max_nlev;
+  D.max_nch = P.max_nch;
   D.max_len = P.max_len;
   D.max_slots = P.max_slots;
   D.total_nodes = (int64_t)P.nd_a.size();
