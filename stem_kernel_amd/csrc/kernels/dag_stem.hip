@@ -102,6 +102,9 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_W20
 #define SK_W20 8
 #endif
+#ifndef SK_NPF16  // rows prefetched per row in the MAXK 16 class
+#define SK_NPF16 1
+#endif
 #ifndef SK_SW  // IY sweep chunk width in 64-edge groups
 #define SK_SW 2
 #endif
@@ -393,7 +396,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      land during the sweep; this row itself, when a child of the next,
     //      is added from registers in D.
     // rows prefetched per row: two where the register budget allows
-    constexpr int NPF = (MAXK <= 12 || (MAXK == 20 && SK_W20 == 8)) ? 2 : 1;
+    constexpr int NPF = (MAXK <= 12 || (MAXK == 16 && SK_NPF16 == 2) || (MAXK == 20 && SK_W20 == 8)) ? 2 : 1;
     uint32_t nxt_done = 0;
     double egd = 0.0, egt0 = 0.0, egt1 = 0.0;
     double T0[MAXK], T1[MAXK];
@@ -506,7 +509,9 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) {
         const double o = R[lane + 64 * k] + xwg * S[k];
+#ifndef SK_XNOSTORE
         orow[64 * k] = o;
+#endif
         // the next row's partial sum: itself (distance-1) + prefetched rows
         S[k] = egd * o + egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
       }
