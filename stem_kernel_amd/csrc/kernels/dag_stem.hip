@@ -105,6 +105,9 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_NPF16  // rows prefetched per row in the MAXK 16 class
 #define SK_NPF16 1
 #endif
+#ifndef SK_TOUCH  // pull the next row's remaining child rows into L2 during the sweep
+#define SK_TOUCH 0
+#endif
 #ifndef SK_SW  // IY sweep chunk width in 64-edge groups
 #define SK_SW 2
 #endif
@@ -153,6 +156,24 @@ __device__ __forceinline__ double match_node_score(const lds_f64* co, const DevS
   return v;
 }
 
+// S[k] += eg0 * r0[64k] + eg1 * r1[64k]: every load of both rows is issued
+// before the first is consumed (one memory round trip, not one per slot).
+// Row slots are 64*MAXK doubles, so no index is clamped: the padded tail of
+// a row holds the zeros its producer wrote there.
+template <int MAXK>
+__device__ __forceinline__ void add_rows2(double (&S)[MAXK], const double* __restrict__ r0,
+                                          const double* __restrict__ r1, double eg0, double eg1) {
+  double a[MAXK], b[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    a[k] = r0[64 * k];
+    b[k] = r1[64 * k];
+  }
+  SCHED_FENCE();
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) S[k] += eg0 * a[k] + eg1 * b[k];
+}
+
 // One (x,y) pair on one wavefront.
 //
 // Rows p of G0 (x non-leaf nodes) are produced in the reference's post-order,
@@ -194,10 +215,8 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
   const XRow* __restrict__ xrows = s.xrow + xnb;
   const double* __restrict__ xsl = P.pn.xr_SL + xnb;
   const uint32_t* __restrict__ xch = s.xr_ch;
-  // slot index clamped to the last valid node: padded lanes re-read a line
-  // other lanes already fetch (no extra HBM traffic)
-  const int qlast = NLy - 1;
   double kacc = 0.0;
+  uint32_t tjunk = 0u;  // L2 touches (never meaningful; keeps the loads)
 #ifdef SK_STAMPS
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long cnt[4] = {0, 0, 0, 0};  // A-loaded rows, levels, passes, band nodes
@@ -265,14 +284,8 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
           const bool two = na > h + 1;
           const uint32_t c0 = c[h], c1 = two ? c[h + 1] : c[h];
           const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
-          const double* __restrict__ r0 = slab + (size_t)(c0 & 0xffff) * stride;
-          const double* __restrict__ r1 = slab + (size_t)(c1 & 0xffff) * stride;
-#pragma unroll
-          for (int k = 0; k < MAXK; ++k) {
-            const int qi = min(lane + 64 * k, qlast);
-            S[k] += eg0 * r0[qi] + eg1 * r1[qi];
-            if ((k % SK_CHUNK_A) == SK_CHUNK_A - 1) SCHED_FENCE();
-          }
+          add_rows2<MAXK>(S, slab + (size_t)(c0 & 0xffff) * stride + lane,
+                          slab + (size_t)(c1 & 0xffff) * stride + lane, eg0, eg1);
         }
       }
     }
@@ -288,14 +301,8 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       const bool two = t + 1 < xne;
       const uint32_t c1 = two ? xch[chp_r + t + 1] : c0;
       const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
-      const double* __restrict__ r0 = slab + (size_t)(c0 & 0xffff) * stride;
-      const double* __restrict__ r1 = slab + (size_t)(c1 & 0xffff) * stride;
-#pragma unroll
-      for (int k = 0; k < MAXK; ++k) {
-        const int qi = min(lane + 64 * k, qlast);
-        S[k] += eg0 * r0[qi] + eg1 * r1[qi];
-        if ((k % SK_CHUNK_A) == SK_CHUNK_A - 1) SCHED_FENCE();
-      }
+      add_rows2<MAXK>(S, slab + (size_t)(c0 & 0xffff) * stride + lane,
+                      slab + (size_t)(c1 & 0xffff) * stride + lane, eg0, eg1);
     }
     STAMP(1);
 
@@ -402,6 +409,11 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     double T0[MAXK], T1[MAXK];
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) T0[k] = T1[k] = 0.0;
+#if SK_TOUCH
+    uint32_t tch0[(MAXK + 15) / 16], tch1[(MAXK + 15) / 16];
+#pragma unroll
+    for (int u = 0; u < (MAXK + 15) / 16; ++u) tch0[u] = tch1[u] = 0u;
+#endif
     if (r + 1 < nlx) {
       const int nne = nx.a & 0xff;
       uint32_t pf0 = 0, pf1 = 0;
@@ -427,15 +439,36 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
           }
         }
       }
-      if (npf >= 1) {
-        const double* __restrict__ r0 = slab + (size_t)(pf0 & 0xffff) * stride;
+#if SK_TOUCH
+      // the children left for A are pulled into L2 now: one dword per
+      // 128-byte line, values folded into `tjunk` only after the sweep
+      {
+        int nt = 0;
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) T0[k] = r0[min(lane + 64 * k, qlast)];
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t c = nch[j];
+          const bool t = j < nne && !(nxt_done >> j & 1u) && nt < 2;
+          if (t) {
+            const uint32_t* rw = (const uint32_t*)(slab + (size_t)(c & 0xffff) * stride);
+#pragma unroll
+            for (int u = 0; u < (MAXK + 15) / 16; ++u) {
+              const int o = min((lane + 64 * u) * 32, stride * 2 - 1);
+              if (nt == 0) tch0[u] = rw[o]; else tch1[u] = rw[o];
+            }
+            ++nt;
+          }
+        }
+      }
+#endif
+      if (npf >= 1) {
+        const double* __restrict__ r0 = slab + (size_t)(pf0 & 0xffff) * stride + lane;
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k) T0[k] = r0[64 * k];
       }
       if (NPF >= 2 && npf >= 2) {
-        const double* __restrict__ r1 = slab + (size_t)(pf1 & 0xffff) * stride;
+        const double* __restrict__ r1 = slab + (size_t)(pf1 & 0xffff) * stride + lane;
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) T1[k] = r1[min(lane + 64 * k, qlast)];
+        for (int k = 0; k < MAXK; ++k) T1[k] = r1[64 * k];
       }
     }
 
@@ -517,6 +550,10 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       }
     }
     done = nxt_done;
+#if SK_TOUCH
+#pragma unroll
+    for (int u = 0; u < (MAXK + 15) / 16; ++u) tjunk ^= tch0[u] ^ tch1[u];
+#endif
     wave_sync();
     STAMP(5);
   }
@@ -530,6 +567,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #endif
   // wave reduction of the K partial sums (fixed order -> deterministic)
   for (int off = 32; off > 0; off >>= 1) kacc += __shfl_xor(kacc, off, 64);
+  if (x < 0 && tjunk == 1u) kacc += 1.0;  // x >= 0: never taken
   return kacc;
 }
 
