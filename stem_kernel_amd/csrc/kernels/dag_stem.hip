@@ -108,6 +108,12 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_TOUCH  // pull the next row's remaining child rows into L2 during the sweep
 #define SK_TOUCH 0
 #endif
+#ifndef SK_PW  // MATCH pass width in 64-node groups
+#define SK_PW 3
+#endif
+#ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
+#define SK_MU 3
+#endif
 #ifndef SK_SW  // IY sweep chunk width in 64-edge groups
 #define SK_SW 2
 #endif
@@ -260,6 +266,31 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // single bp-frequency entry of x (the common single-sequence case)
     const bool x_one = xnbf == 1 && x_nbp == 0.0;
     const uint32_t xcode = (xc >> 16) * 16u;
+    // MATCH node range [qa, qb): y nodes are numbered by length, so the
+    // length band [xlen-band, xlen+band] is one index range; its first
+    // pass's node records are requested now, ahead of the child rows
+    int qa = 0, qb = NLy;
+    if (band > 0) {
+      qa = Y.lfirst[min(max(xlen - band, 0), Y.lmax + 1)];
+      qb = Y.lfirst[min(max(xlen + band + 1, 0), Y.lmax + 1)];
+    }
+    qa = __builtin_amdgcn_readfirstlane(qa);
+    qb = __builtin_amdgcn_readfirstlane(qb);
+    uint4 nd_first[SK_PW];
+    double Pq_first[SK_PW];
+#pragma unroll
+    for (int j = 0; j < SK_PW; ++j) {
+      nd_first[j] = make_uint4(0u, 0u, 0u, 0u);
+      Pq_first[j] = 0.0;
+    }
+    if (qa < qb) {
+#pragma unroll
+      for (int j = 0; j < SK_PW; ++j) {
+        const int qf = min(max(qb - 64 * SK_PW, qa) + 64 * j + lane, qb - 1);
+        nd_first[j] = Y.nrg[qf];
+        Pq_first[j] = yPg[qf];
+      }
+    }
     STAMP(0);
 
     // ---- A: S = sum_c g^gaps G0[c][*]  (coalesced HBM row streams).
@@ -321,82 +352,135 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      (LDS ops of a wave complete in issue order.)
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = S[k];
-    int qa = 0, qb = NLy;
-    if (band > 0) {
-      qa = Y.lfirst[min(max(xlen - band, 0), Y.lmax + 1)];
-      qb = Y.lfirst[min(max(xlen + band + 1, 0), Y.lmax + 1)];
-    }
-    qa = __builtin_amdgcn_readfirstlane(qa);
-    qb = __builtin_amdgcn_readfirstlane(qb);
     double rowk = 0.0;
+    STAMP(2);
+#ifdef SK_STAMPS
+    cnt[3] += qb > qa ? qb - qa : 0;
+#endif
     if (qa < qb) {
       // node records and path counts come from HBM (L2-resident per y),
-      // each pass's prefetched during the pass before
-      int top = qb - 1, q0 = max(top - 63, qa);
-      uint4 nd_n = Y.nrg[min(q0 + lane, top)];
-      double Pq_n = yPg[min(q0 + lane, top)];
+      // the first pass's issued before A, each later pass's during the
+      // pass before.  A pass covers NW = 64*SK_PW nodes [q0, top], lane l
+      // scoring nodes q0 + 64j + l.
+      constexpr int NW = 64 * SK_PW;
+      int top = qb - 1, q0 = max(top - NW + 1, qa);
+      uint4 nd_n[SK_PW];
+      double Pq_n[SK_PW];
+#pragma unroll
+      for (int j = 0; j < SK_PW; ++j) {
+        nd_n[j] = nd_first[j];
+        Pq_n[j] = Pq_first[j];
+      }
       for (;;) {
-        const uint4 nd = nd_n;
-        const double Pq = Pq_n;
-        const int ntop = top - 64, nq0 = max(ntop - 63, qa);
+        uint4 nd[SK_PW];
+        double Pq[SK_PW];
+#pragma unroll
+        for (int j = 0; j < SK_PW; ++j) {
+          nd[j] = nd_n[j];
+          Pq[j] = Pq_n[j];
+        }
+        const int ntop = top - NW, nq0 = max(ntop - NW + 1, qa);
         if (ntop >= qa) {
-          nd_n = Y.nrg[min(nq0 + lane, ntop)];
-          Pq_n = yPg[min(nq0 + lane, ntop)];
-        }
-        const int q = q0 + lane;
-        const bool on = q <= top;
-        const uint32_t nda = nd.x, ndc = nd.y;
-        double Hq;
-        if (!xloop) {
-          // edge range of nodes [q0, top]: E(q0) .. E(top) + n_edges(top)
-          const int ea = __builtin_amdgcn_readfirstlane(nda & 0xffff);
-          const uint32_t at = __builtin_amdgcn_readlane(nda, top - q0);
-          const int eb = (int)((at & 0xffff) + ((at >> 16) & 0xff));
-          for (int f = ea + lane; f < eb; f += 64) {
-            const uint32_t e = Y.ed2[f];
-            __hip_atomic_fetch_add(&hb[((e >> 11) & 0x7ff) - q0], gp[e >> 22] * R[e & 0x7ff],
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#pragma unroll
+          for (int j = 0; j < SK_PW; ++j) {
+            nd_n[j] = Y.nrg[min(nq0 + 64 * j + lane, ntop)];
+            Pq_n[j] = yPg[min(nq0 + 64 * j + lane, ntop)];
           }
-          Hq = hb[lane];
-          hb[lane] = 0.0;
-        } else {  // x leaf child against a y stem: G0[leaf][*] = 0
-          Hq = 0.0;
         }
-        const int ne = (nda >> 16) & 0xff;
-        if (ne == 0)  // loop node: closed form over the two leaf children
-          Hq = (xloop ? xeg0 : xSL) * gp[ndc & 0xffff];
-        double vs;
-        if (x_one && (ndc >> 24) != 0u) {
-          // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:350-364)
-          vs = co[xcode + ((ndc >> 16) & 0xf)] * xpf * (double)__uint_as_float(nd.w);
-        } else {
-          // general bp-frequency lists / gap columns (score_table.cpp:343-380)
-          const int qq = on ? q : top;
-          vs = Hq != 0.0 ? match_node_score(co, s, xbb, xb0, xnbf, ys, Y, ys.yn_b[Y.nb + qq] >> 16,
-                                             nda >> 24, xwg, gap2 * (double)__uint_as_float(nd.z),
+        // node-score operands, requested ahead of the child sums
+        double co_v[SK_PW], gl_v[SK_PW];
+#pragma unroll
+        for (int j = 0; j < SK_PW; ++j) {
+          co_v[j] = co[xcode + ((nd[j].y >> 16) & 0xf)];
+          gl_v[j] = gp[nd[j].y & 0xffff];
+        }
+        double Hq[SK_PW];  // x leaf child against a y stem: G0[leaf][*] = 0
+#pragma unroll
+        for (int j = 0; j < SK_PW; ++j) Hq[j] = 0.0;
+        if (!xloop) {
+          // edge range of nodes [q0, top]: E(q0) .. E(top) + n_edges(top),
+          // 64*SK_MU edges per round: all reads of a round are issued
+          // before its first accumulate (two LDS round trips per round, not
+          // per 64 edges)
+          const int ea = __builtin_amdgcn_readfirstlane(nd[0].x & 0xffff);
+          const int jt = (top - q0) >> 6;
+          uint32_t ndt = nd[0].x;
+#pragma unroll
+          for (int j = 1; j < SK_PW; ++j) ndt = jt == j ? nd[j].x : ndt;
+          const uint32_t at = __builtin_amdgcn_readlane(ndt, (top - q0) & 63);
+          const int eb = (int)((at & 0xffff) + ((at >> 16) & 0xff));
+          for (int f0 = ea; f0 < eb; f0 += 64 * SK_MU) {
+            uint32_t e[SK_MU];
+#pragma unroll
+            for (int u = 0; u < SK_MU; ++u) e[u] = Y.ed2[min(f0 + 64 * u + lane, eb - 1)];
+            // unconditional accumulates (lanes past the range add 0 to their
+            // own slot), so no read is sunk into a branch
+            double g[SK_MU], rv[SK_MU];
+#pragma unroll
+            for (int u = 0; u < SK_MU; ++u) {
+              g[u] = gp[e[u] >> 22];
+              rv[u] = R[e[u] & 0x7ff];
+            }
+#pragma unroll
+            for (int u = 0; u < SK_MU; ++u) {
+              const bool ok = f0 + 64 * u + lane < eb;
+              // (a product, not a select: a select lets the compiler sink
+              // this round's reads into a branch)
+              const double w = g[u] * rv[u] * (ok ? 1.0 : 0.0);
+              const int h = ok ? (int)((e[u] >> 11) & 0x7ff) - q0 : lane;
+              __hip_atomic_fetch_add(&hb[h], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < SK_PW; ++j) {
+            Hq[j] = hb[64 * j + lane];
+            hb[64 * j + lane] = 0.0;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < SK_PW; ++j) {
+          const int q = q0 + 64 * j + lane;
+          const bool on = q <= top;
+          const uint32_t nda = nd[j].x, ndc = nd[j].y;
+          double H = Hq[j];
+          if (((nda >> 16) & 0xff) == 0)  // loop node: closed form over the two leaf children
+            H = (xloop ? xeg0 : xSL) * gl_v[j];
+          double vs;
+          if (x_one && (ndc >> 24) != 0u) {
+            // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:350-364)
+            vs = co_v[j] * xpf * (double)__uint_as_float(nd[j].w);
+          } else {
+            // general bp-frequency lists / gap columns (score_table.cpp:343-380)
+            const int qq = on ? q : top;
+            vs = H != 0.0 ? match_node_score(co, s, xbb, xb0, xnbf, ys, Y, ys.yn_b[Y.nb + qq] >> 16,
+                                             nda >> 24, xwg, gap2 * (double)__uint_as_float(nd[j].z),
                                              x_nbp, (double)ys.yn_nbp[Y.nb + qq], x_nseq)
-                         : 0.0;
+                          : 0.0;
+          }
+          const double M = vs * H;
+          if (on) {
+            R[q] = M;
+            rowk += M * Pq[j];
+          }
         }
-        const double M = vs * Hq;
-        if (on) {
-          R[q] = M;
-          rowk += M * Pq;
-        }
+#ifdef SK_STAMPS
+        cnt[2] += 1;
+#endif
         if (ntop < qa) break;
         top = ntop;
         q0 = nq0;
       }
     }
+    STAMP(3);
     // outside the band: M = 0
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) {
       const int q = lane + 64 * k;
       if (q < qa || q >= qb) R[q] = 0.0;
     }
-    STAMP(2);
     kacc += xP * rowk;
     wave_sync();
-    STAMP(3);
+    STAMP(4);
 
     // ---- next row's children: the ones this row cannot produce are loaded
     //      now (two at most, into registers the MATCH sums have freed) and
@@ -528,7 +612,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       }
       wave_sync();
     }
-    STAMP(4);
+    STAMP(5);
 
     // ---- D: G0 row p = G1 + v_s*S, to p's slot (roots are never read).
     // Every later read of element q of this row is by the same lane (q =
@@ -555,14 +639,14 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     for (int u = 0; u < (MAXK + 15) / 16; ++u) tjunk ^= tch0[u] ^ tch1[u];
 #endif
     wave_sync();
-    STAMP(5);
+    STAMP(6);
   }
 #ifdef SK_STAMPS
   if (lane == 0 && P.stamps) {
-    for (int i = 0; i < 6; ++i) atomicAdd(&P.stamps[i], tacc[i]);
-    atomicAdd(&P.stamps[6], (unsigned long long)nlx);
-    atomicAdd(&P.stamps[7], 1ull);
-    for (int i = 0; i < 4; ++i) atomicAdd(&P.stamps[8 + i], cnt[i]);
+    for (int i = 0; i < 8; ++i) atomicAdd(&P.stamps[i], tacc[i]);
+    atomicAdd(&P.stamps[8], (unsigned long long)nlx);
+    atomicAdd(&P.stamps[9], 1ull);
+    for (int i = 0; i < 4; ++i) atomicAdd(&P.stamps[10 + i], cnt[i]);
   }
 #endif
   // wave reduction of the K partial sums (fixed order -> deterministic)
@@ -588,8 +672,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   lds_f64* co = (lds_f64*)(smem);                             // 256
   lds_f64* gp = co + 256;                                     // n_gpow_pad
   lds_f64* Rall = gp + P.n_gpow_pad;                          // nwaves*maxnl
-  lds_f64* hball = Rall + (size_t)nwaves * maxnl;             // nwaves*64 (MATCH sums)
-  lds_f64* yew = hball + (size_t)nwaves * 64;                 // lds_max_nch*64 weights
+  lds_f64* hball = Rall + (size_t)nwaves * maxnl;             // nwaves*64*SK_PW (MATCH sums)
+  lds_f64* yew = hball + (size_t)nwaves * 64 * SK_PW;         // lds_max_nch*64 weights
   lds_u32* ysc = (lds_u32*)(yew + (size_t)P.lds_max_nch * 64);  // lds_max_nch*64 records
   lds_u32* yed2 = ysc + (size_t)P.lds_max_nch * 64;           // lds_max_edges (mult. of 4)
   lds_i32* ylf = (lds_i32*)(yed2 + P.lds_max_edges);          // lds_max_len_pad
@@ -600,8 +684,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   for (int k = threadIdx.x; k < P.n_gpow; k += blockDim.x) gp[k] = P.gpow[k];
 
   lds_f64* R = Rall + (size_t)wave * maxnl;
-  lds_f64* hb = hball + (size_t)wave * 64;
-  hb[lane] = 0.0;  // kept zero between MATCH passes
+  lds_f64* hb = hball + (size_t)wave * 64 * SK_PW;
+  for (int j = 0; j < SK_PW; ++j) hb[64 * j + lane] = 0.0;  // kept zero between MATCH passes
   double* slab = P.scratch + (size_t)(blockIdx.x * nwaves + wave) * P.slab_doubles;
   const double gap2 = P.gap2;
 
@@ -678,7 +762,7 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += 256 * 8;
   b += (size_t)P.n_gpow_pad * 8;
   b += (size_t)nwaves * P.lds_max_nl * 8;          // one row per wave
-  b += (size_t)nwaves * 64 * 8;                    // MATCH accumulators
+  b += (size_t)nwaves * 64 * SK_PW * 8;            // MATCH accumulators
   b += (size_t)P.lds_max_nch * 64 * 12;            // sweep schedule: weights + records
   b += (size_t)P.lds_max_edges * 4;                // node-major edges
   b += (size_t)P.lds_max_len_pad * 4 * 2 + 16;     // length tables, control

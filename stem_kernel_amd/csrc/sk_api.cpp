@@ -1039,13 +1039,13 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SK_HIP(ctx, hipMemcpyAsync(h, d_stamps, sizeof(h), hipMemcpyDeviceToHost, S));
       SK_HIP(ctx, hipStreamSynchronize(S));
       (void)hipFree(d_stamps);
-      const double rows = (double)h[6];
+      const double rows = (double)h[8];
       std::fprintf(stderr, "[stamps] classes=%zu pairs=%llu rows=%.0f cycles/row:", classes.size(),
-                   h[7], rows);
-      const char* nm[6] = {"hdr", "load", "gather", "match", "sweep", "store"};
-      for (int i = 0; i < 6; ++i) std::fprintf(stderr, " %s=%.0f", nm[i], h[i] / rows);
-      std::fprintf(stderr, "\n[stamps] per row: A-loaded rows=%.3f swept levels=%.2f match passes=%.2f band nodes=%.1f\n",
-                   h[8] / rows, h[9] / rows, h[10] / rows, h[11] / rows);
+                   h[9], rows);
+      const char* nm[7] = {"hdr", "A", "Rfill", "passes", "zero", "sweep", "store"};
+      for (int i = 0; i < 7; ++i) std::fprintf(stderr, " %s=%.0f", nm[i], h[i] / rows);
+      std::fprintf(stderr, "\n[stamps] per row: A-loaded rows=%.3f swept chunks=%.2f match passes=%.2f band nodes=%.1f\n",
+                   h[10] / rows, h[11] / rows, h[12] / rows, h[13] / rows);
       for (const StemClass& C : classes)
         std::fprintf(stderr, "[stamps] class maxk=%d max_nl=%d waves/wg=%d grid=%d items=%zu\n",
                      C.maxk, C.max_nl, C.nwaves, C.grid, C.n_items);
