@@ -162,18 +162,34 @@ __device__ __forceinline__ double match_node_score(const lds_f64* co, const DevS
   return v;
 }
 
-// S[k] += eg0 * r0[64k] + eg1 * r1[64k]: every load of both rows is issued
-// before the first is consumed (one memory round trip, not one per slot).
-// Row slots are 64*MAXK doubles, so no index is clamped: the padded tail of
-// a row holds the zeros its producer wrote there.
+// A G0 row slot as a buffer resource whose range is the y example's NLy
+// valid columns: loads of the padded tail return 0 without touching memory
+// (the tail is never needed).  Built from wave-uniform values only.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* base, int nly) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, nly * 8,
+                                           0x00020000);
+}
+
+// element lane + 64k of a row
+__device__ __forceinline__ double row_ld(__amdgpu_buffer_rsrc_t r, int lane, int k) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8, k * 512, 0));
+}
+
+// S[k] += eg0 * r0[lane + 64k] + eg1 * r1[lane + 64k]: every load of both rows
+// is issued before the first is consumed (one memory round trip, not one per
+// slot).
 template <int MAXK>
-__device__ __forceinline__ void add_rows2(double (&S)[MAXK], const double* __restrict__ r0,
-                                          const double* __restrict__ r1, double eg0, double eg1) {
+__device__ __forceinline__ void add_rows2(double (&S)[MAXK], __amdgpu_buffer_rsrc_t r0,
+                                          __amdgpu_buffer_rsrc_t r1, double eg0, double eg1,
+                                          int lane) {
   double a[MAXK], b[MAXK];
 #pragma unroll
   for (int k = 0; k < MAXK; ++k) {
-    a[k] = r0[64 * k];
-    b[k] = r1[64 * k];
+    a[k] = row_ld(r0, lane, k);
+    b[k] = row_ld(r1, lane, k);
   }
   SCHED_FENCE();
 #pragma unroll
@@ -315,8 +331,8 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
           const bool two = na > h + 1;
           const uint32_t c0 = c[h], c1 = two ? c[h + 1] : c[h];
           const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
-          add_rows2<MAXK>(S, slab + (size_t)(c0 & 0xffff) * stride + lane,
-                          slab + (size_t)(c1 & 0xffff) * stride + lane, eg0, eg1);
+          add_rows2<MAXK>(S, row_rsrc(slab + (size_t)(c0 & 0xffff) * stride, NLy),
+                          row_rsrc(slab + (size_t)(c1 & 0xffff) * stride, NLy), eg0, eg1, lane);
         }
       }
     }
@@ -332,8 +348,8 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       const bool two = t + 1 < xne;
       const uint32_t c1 = two ? xch[chp_r + t + 1] : c0;
       const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
-      add_rows2<MAXK>(S, slab + (size_t)(c0 & 0xffff) * stride + lane,
-                      slab + (size_t)(c1 & 0xffff) * stride + lane, eg0, eg1);
+      add_rows2<MAXK>(S, row_rsrc(slab + (size_t)(c0 & 0xffff) * stride, NLy),
+                      row_rsrc(slab + (size_t)(c1 & 0xffff) * stride, NLy), eg0, eg1, lane);
     }
     STAMP(1);
 
@@ -545,14 +561,14 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       }
 #endif
       if (npf >= 1) {
-        const double* __restrict__ r0 = slab + (size_t)(pf0 & 0xffff) * stride + lane;
+        const __amdgpu_buffer_rsrc_t r0 = row_rsrc(slab + (size_t)(pf0 & 0xffff) * stride, NLy);
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) T0[k] = r0[64 * k];
+        for (int k = 0; k < MAXK; ++k) T0[k] = row_ld(r0, lane, k);
       }
       if (NPF >= 2 && npf >= 2) {
-        const double* __restrict__ r1 = slab + (size_t)(pf1 & 0xffff) * stride + lane;
+        const __amdgpu_buffer_rsrc_t r1 = row_rsrc(slab + (size_t)(pf1 & 0xffff) * stride, NLy);
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) T1[k] = r1[64 * k];
+        for (int k = 0; k < MAXK; ++k) T1[k] = row_ld(r1, lane, k);
       }
     }
 
