@@ -138,6 +138,87 @@ int fail(sk_context* ctx, int code, const std::string& msg) {
   return code;
 }
 
+
+// Lane placement of one IY sweep chunk (records child:11 | parent:11 |
+// gaps:10, sorted ids).  The kernel reads R[child] (ds_read_b64: banks by
+// element mod 32 within each 32-lane half) and adds into R[parent]
+// (ds_add_f64: taken as 16-lane groups, element mod 16), so the edges are
+// dealt to the four 16-lane groups greedily to spread both, the parents with
+// most edges in the chunk first; dummies (child == parent, weight 0) take
+// the emptiest slots.
+static void assign_sweep_lanes(const std::vector<int>& take, const std::vector<uint32_t>& er, int nl,
+                               uint32_t lanes[64]) {
+  int n = (int)take.size();
+  std::vector<int> cntp(n, 0);
+  {
+    std::vector<std::pair<uint32_t, int>> pp(n);
+    for (int i = 0; i < n; ++i) pp[i] = {(er[take[i]] >> 11) & 0x7ff, i};
+    std::sort(pp.begin(), pp.end());
+    for (int a = 0; a < n;) {
+      int b = a;
+      while (b < n && pp[b].first == pp[a].first) ++b;
+      for (int t = a; t < b; ++t) cntp[pp[t].second] = b - a;
+      a = b;
+    }
+  }
+  std::vector<int> ord(n);
+  std::iota(ord.begin(), ord.end(), 0);
+  std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cntp[a] > cntp[b]; });
+  int fill[4] = {0, 0, 0, 0};
+  int at[4][16];         // group -> parent slot load
+  uint32_t rd[2][32][4];  // half -> child slot -> distinct children (up to 4 kept)
+  int rdn[2][32];
+  std::memset(at, 0, sizeof(at));
+  std::memset(rdn, 0, sizeof(rdn));
+  auto child_load = [&](int h, uint32_t c) {
+    const int sl = c & 31;
+    for (int t = 0; t < std::min(rdn[h][sl], 4); ++t)
+      if (rd[h][sl][t] == c) return rdn[h][sl];
+    return rdn[h][sl] + 1;
+  };
+  auto put = [&](int g, uint32_t r) {
+    const uint32_t c = r & 0x7ff, q = (r >> 11) & 0x7ff;
+    const int h = g >> 1, sl = c & 31;
+    bool seen = false;
+    for (int t = 0; t < std::min(rdn[h][sl], 4); ++t) seen |= rd[h][sl][t] == c;
+    if (!seen) {
+      if (rdn[h][sl] < 4) rd[h][sl][rdn[h][sl]] = c;
+      ++rdn[h][sl];
+    }
+    at[g][q & 15]++;
+    lanes[16 * g + fill[g]++] = r;
+  };
+  for (int i : ord) {
+    const uint32_t r = er[take[i]];
+    const uint32_t c = r & 0x7ff, q = (r >> 11) & 0x7ff;
+    int best = -1, bc = 1 << 30;
+    for (int g = 0; g < 4; ++g) {
+      if (fill[g] == 16) continue;
+      const int cost = 4 * (child_load(g >> 1, c) + at[g][q & 15] + 1) + fill[g];
+      if (cost < bc) {
+        bc = cost;
+        best = g;
+      }
+    }
+    put(best, r);
+  }
+  const int nl1 = std::max(nl, 1);
+  for (int g = 0; g < 4; ++g) {
+    while (fill[g] < 16) {
+      int bs = 0, bc = 1 << 30;
+      for (int sl = 0; sl < 32 && sl < nl1; ++sl) {
+        const int cost = rdn[g >> 1][sl] + at[g][sl & 15];
+        if (cost < bc) {
+          bc = cost;
+          bs = sl;
+        }
+      }
+      const uint32_t d = (uint32_t)(bs % nl1);
+      put(g, d | (d << 11));
+    }
+  }
+}
+
 #define SK_HIP(ctx, expr)                                                              \
   do {                                                                                 \
     hipError_t _e = (expr);                                                            \
@@ -148,6 +229,9 @@ int fail(sk_context* ctx, int code, const std::string& msg) {
 // --------------------------------------------------------------- packing
 int pack_dataset(sk_dataset* ds, std::string& err) {
   HostPack& P = ds->pack;
+  // SK_SWEEP_LANES=0: sweep chunks in schedule order (A/B diagnostics)
+  const char* lanes_env = std::getenv("SK_SWEEP_LANES");
+  const bool sweep_lanes_greedy = !lanes_env || std::atoi(lanes_env) != 0;
   P = HostPack();
   const int n = (int)ds->ex.size();
   P.ex_node_base.push_back(0);
@@ -299,13 +383,19 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
             ready.pop();
           }
           for (int f : take) {
-            P.ysc.push_back(er[f]);
             run = std::max<int32_t>(run, (int32_t)(P.nd_b[nb0 + srt[ech[f]]] & 0xffff));
             if (--rem[epar[f]] == 0) done.push_back(epar[f]);
           }
-          for (int j = (int)take.size(); j < 64; ++j) {
-            const uint32_t d = (uint32_t)(j % std::max(nl, 1));
-            P.ysc.push_back(d | (d << 11));
+          if (sweep_lanes_greedy) {
+            uint32_t lanes[64];
+            assign_sweep_lanes(take, er, nl, lanes);
+            P.ysc.insert(P.ysc.end(), lanes, lanes + 64);
+          } else {
+            for (int f : take) P.ysc.push_back(er[f]);
+            for (int j = (int)take.size(); j < 64; ++j) {
+              const uint32_t d = (uint32_t)(j % std::max(nl, 1));
+              P.ysc.push_back(d | (d << 11));
+            }
           }
           placed += (int)take.size();
           cm.push_back(run);
