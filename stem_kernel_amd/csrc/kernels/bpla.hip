@@ -6,12 +6,14 @@
 //   local_alignment_max :117-157 (M, X, Y; result max M)
 //   LAScore :16-43, BPLAScore :45-62, fill_weight bpla_kernel/data.cpp:19-45.
 //
-// Systolic schedule (as the profile string kernel): one wavefront per pair,
-// lane l owns DP row i = 64*strip + l + 1 and computes column j = t - l + 1 at
-// step t.  Row i-1 lives one lane down and one step ahead, so the "up" cell
-// (i-1, j) is lane l-1's previous output (one DPP wave_shr), and the diagonal
-// (i-1, j-1) is what lane l received one step earlier.  The strip boundary
-// row goes through a per-wave LDS row of the four states lane 0 reads.
+// Systolic schedule: one wavefront per pair, lane l owns DP rows
+// i = 64*strip + l + 1 and computes column j of its current row at step t.
+// Row i-1 lives one lane down and one step ahead, so the "up" cell (i-1, j)
+// is lane l-1's previous output (one DPP wave_shr), and the diagonal
+// (i-1, j-1) is what lane l received one step earlier.  Strips are streamed:
+// a lane starts its next row as soon as it finishes one, so the 64-step fill
+// and drain is paid once per pair, not per strip; the strip boundary row goes
+// through a per-wave LDS row of the four states lane 0 reads.
 // FP64 throughout; one exp per cell is the bound.
 #include <hip/hip_runtime.h>
 
@@ -29,30 +31,36 @@ __device__ __forceinline__ double wave_shr1(double v, double low) {
   return __hiloint2double(rhi, rlo);
 }
 
-__device__ __forceinline__ int bpla_onehot(float4 c) {
-  if (c.x == 1.0f && c.y == 0.0f && c.z == 0.0f && c.w == 0.0f) return 0;
-  if (c.x == 0.0f && c.y == 1.0f && c.z == 0.0f && c.w == 0.0f) return 1;
-  if (c.x == 0.0f && c.y == 0.0f && c.z == 1.0f && c.w == 0.0f) return 2;
-  if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f && c.w == 1.0f) return 3;
-  return -1;
+// Column sum of a profile column if every entry is a multiple of 1/256
+// (then every product, partial sum and the total weight of LAScore are exact
+// in float, whatever the order), else -1.
+__device__ __forceinline__ float dyadic_sum(float4 c) {
+  const bool ex = c.x * 256.0f == rintf(c.x * 256.0f) && c.y * 256.0f == rintf(c.y * 256.0f) &&
+                  c.z * 256.0f == rintf(c.z * 256.0f) && c.w * 256.0f == rintf(c.w * 256.0f);
+  return ex ? c.x + c.y + c.z + c.w : -1.0f;
 }
 
-// LAScore::operator() (bpla_kernel.cpp:24-43): 0 when either column is empty
-__device__ __forceinline__ double la_score(const double* __restrict__ tb, float4 xc, float4 yc) {
-  const float xa[4] = {xc.x, xc.y, xc.z, xc.w};
+// LAScore::operator() (bpla_kernel.cpp:24-43), 0 when either column is empty.
+// Branch-free numerator from the row's factored u; the float weight n is
+// xs*ys when both columns are dyadic (exact, see dyadic_sum), else every
+// product added in the reference's (k, l) order (the skipped ones are exact
+// zeros).
+__device__ __forceinline__ double la_score_f(const double (&u)[4], float4 xc, float4 yc, float xs,
+                                             float ys) {
   const float yb[4] = {yc.x, yc.y, yc.z, yc.w};
-  double v = 0.0;
-  float n = 0.0f;
+  float n;
+  if (xs >= 0.0f && ys >= 0.0f) {
+    n = xs * ys;
+  } else {
+    const float xa[4] = {xc.x, xc.y, xc.z, xc.w};
+    n = 0.0f;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (xa[k] == 0.0f) continue;
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      if (yb[l] == 0.0f) continue;
-      n = __fadd_rn(n, __fmul_rn(xa[k], yb[l]));
-      v += tb[k * 4 + l] * (double)xa[k] * (double)yb[l];
-    }
+      for (int l = 0; l < 4; ++l) n = __fadd_rn(n, __fmul_rn(xa[k], yb[l]));
   }
+  const double v = u[0] * (double)yb[0] + u[1] * (double)yb[1] + u[2] * (double)yb[2] +
+                   u[3] * (double)yb[3];
   return n == 0.0f ? 0.0 : v / (double)n;
 }
 
@@ -63,7 +71,7 @@ __global__ void __launch_bounds__(256) sk_bpla_kernel(BplaLaunch P) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
   const int maxlen = P.lds_max_len;  // even
-  // LDS: table[16] | per wave: bM,bX,bY,bX2 [maxlen+2] | yprof, ylru float4 [maxlen] | ycode [maxlen]
+  // LDS: table[16] | per wave: bM,bX,bY,bX2 [maxlen+2] | yprof, ylru float4 [maxlen]
   double* tb = reinterpret_cast<double*>(smem);
   const size_t wbytes = bpla_wave_lds_bytes(maxlen);
   unsigned char* wbase = smem + 16 * 8 + (size_t)wave * wbytes;
@@ -73,7 +81,6 @@ __global__ void __launch_bounds__(256) sk_bpla_kernel(BplaLaunch P) {
   double* bX2 = bY + (maxlen + 2);
   float4* yprof = reinterpret_cast<float4*>(bX2 + (maxlen + 2));
   float4* ylru = yprof + maxlen;
-  int* ycode = reinterpret_cast<int*>(ylru + maxlen);
   (void)nwaves;
 
   if (threadIdx.x < 16) tb[threadIdx.x] = P.table[threadIdx.x];
@@ -94,10 +101,16 @@ __global__ void __launch_bounds__(256) sk_bpla_kernel(BplaLaunch P) {
     for (int j = lane; j < Ly; j += 64) {
       const float4 c = sy.pos_prof[ypb + j];
       yprof[j] = c;
-      ylru[j] = sy.pos_lru[ypb + j];
-      ycode[j] = bpla_onehot(c);
+      float4 w = sy.pos_lru[ypb + j];
+      w.w = dyadic_sum(c);  // (the 4th weight slot is unused)
+      ylru[j] = w;
     }
-    for (int j = lane; j <= Ly; j += 64) {  // row 0 (bpla_kernel.cpp:90-96)
+    // streamed strips: a strip takes Lys = max(Ly, 64) steps, so lane 0
+    // reads boundary column j of strip s (row 64s, written by lane 63 one
+    // strip earlier) at least one step after it was written, and before
+    // lane 63 overwrites it with strip s's own row
+    const int Lys = max(Ly, 64);
+    for (int j = lane; j <= Lys; j += 64) {  // row 0 (bpla_kernel.cpp:90-96)
       bM[j] = 0.0;
       bX[j] = 0.0;
       bY[j] = 0.0;
@@ -109,84 +122,115 @@ __global__ void __launch_bounds__(256) sk_bpla_kernel(BplaLaunch P) {
 
     double result = 0.0, mmax = 0.0;
     const int nstrips = (Lx + 63) / 64;
-    for (int strip = 0; strip < nstrips; ++strip) {
-      const int i = strip * 64 + lane + 1;
-      const bool row_ok = i <= Lx;
-      float4 xc = make_float4(0.f, 0.f, 0.f, 0.f), xw = make_float4(0.f, 0.f, 0.f, 0.f);
-      int xcode = -1;
-      if (row_ok) {
-        xc = sx.pos_prof[xpb + i - 1];
-        xw = sx.pos_lru[xpb + i - 1];
-        xcode = bpla_onehot(xc);
-      }
-      // my outputs of the previous step (row i, column j-1); zero at j <= 0
-      double lM = 0.0, lX = 0.0, lY = 0.0, lX2 = 0.0, lY2 = 0.0;
-      // what I received last step: (i-1, j-1)
-      double dM = 0.0, dX = 0.0, dY = 0.0;
-      for (int t = 0; t < Ly + 64; ++t) {
-        const int j = t - lane + 1;
-        // lane 0 takes row i-1 from the boundary row (column t+1 = its j)
-        double b0M = 0.0, b0X = 0.0, b0Y = 0.0, b0X2 = 0.0;
-        if (t + 1 <= Ly) {
-          b0M = bM[t + 1];
-          b0X = bX[t + 1];
-          b0Y = bY[t + 1];
-          b0X2 = bX2[t + 1];
-        }
-        const double upM = wave_shr1(lM, b0M);
-        const double upX = wave_shr1(lX, b0X);
-        const double upY = wave_shr1(lY, b0Y);
-        const double upX2 = wave_shr1(lX2, b0X2);
-        if (j >= 1 && j <= Ly) {
-          const float4 yc = yprof[j - 1];
-          const int yk = ycode[j - 1];
-          double s = (xcode >= 0 && yk >= 0) ? tb[xcode * 4 + yk] : la_score(tb, xc, yc);
-          if (bp) {
-            // BPLAScore (bpla_kernel.cpp:55-60): float products as written
-            const float4 yw = ylru[j - 1];
-            const float pp = __fadd_rn(__fmul_rn(xw.y, yw.y), __fmul_rn(xw.x, yw.x));
-            const float uu = __fmul_rn(xw.z, yw.z);
-            s = alpha * (double)pp + (double)uu * s;
-          }
-          double nM, nX, nY, nX2 = 0.0, nY2 = 0.0;
-          if (!sw) {
-            nM = exp(beta * s) * (1.0 + dX + dY + dM);
-            nX = bg * upM + be * upX;
-            nY = bg * (lM + lX) + be * lY;
-            nX2 = upM + upX2;
-            nY2 = lM + lX2 + lY2;
-          } else {
-            double v = fmax(0.0, dM);
-            v = fmax(v, dX);
-            v = fmax(v, dY);
-            nM = v + s;
-            nX = fmax(upM + gap, upX + ext);
-            nY = fmax(fmax(lM + gap, lX + gap), lY + ext);
-          }
-          if (row_ok) {
-            lM = nM;
-            lX = nX;
-            lY = nY;
-            lX2 = nX2;
-            lY2 = nY2;
-            mmax = fmax(mmax, nM);
-            if (i == Lx && j == Ly) result = 1.0 + nX2 + nY2 + nM;
-          }
-          if (lane == 63) {
-            bM[j] = nM;
-            bX[j] = nX;
-            bY[j] = nY;
-            bX2[j] = nX2;
-          }
-        }
-        dM = upM;
-        dX = upX;
-        dY = upY;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // lane l owns rows l+1, l+65, ...: at step t it is at strip
+    // s = (t-l) / Lys, column j = (t-l) % Lys + 1 (nothing before t = l)
+    int strip = 0, j = 1 - lane;
+    int i = lane + 1;
+    bool row_ok = i <= Lx;
+    // x column of the current row, the next row's prefetched
+    float4 xc = make_float4(0.f, 0.f, 0.f, 0.f), xw = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row_ok) {
+      xc = sx.pos_prof[xpb + i - 1];
+      xw = sx.pos_lru[xpb + i - 1];
     }
+    float4 nxc = make_float4(0.f, 0.f, 0.f, 0.f), nxw = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i + 64 <= Lx) {
+      nxc = sx.pos_prof[xpb + i + 63];
+      nxw = sx.pos_lru[xpb + i + 63];
+    }
+    // LAScore numerator factored per row: v = sum_l u_l y_l with
+    // u_l = sum_k table[k][l] x_k (one-hot columns give table[k][l] exactly)
+    double u[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+      u[l] = tb[l] * (double)xc.x + tb[4 + l] * (double)xc.y + tb[8 + l] * (double)xc.z +
+             tb[12 + l] * (double)xc.w;
+    float xsum = dyadic_sum(xc);
+    // my outputs of the previous step (row i, column j-1)
+    double lM = 0.0, lX = 0.0, lY = 0.0, lX2 = 0.0, lY2 = 0.0;
+    // what I received last step: (i-1, j-1)
+    double dM = 0.0, dX = 0.0, dY = 0.0;
+    const int T = (nstrips - 1) * Lys + ((Lx - 1) & 63) + Ly;
+    for (int t = 0; t < T; ++t) {
+      // lane 0 takes row i-1 from the boundary row (a wave-uniform column)
+      const int jb = __builtin_amdgcn_readfirstlane(j);
+      const int jr = jb >= 1 && jb <= Ly ? jb : 0;
+      const double b0M = bM[jr], b0X = bX[jr], b0Y = bY[jr], b0X2 = bX2[jr];
+      const double upM = wave_shr1(lM, strip == 0 ? 0.0 : b0M);
+      const double upX = wave_shr1(lX, strip == 0 ? 0.0 : b0X);
+      const double upY = wave_shr1(lY, strip == 0 ? 0.0 : b0Y);
+      const double upX2 = wave_shr1(lX2, strip == 0 ? 0.0 : b0X2);
+      if (j >= 1 && j <= Ly) {
+        const float4 yc = yprof[j - 1];
+        const float4 yw = ylru[j - 1];
+        double s = la_score_f(u, xc, yc, xsum, yw.w);
+        if (bp) {
+          // BPLAScore (bpla_kernel.cpp:55-60): float products as written
+          const float pp = __fadd_rn(__fmul_rn(xw.y, yw.y), __fmul_rn(xw.x, yw.x));
+          const float uu = __fmul_rn(xw.z, yw.z);
+          s = alpha * (double)pp + (double)uu * s;
+        }
+        // the left cell (i, j-1); column 0 is zero.  (lM.. keep the last
+        // column of the previous row until lane l+1 has taken it.)
+        const bool c1 = j == 1;
+        const double aM = c1 ? 0.0 : lM, aX = c1 ? 0.0 : lX, aY = c1 ? 0.0 : lY;
+        const double aX2 = c1 ? 0.0 : lX2, aY2 = c1 ? 0.0 : lY2;
+        double nM, nX, nY, nX2 = 0.0, nY2 = 0.0;
+        if (!sw) {
+          nM = exp(beta * s) * (1.0 + dX + dY + dM);
+          nX = bg * upM + be * upX;
+          nY = bg * (aM + aX) + be * aY;
+          nX2 = upM + upX2;
+          nY2 = aM + aX2 + aY2;
+        } else {
+          double v = fmax(0.0, dM);
+          v = fmax(v, dX);
+          v = fmax(v, dY);
+          nM = v + s;
+          nX = fmax(upM + gap, upX + ext);
+          nY = fmax(fmax(aM + gap, aX + gap), aY + ext);
+        }
+        if (row_ok) {
+          lM = nM;
+          lX = nX;
+          lY = nY;
+          lX2 = nX2;
+          lY2 = nY2;
+          mmax = fmax(mmax, nM);
+          if (i == Lx && j == Ly) result = 1.0 + nX2 + nY2 + nM;
+        }
+        if (lane == 63) {
+          bM[j] = nM;
+          bX[j] = nX;
+          bY[j] = nY;
+          bX2[j] = nX2;
+        }
+      }
+      dM = upM;
+      dX = upX;
+      dY = upY;
+      if (++j > Lys) {  // next strip: row i + 64, column 1 (column 0 is zero)
+        j = 1;
+        ++strip;
+        i += 64;
+        row_ok = i <= Lx;
+        xc = nxc;
+        xw = nxw;
+        if (i + 64 <= Lx) {
+          nxc = sx.pos_prof[xpb + i + 63];
+          nxw = sx.pos_lru[xpb + i + 63];
+        }
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+          u[l] = tb[l] * (double)xc.x + tb[4 + l] * (double)xc.y + tb[8 + l] * (double)xc.z +
+                 tb[12 + l] * (double)xc.w;
+        xsum = dyadic_sum(xc);
+        dM = dX = dY = 0.0;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     double r;
     if (sw) {
       for (int off = 32; off > 0; off >>= 1) mmax = fmax(mmax, __shfl_xor(mmax, off, 64));

@@ -60,12 +60,12 @@ struct BplaLaunch {
   int64_t n_pairs = 0;
   double* out = nullptr;
   unsigned long long* pair_counter = nullptr;
-  int32_t lds_max_len = 0;  // even
+  int32_t lds_max_len = 0;  // even, >= 64 (streamed strips)
 };
 
 // per-wave LDS of the BPLA kernel: 4 boundary rows + y columns (16-B aligned)
 __host__ __device__ inline size_t bpla_wave_lds_bytes(int maxlen) {
-  const size_t b = (size_t)4 * (maxlen + 2) * 8 + (size_t)maxlen * 32 + (size_t)maxlen * 4;
+  const size_t b = (size_t)4 * (maxlen + 2) * 8 + (size_t)maxlen * 32;
   return (b + 15) & ~(size_t)15;
 }
 

@@ -668,7 +668,7 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   T.n_pairs = n;
   T.out = out_dev;
   T.pair_counter = d_ctr;
-  T.lds_max_len = (std::max(PY.max_len, 1) + 1) & ~1;
+  T.lds_max_len = (std::max(PY.max_len, 64) + 1) & ~1;
   const int w = 4;
   const size_t lds = sk::bpla_lds_bytes(T, w);
   if (lds > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
