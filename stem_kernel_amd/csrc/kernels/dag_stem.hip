@@ -87,6 +87,15 @@ struct YView {  // the y example (staged in LDS unless noted)
   int nb, bb;             // node / bp-freq base of the example in the y set (HBM)
 };
 
+// read-only global data through the constant address space (scalar loads)
+#if defined(__HIP_DEVICE_COMPILE__)
+template <typename T>
+using cst_ptr = const __attribute__((address_space(4))) T*;
+#else
+template <typename T>
+using cst_ptr = const T*;
+#endif
+
 __device__ __forceinline__ void wave_sync() {
   // LDS traffic of one wave is processed in issue order; this pins the
   // compiler's instruction order and waits for outstanding LDS operations.
@@ -104,9 +113,6 @@ __device__ __forceinline__ void wave_sync() {
 #endif
 #ifndef SK_NPF16  // rows prefetched per row in the MAXK 16 class
 #define SK_NPF16 1
-#endif
-#ifndef SK_TOUCH  // pull the next row's remaining child rows into L2 during the sweep
-#define SK_TOUCH 0
 #endif
 #ifndef SK_PW  // MATCH pass width in 64-node groups
 #define SK_PW 3
@@ -238,19 +244,26 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
   const double* __restrict__ xsl = P.pn.xr_SL + xnb;
   const uint32_t* __restrict__ xch = s.xr_ch;
   double kacc = 0.0;
-  uint32_t tjunk = 0u;  // L2 touches (never meaningful; keeps the loads)
 #ifdef SK_STAMPS
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long cnt[4] = {0, 0, 0, 0};  // A-loaded rows, levels, passes, band nodes
   unsigned long long tlast = __builtin_amdgcn_s_memtime();
 #endif
 
-  // x-row header and first child records, prefetched one row ahead
-  XRow nx = xrows[0];
-  double nSL = xsl[0];
+  // x-row header, its child-sum leaf term and its first four child records,
+  // prefetched one row ahead with scalar loads (constant address space: the
+  // x set is read-only here).  A vector load of these uniform values would
+  // be moved to SGPRs, i.e. waited for, right away, behind the previous
+  // row's stores; a scalar load is waited for at the next LDS wait, issued
+  // where the next one is a phase away.
+  const cst_ptr<XRow> xrows_c = (cst_ptr<XRow>)xrows;
+  const cst_ptr<double> xsl_c = (cst_ptr<double>)xsl;
+  const cst_ptr<uint32_t> xch_c = (cst_ptr<uint32_t>)xch;
+  XRow nx = xrows_c[0];
+  double nSL = xsl_c[0];
   uint32_t nch[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) nch[j] = xch[chp + j];
+  for (int j = 0; j < 4; ++j) nch[j] = xch_c[chp + j];
 
   double S[MAXK];  // this row's weighted child sum (carried over rows)
 #pragma unroll
@@ -268,12 +281,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     const int xne = xa & 0xff, xnbf = (xa >> 8) & 0xff;
     const int chp_r = chp;
     chp += xne;
-    if (r + 1 < nlx) {
-      nx = xrows[r + 1];
-      nSL = xsl[r + 1];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nch[j] = xch[chp + j];
-    }
     const int xlen = xb & 0xffff;
     const uint32_t pslot = xb >> 16;
     const int xb0 = xc & 0xffff;
@@ -309,6 +316,17 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     }
     STAMP(0);
 
+    // next row's header (see above): issued ahead of A, which has no LDS
+    // waits
+    SCHED_FENCE();
+    if (r + 1 < nlx) {
+      nx = xrows_c[r + 1];
+      nSL = xsl_c[r + 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nch[j] = xch_c[chp + j];
+    }
+    SCHED_FENCE();
+
     // ---- A: S = sum_c g^gaps G0[c][*]  (coalesced HBM row streams).
     //      S arrives partly filled: the previous row added the child rows it
     //      prefetched during its sweep and itself (a distance-1 child) from
@@ -325,7 +343,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
         c[3] = (take && na == 3) ? ch[j] : c[3];
         na += take ? 1 : 0;
       }
-#pragma unroll
       for (int h = 0; h < 4; h += 2) {
         if (na > h) {
           const bool two = na > h + 1;
@@ -509,11 +526,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     double T0[MAXK], T1[MAXK];
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) T0[k] = T1[k] = 0.0;
-#if SK_TOUCH
-    uint32_t tch0[(MAXK + 15) / 16], tch1[(MAXK + 15) / 16];
-#pragma unroll
-    for (int u = 0; u < (MAXK + 15) / 16; ++u) tch0[u] = tch1[u] = 0u;
-#endif
     if (r + 1 < nlx) {
       const int nne = nx.a & 0xff;
       uint32_t pf0 = 0, pf1 = 0;
@@ -539,27 +551,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
           }
         }
       }
-#if SK_TOUCH
-      // the children left for A are pulled into L2 now: one dword per
-      // 128-byte line, values folded into `tjunk` only after the sweep
-      {
-        int nt = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t c = nch[j];
-          const bool t = j < nne && !(nxt_done >> j & 1u) && nt < 2;
-          if (t) {
-            const uint32_t* rw = (const uint32_t*)(slab + (size_t)(c & 0xffff) * stride);
-#pragma unroll
-            for (int u = 0; u < (MAXK + 15) / 16; ++u) {
-              const int o = min((lane + 64 * u) * 32, stride * 2 - 1);
-              if (nt == 0) tch0[u] = rw[o]; else tch1[u] = rw[o];
-            }
-            ++nt;
-          }
-        }
-      }
-#endif
       if (npf >= 1) {
         const __amdgpu_buffer_rsrc_t r0 = row_rsrc(slab + (size_t)(pf0 & 0xffff) * stride, NLy);
 #pragma unroll
@@ -650,10 +641,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       }
     }
     done = nxt_done;
-#if SK_TOUCH
-#pragma unroll
-    for (int u = 0; u < (MAXK + 15) / 16; ++u) tjunk ^= tch0[u] ^ tch1[u];
-#endif
     wave_sync();
     STAMP(6);
   }
@@ -667,7 +654,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #endif
   // wave reduction of the K partial sums (fixed order -> deterministic)
   for (int off = 32; off > 0; off >>= 1) kacc += __shfl_xor(kacc, off, 64);
-  if (x < 0 && tjunk == 1u) kacc += 1.0;  // x >= 0: never taken
   return kacc;
 }
 
