@@ -383,8 +383,9 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      accumulator hb[parent - q0] (LDS atomics), so the cost follows
     //      the pass's edge count, not its largest node degree.
     //      (LDS ops of a wave complete in issue order.)
+    // (nodes from qb up have M = 0 and are never read as children here)
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = S[k];
+    for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = lane + 64 * k < qb ? S[k] : 0.0;
     double rowk = 0.0;
     STAMP(2);
 #ifdef SK_STAMPS
@@ -505,11 +506,11 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       }
     }
     STAMP(3);
-    // outside the band: M = 0
+    // below the band: M = 0 (above it R was filled with 0)
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) {
       const int q = lane + 64 * k;
-      if (q < qa || q >= qb) R[q] = 0.0;
+      if (64 * k < qa && q < qa) R[q] = 0.0;
     }
     kacc += xP * rowk;
     wave_sync();
@@ -630,9 +631,14 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     {
       const uint32_t oslot = pslot == 0xffffu ? (uint32_t)(P.slab_doubles / stride - 1) : pslot;
       double* __restrict__ orow = slab + (size_t)oslot * stride + lane;
+      // all R reads issued before the first store (one LDS round trip)
+      double g1[MAXK];
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k) g1[k] = R[lane + 64 * k];
+      SCHED_FENCE();
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) {
-        const double o = R[lane + 64 * k] + xwg * S[k];
+        const double o = g1[k] + xwg * S[k];
 #ifndef SK_XNOSTORE
         orow[64 * k] = o;
 #endif
