@@ -107,12 +107,15 @@ __device__ __forceinline__ void wave_sync() {
 // scheduling fence: keeps the compiler from hoisting every slot's memory ops
 // to the top of a phase (which would exceed the register budget)
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-// waves per workgroup of the MAXK 20 class (8: two prefetched rows; 12: one)
+// waves per workgroup of the MAXK 16 / 20 classes (8: two prefetched rows; 12: one)
 #ifndef SK_W20
 #define SK_W20 8
 #endif
+#ifndef SK_W16  // waves per workgroup of the MAXK 16 class
+#define SK_W16 8
+#endif
 #ifndef SK_NPF16  // rows prefetched per row in the MAXK 16 class
-#define SK_NPF16 1
+#define SK_NPF16 2
 #endif
 #ifndef SK_PW  // MATCH pass width in 64-node groups
 #define SK_PW 3
@@ -665,7 +668,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 
 template <int MAXK>
 struct StemWaves {
-  static constexpr int value = MAXK <= 16 ? 12 : MAXK <= 20 ? SK_W20 : 8;
+  static constexpr int value = MAXK <= 12 ? 12 : MAXK <= 16 ? SK_W16 : MAXK <= 20 ? SK_W20 : 8;
 };
 
 template <int MAXK>
