@@ -118,7 +118,7 @@ __device__ __forceinline__ void wave_sync() {
 #define SK_NPF16 2
 #endif
 #ifndef SK_PW  // MATCH pass width in 64-node groups
-#define SK_PW 3
+#define SK_PW 4
 #endif
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
 #define SK_MU 3
