@@ -759,7 +759,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // batches bounded by scratch memory
   size_t free_b = 0, total_b = 0;
   SK_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
-  const double budget = std::min(32e9, 0.5 * (double)free_b);
+  const double budget = std::min(128e9, 0.5 * (double)free_b);
   std::vector<int64_t> order(n);
   std::iota(order.begin(), order.end(), 0);
   std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
