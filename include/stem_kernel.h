@@ -87,6 +87,17 @@ typedef struct {
   int32_t bp_model;   /* 0: dataset bpp (BPMatrix/PFWrapper, the -p path),
                          1: NormalBasePair, 2: WobbleBasePair (-w) */
   uint32_t loop;      /* -l minimum loop (Normal/Wobble models), 3 */
+  /* -a alignment constraints (stem_kernel.cpp:14-81): when > 0, partial_dp
+   * restricted to the PairHMM MAP path's match positions whose posterior is
+   * >= ali_bound (PairHMM<Ribosum>, stem_kernel/phmm.cpp), widened by
+   * len_band; 0.0 = off.  Sequences must then be ACGU only (the reference
+   * asserts in char2rna, phmm.cpp:247-258). */
+  double ali_bound;   /* float option, compared as float */
+  /* LogValue zerop semantics (log_value.h:374-378).  0: as the reference
+   * builds with a C++11 <cmath> (std::isinf returns bool, `<0` is never true,
+   * posteriors are NaN and no position is anchored); 1: the intended -inf
+   * test (anchored constraints). */
+  int32_t ali_zerop_fixed;
 } sk_kernel_params;
 
 void sk_kernel_params_default(sk_kernel_params *p, int32_t kind);

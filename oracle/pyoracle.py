@@ -65,6 +65,15 @@ def oracle():
         L.orc_stem4d_banded.restype = C.c_double
         L.orc_stem4d_banded.argtypes = [C.c_char_p, _D, C.c_char_p, _D, C.c_double, C.c_double,
                                         C.c_double, C.c_float, C.c_int, C.c_uint, C.c_uint]
+        L.orc_stem4d_partial.restype = C.c_double
+        L.orc_stem4d_partial.argtypes = [C.c_char_p, _D, C.c_char_p, _D, C.c_double, C.c_double,
+                                         C.c_double, C.c_float, C.c_int, C.c_uint, C.c_uint,
+                                         C.c_float, C.c_int]
+        L.orc_phmm_posterior.restype = C.c_int
+        L.orc_phmm_posterior.argtypes = [C.c_char_p, C.c_char_p, C.c_int, _D]
+        L.orc_alignment_constraints.restype = C.c_int
+        L.orc_alignment_constraints.argtypes = [C.c_char_p, C.c_char_p, C.c_float, C.c_uint,
+                                                C.c_int, _U, _U]
         L.orc_naive_string.restype = C.c_double
         L.orc_naive_string.argtypes = [C.c_char_p, C.c_char_p, C.c_double]
         _o = L
@@ -199,9 +208,10 @@ def bpla_weights(x: OMData):
 
 
 def stem4d(x: str, bpx, y: str, bpy, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0, model=0,
-           loop=3, band=0) -> float:
-    """full_dp of stem_kernel/stem_kernel.cpp:282-351 (x, y as the loader
-    gives them: lowercase)."""
+           loop=3, band=0, ali_bound=0.0, zerop_fixed=0) -> float:
+    """StemKernel::operator() of stem_kernel/stem_kernel.h:52-55: full_dp
+    (stem_kernel.cpp:282-351), or partial_dp (:113-280) when band or
+    ali_bound is set (x, y as the loader gives them: lowercase)."""
     def arr(b):
         if b is None:
             return None
@@ -210,8 +220,29 @@ def stem4d(x: str, bpx, y: str, bpy, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0
     keep = [np.ascontiguousarray(b, dtype=np.float64) if b is not None else None for b in (bpx, bpy)]
     px = keep[0].ctypes.data_as(_D) if keep[0] is not None and keep[0].size else None
     py = keep[1].ctypes.data_as(_D) if keep[1] is not None and keep[1].size else None
+    if ali_bound > 0.0:
+        return oracle().orc_stem4d_partial(x.encode(), px, y.encode(), py, gap, stack, subst,
+                                           bp_bound, model, loop, band, ali_bound, zerop_fixed)
     if band:
         return oracle().orc_stem4d_banded(x.encode(), px, y.encode(), py, gap, stack, subst,
                                           bp_bound, model, loop, band)
     return oracle().orc_stem4d(x.encode(), px, y.encode(), py, gap, stack, subst, bp_bound,
                                model, loop)
+
+
+def phmm_posterior(x: str, y: str, zerop_fixed=0) -> np.ndarray:
+    """PairHMM posteriors fb[s, i, j] (stem_kernel/phmm.cpp:10-115)."""
+    fb = np.zeros((3, len(x) + 1, len(y) + 1))
+    if oracle().orc_phmm_posterior(x.encode(), y.encode(), zerop_fixed, fb.ctypes.data_as(_D)):
+        raise ValueError("unknown nucleotide")
+    return fb
+
+
+def alignment_constraints(x: str, y: str, ali_bound: float, band=0, zerop_fixed=0):
+    """StemKernel::alignment_constraints (stem_kernel/stem_kernel.cpp:14-81)."""
+    lo = np.zeros(len(x) + 1, np.uint32)
+    hi = np.zeros(len(x) + 1, np.uint32)
+    if oracle().orc_alignment_constraints(x.encode(), y.encode(), ali_bound, band, zerop_fixed,
+                                          lo.ctypes.data_as(_U), hi.ctypes.data_as(_U)):
+        raise ValueError("unknown nucleotide")
+    return lo, hi

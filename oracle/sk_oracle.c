@@ -1028,20 +1028,257 @@ void orc_stem4d_band(int n, int m, unsigned band, unsigned *c_low, unsigned *c_h
   }
 }
 
-/* StemKernel<double,BPMat>::partial_dp (stem_kernel/stem_kernel.cpp:113-280)
- * with band constraints only: cells outside the band stay at the planes'
- * zero fill; K0 past c_high[j-1] and K1 below c_low[i+1] use the
- * reference's boundary approximations. */
+/* ---- PairHMM alignment constraints (the 4-D kernel's -a option) ----------
+ * PairHMM<Ribosum> of stem_kernel/phmm.cpp over LogValue<double>
+ * (stem_kernel/log_value.h).  A LogValue holds log(v); products add logs
+ * (:128-189); += is the branchy log-sum of :212-224 with log1exp0 the
+ * probcons polynomial, FAST_LOG1EXP0 being defined at log_value.h:28
+ * (:312-347).  zerop(LogValue) is `std::isinf(x.log())<0` (:374-378): with a
+ * C++11 <cmath> std::isinf returns bool, so the test is always false and
+ * every += onto log(0) = -inf yields NaN (-inf + log1exp0(+inf) = -inf+inf).
+ * zerop_fixed = 0 reproduces that (the reference as g++ >= 6 builds it);
+ * zerop_fixed = 1 gives the intended -inf test. */
+enum { PH_M = 0, PH_IX = 1, PH_IY = 2 };
+
+/* ribosum_trans / ribosum_emit, phmm.cpp:262-276, stored as logs (ExpOf) */
+static const double kPhTrans[3][3] = {{0.0, -5.0, -5.0}, {-10.0, -5.0, -15.0}, {-10.0, -5.0, -15.0}};
+static const double kPhEmit[4][4] = {{2.22, -1.86, -1.46, -1.39},
+                                     {-1.86, 1.16, -2.48, -1.05},
+                                     {-1.46, -2.48, 1.03, -1.74},
+                                     {-1.39, -1.05, -1.74, 1.65}};
+
+/* log_value.h:312-347 with FAST_LOG1EXP0 */
+static double lv_log1exp0(double x) {
+  if (x > 10.0f) return x;
+  if (x >= 0.00f) {
+    if (x <= 1.00f)
+      return ((-0.009350833524763f * x + 0.130659527668286f) * x + 0.498799810682272f) * x +
+             0.693203116424741f;
+    if (x <= 2.50f)
+      return ((-0.014532321752540f * x + 0.139942324101744f) * x + 0.495635523139337f) * x +
+             0.692140569840976f;
+    if (x <= 4.50f)
+      return ((-0.004605031767994f * x + 0.063427417320019f) * x + 0.695956496475118f) * x +
+             0.514272634594009f;
+    if (x <= 7.50f)
+      return ((-0.000458661602210f * x + 0.009695946122598f) * x + 0.930734667215156f) * x +
+             0.168037164329057f;
+    return (((0.00000051726300753785 * x - 0.00002720671238876090) * x + 0.00053403733818413500) * x +
+            0.99536021775747900000) * x + 0.01507065715532010000;
+  }
+  return log(exp(x) + 1.0);
+}
+
+static int lv_zerop(double v, int fixed) { return fixed && isinf(v) && v < 0; }
+
+/* LogValue::operator+= (log_value.h:212-224) */
+static void lv_addto(double *a, double b, int fixed) {
+  if (lv_zerop(b, fixed)) return;
+  if (lv_zerop(*a, fixed)) {
+    *a = b;
+    return;
+  }
+  if (*a < b)
+    *a += lv_log1exp0(b - *a);
+  else
+    *a = b + lv_log1exp0(*a - b);
+}
+
+/* char2rna of phmm.cpp:247-258 (asserts on anything but ACGU) */
+static int ph_base(char c) {
+  switch (c) {
+    case 'a': case 'A': return 0;
+    case 'c': case 'C': return 1;
+    case 'g': case 'G': return 2;
+    case 'u': case 'U': return 3;
+  }
+  return -1;
+}
+
+#define PH(T, s, i, j) ((T)[((size_t)(s) * (n + 1) + (size_t)(i)) * (m + 1) + (size_t)(j)])
+
+/* PairHMM::forward_backward (phmm.cpp:10-50 forward, :52-93 backward,
+ * :95-115 posterior fw*bk/w); fb: 3*(n+1)*(m+1) doubles.  Returns -1 on a
+ * non-ACGU residue (the reference asserts). */
+int orc_phmm_posterior(const char *x, const char *y, int fixed, double *fb) {
+  const int n = (int)strlen(x), m = (int)strlen(y);
+  for (int i = 0; i < n; ++i)
+    if (ph_base(x[i]) < 0) return -1;
+  for (int j = 0; j < m; ++j)
+    if (ph_base(y[j]) < 0) return -1;
+  const size_t cells = (size_t)3 * (n + 1) * (m + 1);
+  double *fw = (double *)malloc(cells * sizeof(double));
+  double *bk = (double *)malloc(cells * sizeof(double));
+  const double z = log(0.0); /* LogValue(0.0) */
+  for (size_t c = 0; c < cells; ++c) fw[c] = bk[c] = z;
+  /* forward */
+  PH(fw, PH_M, 0, 0) = log(1.0);
+  for (int i = 1; i <= n; ++i) {
+    PH(fw, PH_M, i, 0) = PH(fw, PH_IY, i, 0) = z;
+    for (int s = 0; s < 3; ++s) lv_addto(&PH(fw, PH_IX, i, 0), PH(fw, s, i - 1, 0) + kPhTrans[s][PH_IX], fixed);
+  }
+  for (int j = 1; j <= m; ++j) {
+    PH(fw, PH_M, 0, j) = PH(fw, PH_IX, 0, j) = z;
+    for (int s = 0; s < 3; ++s) lv_addto(&PH(fw, PH_IY, 0, j), PH(fw, s, 0, j - 1) + kPhTrans[s][PH_IY], fixed);
+  }
+  for (int i = 1; i <= n; ++i)
+    for (int j = 1; j <= m; ++j) {
+      const double e = kPhEmit[ph_base(x[i - 1])][ph_base(y[j - 1])];
+      for (int s = 0; s < 3; ++s) {
+        lv_addto(&PH(fw, PH_M, i, j), PH(fw, s, i - 1, j - 1) + (kPhTrans[s][PH_M] + e), fixed);
+        lv_addto(&PH(fw, PH_IX, i, j), PH(fw, s, i - 1, j) + kPhTrans[s][PH_IX], fixed);
+        lv_addto(&PH(fw, PH_IY, i, j), PH(fw, s, i, j - 1) + kPhTrans[s][PH_IY], fixed);
+      }
+    }
+  /* backward */
+  PH(bk, PH_M, n, m) = log(1.0);
+  for (int i = n; i != 0; --i)
+    for (int j = m; j != 0; --j) {
+      const double e = kPhEmit[ph_base(x[i - 1])][ph_base(y[j - 1])];
+      for (int s = 0; s < 3; ++s) {
+        lv_addto(&PH(bk, s, i - 1, j - 1), PH(bk, PH_M, i, j) + (kPhTrans[s][PH_M] + e), fixed);
+        lv_addto(&PH(bk, s, i - 1, j), PH(bk, PH_IX, i, j) + kPhTrans[s][PH_IX], fixed);
+        lv_addto(&PH(bk, s, i, j - 1), PH(bk, PH_IY, i, j) + kPhTrans[s][PH_IY], fixed);
+      }
+    }
+  for (int j = m; j != 0; --j) {
+    PH(bk, PH_M, 0, j) = PH(bk, PH_IX, 0, j) = z;
+    for (int s = 0; s < 3; ++s) lv_addto(&PH(bk, s, 0, j - 1), PH(bk, PH_IY, 0, j) + kPhTrans[s][PH_IY], fixed);
+  }
+  for (int i = n; i != 0; --i) {
+    PH(bk, PH_M, i, 0) = PH(bk, PH_IY, i, 0) = z;
+    for (int s = 0; s < 3; ++s) lv_addto(&PH(bk, s, i - 1, 0), PH(bk, PH_IX, i, 0) + kPhTrans[s][PH_IX], fixed);
+  }
+  /* posterior: LogValue fw*bk/w converted to double (exp) */
+  const double w = PH(fw, PH_M, n, m);
+  for (size_t c = 0; c < cells; ++c) fb[c] = exp((fw[c] + bk[c]) - w);
+  free(fw);
+  free(bk);
+  return 0;
+}
+
+/* StemKernel::alignment_constraints (stem_kernel/stem_kernel.cpp:14-81):
+ * posteriors, MAP path by PairHMM::forward(fb,tr) + traceback
+ * (phmm.cpp:117-236), anchors = M positions of the path with posterior >=
+ * ali_bound, then the band widening.  c_low/c_high: n+1 entries. */
+int orc_alignment_constraints(const char *x, const char *y, float ali_bound, unsigned band,
+                              int fixed, unsigned *c_low, unsigned *c_high) {
+  const int n = (int)strlen(x), m = (int)strlen(y);
+  for (int i = 0; i <= n; ++i) {
+    c_low[i] = 0;
+    c_high[i] = (unsigned)m;
+  }
+  if (ali_bound > 0.0) {
+    const size_t cells = (size_t)3 * (n + 1) * (m + 1);
+    double *fb = (double *)malloc(cells * sizeof(double));
+    if (orc_phmm_posterior(x, y, fixed, fb)) {
+      free(fb);
+      return -1;
+    }
+    double *mf = (double *)calloc(cells, sizeof(double));
+    unsigned *tr = (unsigned *)malloc(cells * sizeof(unsigned));
+    for (size_t c = 0; c < cells; ++c) tr[c] = (unsigned)-1;
+    for (int s = 0; s < 3; ++s) PH(mf, s, 0, 0) = PH(fb, s, 0, 0);
+#define PH_UPD(S, I, J, V, FROM)                                             \
+  do {                                                                       \
+    const double v_ = (V);                                                   \
+    if (PH(tr, S, I, J) == (unsigned)-1 || PH(mf, S, I, J) < v_) {           \
+      PH(mf, S, I, J) = v_;                                                  \
+      PH(tr, S, I, J) = (FROM);                                              \
+    }                                                                        \
+  } while (0)
+    for (int i = 1; i <= n; ++i) {
+      PH(mf, PH_M, i, 0) = PH(mf, PH_IY, i, 0) = 0.0;
+      for (int s = 0; s < 3; ++s) PH_UPD(PH_IX, i, 0, PH(mf, s, i - 1, 0) + PH(fb, PH_IX, i, 0), s);
+    }
+    for (int j = 1; j <= m; ++j) {
+      PH(mf, PH_M, 0, j) = PH(mf, PH_IX, 0, j) = 0.0;
+      for (int s = 0; s < 3; ++s) PH_UPD(PH_IY, 0, j, PH(mf, s, 0, j - 1) + PH(fb, PH_IY, 0, j), s);
+    }
+    for (int i = 1; i <= n; ++i)
+      for (int j = 1; j <= m; ++j)
+        for (int s = 0; s < 3; ++s) {
+          PH_UPD(PH_M, i, j, PH(mf, s, i - 1, j - 1) + PH(fb, PH_M, i, j), s);
+          PH_UPD(PH_IX, i, j, PH(mf, s, i - 1, j) + PH(fb, PH_IX, i, j), s);
+          PH_UPD(PH_IY, i, j, PH(mf, s, i, j - 1) + PH(fb, PH_IY, i, j), s);
+        }
+#undef PH_UPD
+    /* traceback (phmm.cpp:187-216): path from (M,n,m) back to row/column 0 */
+    int *ps = (int *)malloc(sizeof(int) * 3 * (n + m + 2));
+    int len = 0, s = PH_M, px = n, py = m;
+    ps[0] = s, ps[1] = px, ps[2] = py, len = 1;
+    while (px != 0 && py != 0) {
+      const unsigned t = PH(tr, s, px, py);
+      if (s == PH_M) --px, --py;
+      else if (s == PH_IX) --px;
+      else --py;
+      s = (int)t;
+      ps[3 * len] = s, ps[3 * len + 1] = px, ps[3 * len + 2] = py, ++len;
+    }
+    /* anchors, in path order (:40-57) */
+    unsigned low_x = 0, low_y = 0;
+    for (int k = len - 1; k >= 0; --k) {
+      const int S = ps[3 * k], X = ps[3 * k + 1], Y = ps[3 * k + 2];
+      if (S == PH_M && PH(fb, PH_M, X, Y) >= ali_bound) {
+        for (unsigned i = low_x; i != (unsigned)X; ++i) {
+          c_low[i] = low_y;
+          c_high[i] = (unsigned)Y;
+        }
+        c_low[X] = (unsigned)Y;
+        c_high[X] = (unsigned)Y;
+        low_x = (unsigned)X + 1;
+        low_y = (unsigned)Y;
+      }
+    }
+    for (unsigned i = low_x; i != (unsigned)n + 1; ++i) {
+      c_low[i] = low_y;
+      c_high[i] = (unsigned)m;
+    }
+    if (band > 0)
+      for (int i = 0; i <= n; ++i)
+        if (c_high[i] - c_low[i] < band * 2) {
+          const unsigned j = (c_high[i] + c_low[i]) / 2;
+          c_low[i] = j < band ? 0 : j - band;
+          c_high[i] = j + band > (unsigned)m ? (unsigned)m : j + band;
+        }
+    free(ps);
+    free(tr);
+    free(mf);
+    free(fb);
+  } else if (band > 0) {
+    orc_stem4d_band(n, m, band, c_low, c_high);
+  }
+  return 0;
+}
+#undef PH
+
+/* StemKernel<double,BPMat>::partial_dp (stem_kernel/stem_kernel.cpp:113-280):
+ * cells outside the constraints stay at the planes' zero fill; K0 past
+ * c_high[j-1] and K1 below c_low[i+1] use the reference's boundary
+ * approximations.  Band-only (-b) constraints. */
 double orc_stem4d_banded(const char *x, const double *bpx, const char *y, const double *bpy,
                          double gap, double stack, double subst, float bp_bound, int model,
                          unsigned loop, unsigned band) {
+  return orc_stem4d_partial(x, bpx, y, bpy, gap, stack, subst, bp_bound, model, loop, band, 0.0f, 0);
+}
+
+/* partial_dp with the constraints of alignment_constraints(ali_bound, band);
+ * NaN when a constrained pair holds a non-ACGU residue (the reference asserts). */
+double orc_stem4d_partial(const char *x, const double *bpx, const char *y, const double *bpy,
+                          double gap, double stack, double subst, float bp_bound, int model,
+                          unsigned loop, unsigned band, float ali_bound, int zerop_fixed) {
   const int n = (int)strlen(x), m = (int)strlen(y);
-  if (n == 0) return 1.0; /* K0(0,0,0,m) of the fully initialised plane (0,0) */
   const double g = gap;
   bp4 BX = {x, bpx, n, model, loop}, BY = {y, bpy, m, model, loop};
   unsigned *cl = (unsigned *)malloc(sizeof(unsigned) * (n + 1));
   unsigned *chh = (unsigned *)malloc(sizeof(unsigned) * (n + 1));
-  orc_stem4d_band(n, m, band, cl, chh);
+  /* alignment_constraints runs first (:126) */
+  const int bad = orc_alignment_constraints(x, y, ali_bound, band, zerop_fixed, cl, chh);
+  if (bad || n == 0) {
+    free(cl);
+    free(chh);
+    return bad ? NAN : 1.0; /* n == 0: K0(0,0,0,m) of the initialised plane (0,0) */
+  }
   double *gpw = (double *)malloc(sizeof(double) * (m + 1));
   gpw[0] = 1.0;
   for (int i = 1; i <= m; ++i) gpw[i] = gpw[i - 1] * g;

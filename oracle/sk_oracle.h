@@ -112,6 +112,19 @@ double orc_stem4d_banded(const char *x, const double *bpx, const char *y, const 
                          double gap, double stack, double subst, float bp_bound, int model,
                          unsigned loop, unsigned band);
 void orc_stem4d_band(int n, int m, unsigned band, unsigned *c_low, unsigned *c_high);
+/* partial_dp with the constraints of alignment_constraints(ali_bound, band)
+ * (stem_kernel.cpp:14-81, the -a option); zerop_fixed selects LogValue's
+ * zerop semantics (see sk_oracle.c).  NaN on a non-ACGU residue when
+ * ali_bound > 0 (the reference asserts). */
+double orc_stem4d_partial(const char *x, const double *bpx, const char *y, const double *bpy,
+                          double gap, double stack, double subst, float bp_bound, int model,
+                          unsigned loop, unsigned band, float ali_bound, int zerop_fixed);
+/* PairHMM posteriors fw*bk/w (phmm.cpp:10-115): fb[s][i][j], s = M, IX, IY,
+ * 3*(|x|+1)*(|y|+1) doubles.  -1 on a non-ACGU residue. */
+int orc_phmm_posterior(const char *x, const char *y, int zerop_fixed, double *fb);
+/* alignment_constraints (stem_kernel.cpp:14-81): c_low/c_high, |x|+1 each. */
+int orc_alignment_constraints(const char *x, const char *y, float ali_bound, unsigned band,
+                              int zerop_fixed, unsigned *c_low, unsigned *c_high);
 
 #ifdef __cplusplus
 }

@@ -34,7 +34,7 @@ class KernelParams(C.Structure):
         ("alpha", C.c_double), ("gap", C.c_double), ("match", C.c_double),
         ("mismatch", C.c_double), ("ext", C.c_double), ("score_table", C.c_double * 16),
         ("subst", C.c_double), ("bp_bound", C.c_double), ("bp_model", C.c_int32),
-        ("loop", C.c_uint32),
+        ("loop", C.c_uint32), ("ali_bound", C.c_double), ("ali_zerop_fixed", C.c_int32),
     ]
 
 

@@ -723,6 +723,10 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
                const int32_t* x, const int32_t* y, int64_t n, double* out_dev) {
   if (kp->bp_model < 0 || kp->bp_model > 2 || !(kp->bp_bound >= 0.0))
     return fail(ctx, SK_ERR_INVALID, "4-D stem kernel: bp_model 0..2 and bp_bound >= 0");
+  // StemKernel::operator() (stem_kernel.h:52-55): partial_dp when ali_bound
+  // > 0 or band > 0; ali_bound is a float option
+  const float ali_bound = (float)kp->ali_bound;
+  const bool ali = ali_bound > 0.0f;
   // per-example tables of the examples this call touches
   struct Tab { int64_t bp = -1, chr = -1; };
   std::vector<Tab> tx(xs_->ex.size()), ty(ys_->ex.size());
@@ -738,6 +742,11 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     if (sk::stem4d_cpl(X.len) < 0)
       return fail(ctx, SK_ERR_UNSUPPORTED, "4-D stem kernel: sequence longer than 511");
     stem4d_tables(X, kp, bp, chr);
+    if (ali)  // PairHMM's char2rna asserts on anything else (phmm.cpp:247-258)
+      for (int a = 0; a < X.len; ++a)
+        if (!std::strchr("acguACGU", (char)chr[a]))
+          return fail(ctx, SK_ERR_INVALID,
+                      "4-D stem kernel: alignment constraints need A/C/G/U sequences");
     t.bp = (int64_t)bpall.size();
     t.chr = (int64_t)chall.size();
     bpall.insert(bpall.end(), bp.begin(), bp.end());
@@ -808,10 +817,21 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       prs.push_back(p);
       ++b1;
     }
-    // partial_dp band constraints per pair (alignment_constraints with
-    // ali_bound 0, stem_kernel.cpp:66-72): x position -> [c_low, c_high]
+    // partial_dp constraints per pair: x position -> [c_low, c_high].  With
+    // -a the PairHMM kernel writes them on the device; with -b alone
+    // (alignment_constraints with ali_bound 0, stem_kernel.cpp:68-74) they
+    // are formed here.
     std::vector<int32_t> blo, bhi;
-    if (kp->len_band > 0) {
+    size_t n_band = 0;
+    int max_n1 = 1, max_m1 = 1;
+    if (ali) {
+      for (auto& p : prs) {
+        p.band_off = (int64_t)n_band;
+        n_band += (size_t)p.n + 1;
+        max_n1 = std::max(max_n1, p.n + 1);
+        max_m1 = std::max(max_m1, p.m + 1);
+      }
+    } else if (kp->len_band > 0) {
       for (auto& p : prs) {
         p.band_off = (int64_t)blo.size();
         for (int i = 0; i <= p.n; ++i) {
@@ -830,7 +850,9 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
         for (int i = 0; i + d1 <= prs[p].n; ++i) items.push_back(make_int2((int)p, i));
     }
     ioff[maxn + 1] = (int64_t)items.size();
-    rc = ensure_scratch(ctx, (size_t)bytes + 64);
+    if (!ali) n_band = blo.size();
+    const size_t phmm_bytes = ali ? sk::phmm_scratch_bytes((int64_t)prs.size(), max_n1, max_m1) : 0;
+    rc = ensure_scratch(ctx, std::max((size_t)bytes + 64, phmm_bytes));
     if (rc) return rc;
     if (Bt.cap_pairs < prs.size() || Bt.cap_items < items.size()) {
       if (Bt.pairs) (void)hipFree(Bt.pairs);
@@ -844,15 +866,20 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
                                hipMemcpyHostToDevice, S));
     SK_HIP(ctx, hipMemcpyAsync(Bt.items, items.data(), items.size() * sizeof(int2),
                                hipMemcpyHostToDevice, S));
-    if (!blo.empty()) {
-      if (Bt.cap_band < blo.size()) {
-        if (Bt.band) (void)hipFree(Bt.band);
-        Bt.cap_band = std::max<size_t>(blo.size(), 4096);
+    if (n_band) {
+      if (Bt.cap_band < n_band) {
+        if (Bt.band) {
+          SK_HIP(ctx, hipStreamSynchronize(S));
+          (void)hipFree(Bt.band);
+        }
+        Bt.cap_band = std::max<size_t>(n_band, 4096);
         SK_HIP(ctx, hipMalloc(&Bt.band, 2 * Bt.cap_band * sizeof(int32_t)));
       }
-      SK_HIP(ctx, hipMemcpyAsync(Bt.band, blo.data(), blo.size() * 4, hipMemcpyHostToDevice, S));
-      SK_HIP(ctx, hipMemcpyAsync(Bt.band + Bt.cap_band, bhi.data(), bhi.size() * 4,
-                                 hipMemcpyHostToDevice, S));
+      if (!blo.empty()) {
+        SK_HIP(ctx, hipMemcpyAsync(Bt.band, blo.data(), blo.size() * 4, hipMemcpyHostToDevice, S));
+        SK_HIP(ctx, hipMemcpyAsync(Bt.band + Bt.cap_band, bhi.data(), bhi.size() * 4,
+                                   hipMemcpyHostToDevice, S));
+      }
     }
     sk::Stem4dLaunch L;
     L.pairs = Bt.pairs;
@@ -865,9 +892,24 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     L.subst = kp->subst;
     L.bp_bound = (float)kp->bp_bound;
     L.out = out_dev;
-    L.band_lo = blo.empty() ? nullptr : Bt.band;
-    L.band_hi = blo.empty() ? nullptr : Bt.band + Bt.cap_band;
+    L.band_lo = n_band ? Bt.band : nullptr;
+    L.band_hi = n_band ? Bt.band + Bt.cap_band : nullptr;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
+    if (ali) {
+      sk::PhmmLaunch H;
+      H.pairs = Bt.pairs;
+      H.n_pairs = (int64_t)prs.size();
+      H.chars = d_ch;
+      H.scratch = reinterpret_cast<char*>(ctx->scratch);
+      H.n1 = max_n1;
+      H.m1 = max_m1;
+      H.ali_bound = ali_bound;
+      H.band = kp->len_band;
+      H.zerop_fixed = kp->ali_zerop_fixed ? 1 : 0;
+      H.band_lo = Bt.band;
+      H.band_hi = Bt.band + Bt.cap_band;
+      SK_HIP(ctx, sk::launch_phmm(H, S));
+    }
     for (int d1 = 0; d1 <= maxn; ++d1) {
       L.d1 = d1;
       L.items = Bt.items + ioff[d1];
@@ -1229,6 +1271,8 @@ void sk_kernel_params_default(sk_kernel_params* p, int32_t kind) {
   p->bp_bound = 0.0;
   p->bp_model = 0;
   p->loop = 3;
+  p->ali_bound = 0.0;
+  p->ali_zerop_fixed = 0;
   if (kind == SK_STEM4D) {
     p->gap = (double)0.8f;
     p->stack = (double)1.0f;

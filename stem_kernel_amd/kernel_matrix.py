@@ -153,12 +153,17 @@ class StemKernel4D(_Kernel):
     kind = _lib.STEM4D
 
     def __init__(self, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0, bp_model=0, loop=3, band=0,
-                 cli_float=True):
-        """band > 0 selects partial_dp with the -b band constraints
-        (stem_kernel.cpp:51-75, 113-280); 0 is full_dp."""
+                 ali_bound=0.0, ali_zerop_fixed=False, cli_float=True):
+        """band > 0 or ali_bound > 0 selects partial_dp (stem_kernel.h:52-55)
+        with the constraints of alignment_constraints (stem_kernel.cpp:14-81):
+        -b band around the diagonal, -a anchors from the PairHMM MAP path
+        (computed on the GPU).  ali_zerop_fixed picks LogValue's zerop
+        semantics (see include/stem_kernel.h); both 0 is full_dp."""
         f = (lambda v: float(np.float32(v))) if cli_float else float
         super().__init__(gap=f(gap), stack=f(stack), subst=f(subst), bp_bound=f(bp_bound),
-                         bp_model=int(bp_model), loop=int(loop), len_band=int(band))
+                         bp_model=int(bp_model), loop=int(loop), len_band=int(band),
+                         ali_bound=float(np.float32(ali_bound)),
+                         ali_zerop_fixed=int(bool(ali_zerop_fixed)))
 
 
 class SiStemStrKernel(_Kernel):

@@ -29,7 +29,8 @@ def _oracle(seqs, kern, pairs):
     for a, b in pairs:
         xa, xb = seqs[a], seqs[b]
         out.append(po.stem4d(xa.lower(), ska.fold(xa), xb.lower(), ska.fold(xb), p.gap, p.stack,
-                             p.subst, p.bp_bound, p.bp_model, p.loop, p.len_band))
+                             p.subst, p.bp_bound, p.bp_model, p.loop, p.len_band, p.ali_bound,
+                             p.ali_zerop_fixed))
     return np.array(out)
 
 
@@ -114,3 +115,119 @@ def test_stem4d_rejects_alignments(gpu_ctx):
     ds, _ = make_examples([["ACGUACGU", "ACG-ACGU"], "ACGUAC"])
     with pytest.raises(ska.StemKernelError):
         gpu_ctx.gram(ds, ska.StemKernel4D())
+
+
+# ---------------------------------------------------------------- -a option
+def _indel_variants(seed, n, L):
+    """Related sequences (substitutions, insertions, deletions) so that the
+    PairHMM MAP path leaves the diagonal and anchors are sparse."""
+    rng = np.random.default_rng(seed)
+    base = ska.random_sequences(1, L, seed)[0]
+    out = [base]
+    for _ in range(n - 1):
+        r = []
+        for c in base:
+            u = rng.random()
+            if u < 0.06:
+                continue
+            r.append("ACGU"[rng.integers(4)] if u < 0.2 else c)
+            if rng.random() < 0.06:
+                r.append("ACGU"[rng.integers(4)])
+        out.append("".join(r))
+    return out
+
+
+def test_isinf_bool_makes_zerop_false(tmp_path):
+    """LogValue's zerop is `std::isinf(x.log())<0` (stem_kernel/log_value.h:374-378).
+    Built with a C++11 <cmath> (as g++ builds the reference today) std::isinf
+    returns bool, so the test is false even for log(0): the basis of
+    ali_zerop_fixed = 0.  Compiles the expression itself (not reference code)."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ absent")
+    src = tmp_path / "z.cpp"
+    src.write_text("#include <cmath>\n#include <cstdio>\n#include <limits>\n"
+                   "int main(){double v=-std::numeric_limits<double>::infinity();"
+                   "std::printf(\"%d\", (int)(std::isinf(v)<0));}\n")
+    exe = tmp_path / "z"
+    subprocess.run([gxx, "-std=gnu++17", "-w", str(src), "-o", str(exe)], check=True)
+    assert subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout == "0"
+
+
+def test_oracle_phmm_posteriors():
+    """zerop_fixed: posteriors are a distribution over each residue's state
+    (every x residue is emitted once, in M or IX; every y residue in M or IY),
+    up to the probcons log1exp0 approximation.  As built today (0): NaN."""
+    x, y = [s.lower() for s in _indel_variants(5, 2, 45)]
+    fb = po.phmm_posterior(x, y, 1)
+    assert np.all(np.isfinite(fb)) and fb.min() >= 0.0
+    mx = fb[0, 1:, :].sum(1) + fb[1, 1:, :].sum(1)
+    my = fb[0, :, 1:].sum(0) + fb[2, :, 1:].sum(0)
+    assert np.abs(mx - 1).max() < 1e-3 and np.abs(my - 1).max() < 1e-3
+    assert np.all(np.isnan(po.phmm_posterior(x, y, 0)))
+    with pytest.raises(ValueError):
+        po.phmm_posterior("acgt", "acgu", 1)
+
+
+@pytest.mark.parametrize("band", [0, 2, 5])
+def test_oracle_alignment_constraints_shape(band):
+    """Constraints are monotone (the 4-D kernel's boundary reads rely on it),
+    inside [0, |y|], anchor rows are single points when band == 0, and the
+    NaN posteriors of zerop_fixed = 0 leave the whole range."""
+    seqs = [s.lower() for s in _indel_variants(7, 4, 50)] + ["acgu", "a"]
+    for x in seqs:
+        for y in seqs:
+            for ab in (0.2, 0.5, 0.9):
+                lo, hi = po.alignment_constraints(x, y, ab, band, 1)
+                assert np.all(lo <= hi) and hi.max() <= len(y)
+                assert np.all(np.diff(lo.astype(int)) >= 0) and np.all(np.diff(hi.astype(int)) >= 0)
+                if band == 0 and len(x) > 10 and x[:10] == y[:10]:
+                    assert (lo == hi).sum() > len(x) // 2
+                lo0, hi0 = po.alignment_constraints(x, y, ab, band, 0)
+                assert np.all(lo0 == 0) and np.all(hi0 == len(y))
+    # band alone (ali_bound 0) is the -b diagonal band
+    lo, hi = po.alignment_constraints(seqs[0], seqs[1], 0.0, 3, 1)
+    lo2, hi2 = np.zeros_like(lo), np.zeros_like(hi)
+    po.oracle().orc_stem4d_band(len(seqs[0]), len(seqs[1]), 3,
+                                lo2.ctypes.data_as(po._U), hi2.ctypes.data_as(po._U))
+    assert np.array_equal(lo, lo2) and np.array_equal(hi, hi2)
+
+
+def test_oracle_ali_as_built_equals_full_range():
+    """zerop_fixed = 0 with band 0: partial_dp over the full range."""
+    seqs = _indel_variants(3, 3, 22)
+    for a in seqs:
+        for b in seqs:
+            k0 = po.stem4d(a.lower(), ska.fold(a), b.lower(), ska.fold(b), ali_bound=0.5)
+            kw = po.stem4d(a.lower(), ska.fold(a), b.lower(), ska.fold(b), band=1000)
+            assert k0 == kw
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixed,ab,band", [(1, 0.5, 0), (1, 0.8, 0), (1, 0.3, 4), (0, 0.5, 0),
+                                           (0, 0.5, 3)])
+def test_stem4d_alignment_constraints_match_oracle(gpu_ctx, fixed, ab, band):
+    """-a: PairHMM posteriors, MAP path and anchors on the GPU, then
+    partial_dp over them, against the oracle (1e-6 relative)."""
+    seqs = _indel_variants(11, 5, 48) + _indel_variants(12, 2, 30) + ["GGGAAACCC", "A"]
+    ds, _ = make_examples(seqs)
+    kern = ska.StemKernel4D(ali_bound=ab, ali_zerop_fixed=fixed, band=band)
+    n = len(seqs)
+    iu = list(zip(*np.triu_indices(n)))
+    got = gpu_ctx.gram(ds, kern)
+    ref = _oracle(seqs, kern, iu)
+    assert rel_err(got[tuple(np.array(iu).T)], ref) < TOL
+    x = np.array([5, 0, 7, 8, 2], np.int32)
+    y = np.array([0, 5, 1, 3, 8], np.int32)
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    assert rel_err(got, _oracle(seqs, kern, list(zip(x, y)))) < TOL
+
+
+@pytest.mark.gpu
+def test_stem4d_alignment_constraints_reject_non_acgu(gpu_ctx):
+    ds, _ = make_examples(["ACGUNACGU", "ACGUACGU"])
+    with pytest.raises(ska.StemKernelError):
+        gpu_ctx.gram(ds, ska.StemKernel4D(ali_bound=0.5))
+    gpu_ctx.gram(ds, ska.StemKernel4D())  # without -a the residues are free

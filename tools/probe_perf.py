@@ -14,7 +14,9 @@ print(f"build {N} examples: {time.time()-t:.2f}s", flush=True)
 ctx = ska.Context(0)
 ctx.upload(ds)
 kern = {"stem": ska.SuStemKernel(), "str": ska.StringKernel(), "ss": ska.SuStemStrKernel(),
-        "bpla": ska.BPLAKernel(), "la": ska.BPLAKernel(noBP=True), "stem4d": ska.StemKernel4D()}[kind]
+        "bpla": ska.BPLAKernel(), "la": ska.BPLAKernel(noBP=True), "stem4d": ska.StemKernel4D(),
+        "stem4d_ali": ska.StemKernel4D(ali_bound=0.5, ali_zerop_fixed=True),
+        "stem4d_ali0": ska.StemKernel4D(ali_bound=0.5)}[kind]
 iu = np.triu_indices(N)
 x, y = iu[0].astype(np.int32), iu[1].astype(np.int32)
 if len(sys.argv) > 4:  # limit the pair count (4-D kernel)
