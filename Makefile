@@ -11,7 +11,8 @@ HIPFLAGS := $(CXXFLAGS) --offload-arch=$(ARCH) -munsafe-fp-atomics
 BUILD := $(ROOT)build
 LIB := $(ROOT)stem_kernel_amd/libstem_kernel_amd.so
 
-HOST_SRC := $(ROOT)stem_kernel_amd/csrc/host/synth.cpp $(ROOT)stem_kernel_amd/csrc/host/example_build.cpp
+HOST_SRC := $(ROOT)stem_kernel_amd/csrc/host/synth.cpp $(ROOT)stem_kernel_amd/csrc/host/example_build.cpp \
+            $(ROOT)stem_kernel_amd/csrc/host/readers.cpp
 API_SRC := $(ROOT)stem_kernel_amd/csrc/sk_api.cpp
 HIP_SRC := $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip $(ROOT)stem_kernel_amd/csrc/kernels/profile_string.hip \
            $(ROOT)stem_kernel_amd/csrc/kernels/bpla.hip $(ROOT)stem_kernel_amd/csrc/kernels/stem4d.hip \
@@ -54,7 +55,7 @@ stamps:
 	@mkdir -p $(BUILD)/stamps
 	$(HIPCC) $(HIPFLAGS) -DSK_STAMPS -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip -o $(BUILD)/stamps/dag_stem.o
 	$(HIPCC) $(CXXFLAGS) -DSK_STAMPS -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/stamps/sk_api.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o -Wl,-rpath,/opt/rocm/lib
 .PHONY: stamps
 
 # experiment build: make variant NAME=x DEFS="-DSK_CHUNK_A=32 [-DSK_STAMPS]" -> build/libsk_x.so
@@ -62,5 +63,5 @@ variant:
 	@mkdir -p $(BUILD)/var/$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip -o $(BUILD)/var/$(NAME)/dag_stem.o
 	$(HIPCC) $(CXXFLAGS) $(DEFS) -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/var/$(NAME)/sk_api.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/var/$(NAME)/sk_api.o $(BUILD)/var/$(NAME)/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/var/$(NAME)/sk_api.o $(BUILD)/var/$(NAME)/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o -Wl,-rpath,/opt/rocm/lib
 .PHONY: variant

@@ -235,6 +235,27 @@ int sk_format_libsvm(const double *matrix, int32_t rows, int32_t cols,
  * function (GC 1.5, AU 1.0, GU 0.5 in kT units, hairpin >= 3).  Stand-in for
  * Vienna pf_fold; out gets n*(n-1)/2 doubles in the packed layout above. */
 int sk_fold_synthetic(const char *seq, int32_t n, int32_t no_gu, double *out);
+
+/* ---------------------------------------------------------------- example files
+ * The readers DataLoader<MData>::get (stem_kernel_lite/data.cpp:547-586) pulls
+ * examples from, with the reference grammars' exact acceptance (Boost.Spirit
+ * classic semantics, csrc/host/readers.cpp):
+ *   SK_FMT_FASTA    load_fa   common/fa.cpp:13-55    one sequence per example
+ *   SK_FMT_CLUSTAL  load_aln  common/aln.cpp:16-107  one alignment per example
+ *   SK_FMT_MAF      load_maf  common/maf.cpp:15-49   one alignment block per example
+ * Reading stops at the first example that does not parse.  SK_ERR_INVALID on a
+ * missing file, aln's format_error or rows of unequal length ("wrong
+ * alignment", data.cpp:574-578); sk_seqfile_last_error() (thread-local) says
+ * which.  Rows are returned as written (gaps kept, case kept). */
+typedef enum { SK_FMT_FASTA = 0, SK_FMT_CLUSTAL = 1, SK_FMT_MAF = 2 } sk_file_format;
+typedef struct sk_seqfile sk_seqfile;
+int sk_seqfile_read(const char *path, int32_t format, sk_seqfile **out);
+int sk_seqfile_parse(const char *text, size_t len, int32_t format, sk_seqfile **out);
+int sk_seqfile_free(sk_seqfile *f);
+int64_t sk_seqfile_count(const sk_seqfile *f);                        /* examples */
+int32_t sk_seqfile_rows(const sk_seqfile *f, int64_t i);              /* rows of example i */
+const char *sk_seqfile_row(const sk_seqfile *f, int64_t i, int32_t r); /* NUL-terminated */
+const char *sk_seqfile_last_error(void);
 /* splitmix64 sequences over ACGU: n_seqs strings of length len written to
  * out (n_seqs*(len+1) bytes, NUL separated); *state advances. */
 int sk_random_sequences(uint64_t *state, int32_t n_seqs, int32_t len, char *out);

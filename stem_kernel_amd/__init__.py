@@ -6,7 +6,7 @@ from ._lib import StemKernelError, lib, default_params  # noqa: F401
 from .kernel_matrix import (  # noqa: F401
     BPLAKernel, Context, Dataset, KernelMatrix, LSuStemKernel, LSuStemStrKernel, NaiveStringKernel, SiStemKernel,
     SiStemStrKernel, StemKernel4D, StemStrKernel, StringKernel, SuStemKernel, SuStemStrKernel, fold,
-    format_libsvm, random_sequences,
+    format_libsvm, parse_examples, random_sequences, read_examples,
 )
 
 __version__ = "0.1.0"

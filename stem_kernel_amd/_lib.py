@@ -23,6 +23,7 @@ STATUS = {
 }
 
 # sk_kernel_kind
+FMT_FASTA, FMT_CLUSTAL, FMT_MAF = range(3)
 (SU_STEM, SI_STEM, SU_STR, SI_STR, SU_STEM_STR, SI_STEM_STR, LSU_STEM, LSU_STEM_STR, NAIVE_STR,
  BPLA, LA, BPLA_SW, LA_SW, STEM4D) = range(14)
 
@@ -83,6 +84,13 @@ SIGNATURES = {
     "sk_last_timing": (C.c_int, [_P, _F64P, _F64P, _F64P, _I32P]),
     "sk_ribosum_tables": (None, [_F32P, _F32P]),
     "sk_char2rna": (C.c_int, [C.c_int]),
+    "sk_seqfile_read": (C.c_int, [C.c_char_p, C.c_int32, C.POINTER(_P)]),
+    "sk_seqfile_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.c_int32, C.POINTER(_P)]),
+    "sk_seqfile_free": (C.c_int, [_P]),
+    "sk_seqfile_count": (C.c_int64, [_P]),
+    "sk_seqfile_rows": (C.c_int32, [_P, C.c_int64]),
+    "sk_seqfile_row": (C.c_char_p, [_P, C.c_int64, C.c_int32]),
+    "sk_seqfile_last_error": (C.c_char_p, []),
 }
 
 _lock = threading.Lock()

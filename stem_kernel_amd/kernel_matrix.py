@@ -25,7 +25,7 @@ from typing import Iterable, List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import KernelParams, StemKernelError, check, lib
+from ._lib import SK_OK, KernelParams, StemKernelError, check, lib
 
 __all__ = [
     "fold", "random_sequences", "Dataset", "Context", "KernelMatrix",
@@ -36,6 +36,42 @@ __all__ = [
 
 
 # --------------------------------------------------------------------- inputs
+_FORMATS = {"fa": _lib.FMT_FASTA, "fasta": _lib.FMT_FASTA, "aln": _lib.FMT_CLUSTAL,
+            "clustal": _lib.FMT_CLUSTAL, "maf": _lib.FMT_MAF}
+
+
+def _seqfile_rows(h) -> List[List[str]]:
+    L = lib()
+    try:
+        return [[L.sk_seqfile_row(h, i, r).decode() for r in range(L.sk_seqfile_rows(h, i))]
+                for i in range(L.sk_seqfile_count(h))]
+    finally:
+        L.sk_seqfile_free(h)
+
+
+def _seqfile_check(rc):
+    if rc != SK_OK:
+        m = lib().sk_seqfile_last_error()
+        raise StemKernelError(rc, m.decode() if m else "")
+
+
+def read_examples(path: str, fmt: str = "fa") -> List[List[str]]:
+    """Examples of a FASTA ("fa": one sequence each), CLUSTAL ("aln") or MAF
+    ("maf") file, each a list of rows as written (load_fa / load_aln /
+    load_maf, common/{fa,aln,maf}.cpp, through sk_seqfile_read)."""
+    h = C.c_void_p()
+    _seqfile_check(lib().sk_seqfile_read(path.encode(), _FORMATS[fmt], C.byref(h)))
+    return _seqfile_rows(h)
+
+
+def parse_examples(text: str, fmt: str = "fa") -> List[List[str]]:
+    """read_examples over an in-memory text (sk_seqfile_parse)."""
+    b = text.encode()
+    h = C.c_void_p()
+    _seqfile_check(lib().sk_seqfile_parse(b, len(b), _FORMATS[fmt], C.byref(h)))
+    return _seqfile_rows(h)
+
+
 def fold(seq: str, no_gu: bool = False) -> np.ndarray:
     """Synthetic base-pairing probabilities (Nussinov-Boltzmann stand-in for
     Vienna pf_fold), packed strict upper triangle of length n(n-1)/2."""
@@ -236,6 +272,17 @@ class Dataset:
             barr = None
         rc = lib().sk_dataset_add(self._h, label.encode(), n, carr, barr, C.c_float(th), int(use_bp))
         check(rc)
+
+    def add_file(self, label: str, path: str, fmt: str = "fa", th: float = 0.01,
+                 use_bp: bool = True) -> int:
+        """Append every example of an example file, as DataLoader<MData>
+        (stem_kernel_lite/data.cpp:456-586) does for one `label file` pair of
+        the CLI; each row's bpp from ``fold`` (the synthetic stand-in for
+        Vienna).  Returns the number of examples added."""
+        alns = read_examples(path, fmt)
+        for rows in alns:
+            self.add(label, rows, th=th, use_bp=use_bp)
+        return len(alns)
 
     @classmethod
     def from_sequences(cls, seqs: Iterable[str], labels: Optional[Iterable[str]] = None,
