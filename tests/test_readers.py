@@ -6,7 +6,7 @@ regex restatement in oracle/readers.py and against expectations derived by
 hand from the reference grammars (common/fa.cpp:13-55, aln.cpp:16-107,
 maf.cpp:15-49).  The reference readers need Boost.Spirit, absent here:
 parity unpinned against the reference's own output, pinned by construction.
-Host code only: runs without a GPU."""
+The parsing tests are host code (no GPU); one GPU test runs a file end to end."""
 import numpy as np
 import pytest
 
@@ -153,3 +153,31 @@ def test_read_file_and_dataset(tmp_path):
     assert ds.add_file("+1", str(p), "fa") == 2 and len(ds) == 2
     with pytest.raises(ska.StemKernelError, match="no such file"):
         ska.read_examples(str(tmp_path / "missing.fa"))
+
+
+@pytest.mark.gpu
+def test_clustal_file_to_gram(gpu_ctx, tmp_path):
+    """End to end: a CLUSTAL file through the reader, the synthetic fold and
+    the GPU Gram, against the oracle on the same rows (1e-6 relative)."""
+    from oracle import pyoracle as po
+    from tests.helpers import make_examples, mutate_alignment, rel_err
+    alns = [mutate_alignment(s, 3, 40 + k) for k, s in enumerate(ska.random_sequences(4, 60, 77))]
+    text = ""
+    for a in alns:
+        text += "CLUSTAL W (1.83) multiple sequence alignment\n\n"
+        for off in range(0, 60, 25):
+            text += "".join(f"r{r}   {row[off:off + 25]}\n" for r, row in enumerate(a)) + "     *\n"
+            text += "\n" if off + 25 < 60 else ""
+    p = tmp_path / "x.aln"
+    p.write_text(text)
+    got_rows = ska.read_examples(str(p), "aln")
+    assert got_rows == [list(a) for a in alns]
+    ds = ska.Dataset()
+    ds.add_file("+1", str(p), "aln")
+    _, om = make_examples(got_rows)
+    kern = ska.SuStemStrKernel()
+    K = gpu_ctx.gram(ds, kern)
+    n = len(alns)
+    ref = np.array([[po.kernel_value(kern.params.kind, om[min(i, j)], om[max(i, j)], kern.params)
+                     for j in range(n)] for i in range(n)])
+    assert rel_err(K, ref) < 1e-6
