@@ -65,3 +65,10 @@ variant:
 	$(HIPCC) $(CXXFLAGS) $(DEFS) -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/var/$(NAME)/sk_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/var/$(NAME)/sk_api.o $(BUILD)/var/$(NAME)/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o -Wl,-rpath,/opt/rocm/lib
 .PHONY: variant
+
+# 4-D kernel experiment build: make variant4 NAME=x DEFS="-DSK4_MINB=4" -> build/libsk_x.so
+variant4:
+	@mkdir -p $(BUILD)/var/$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/stem4d.hip -o $(BUILD)/var/$(NAME)/stem4d.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/sk_api.o $(BUILD)/kernels/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/var/$(NAME)/stem4d.o $(BUILD)/kernels/phmm.o -Wl,-rpath,/opt/rocm/lib
+.PHONY: variant4

@@ -55,8 +55,11 @@ __device__ __forceinline__ int row_off(int m, int d2) {
 // BAND: partial_dp (stem_kernel.cpp:113-280) with the -b band constraints:
 // cells outside the band stay zero, K0 past c_high[j-1] and K1 below
 // c_low[i+1] take the reference's boundary approximations.
+#ifndef SK4_MINB  // minimum 4-wave workgroups per CU (register budget knob)
+#define SK4_MINB 1
+#endif
 template <int CPL, bool BAND>
-__global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
+__global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t it = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
@@ -111,7 +114,9 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
   const bool stack_on = bp_ij > bound;
   const uint8_t xi = xs[i], xj = xs[j - 1];
   const double stk = P.stack, sub = P.subst;
-  int clj = 0, chj = m, cli = 0, chi = m, chjm1 = m, cli1 = 0;
+  int clj = 0, chj = m, cli = 0, chi = m, chjm1 = m, cli1 = 0, cljm1 = 0, chi1 = m;
+  // y spans with cells inside the constraints: l in [clj, chj], k in [cli, chi]
+  int d2_lo = 1, d2_hi = m;
   if (BAND) {
     const int32_t* cl = P.band_lo + pr.band_off;
     const int32_t* ch = P.band_hi + pr.band_off;
@@ -121,7 +126,19 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
     chi = ch[i];
     chjm1 = ch[j - 1];
     cli1 = cl[i + 1];
+    cljm1 = cl[j - 1];
+    chi1 = ch[i + 1];
+    d2_lo = max(1, clj - chi);
+    d2_hi = min(m, chj - cli);
+    if (i == 0 && j == n && lane == 0) P.out[pr.out_index] = 0.0;  // K0(0,n,0,m) may lie outside
   }
+  // Partial DP: only the spans [d2_lo, d2_hi] are swept and only cells inside
+  // the constraints are read or written.  Nothing outside them is ever read:
+  // A and B are read at cells inside their own planes' constraints (or at the
+  // boundary cells of the approximations), and the stacking read of plane
+  // (i+1,j-1) is guarded by that plane's constraints unless it is the fully
+  // initialised plane (j-1,j-1) or its diagonal row.
+  const bool cg_guard = BAND && d1 >= 3;
 
   double K2[CPL], G2[CPL], K3[CPL], G3[CPL];
   uint8_t yk[CPL];
@@ -150,7 +167,8 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
   double pK0[CPL], pG0[CPL], pK1[CPL], pG1[CPL], pGs[CPL];
   float pbp[CPL];
   uint8_t pyl[CPL];
-  int Rm2 = 0, Rm1 = 0, R = pad4(m + 1);  // row offsets of d2-2, d2-1, d2
+  // row offsets of d2-1 and d2
+  int Rm1 = BAND ? row_off(m, d2_lo - 1) : 0, R = BAND ? row_off(m, d2_lo) : pad4(m + 1);
   auto fetch = [&](int d2, int Rd, int Rd2) {
     const int kmax = m - d2;
     const int e2 = d2 - 1;
@@ -158,24 +176,33 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + 64 * c;
+      const int l = k + d2;
       pbp[c] = 0.0f;
       pGs[c] = 0.0;
       pyl[c] = 0;
-      if (k <= kmax) {
-        pK0[c] = A[Rd + k];
-        pG0[c] = A[cp + Rd + k];
-        pK1[c] = B[2 * cp + Rd + k];
-        pG1[c] = B[3 * cp + Rd + k];
+      if (BAND) pK0[c] = pG0[c] = pK1[c] = pG1[c] = 0.0;
+      const bool on = !BAND || (l >= clj && l <= chj && k >= cli && k <= chi);
+      if (k <= kmax && on) {
+        if (!BAND || l <= chjm1) {
+          pK0[c] = A[Rd + k];
+          pG0[c] = A[cp + Rd + k];
+        }
+        if (!BAND || k >= cli1) {
+          pK1[c] = B[2 * cp + Rd + k];
+          pG1[c] = B[3 * cp + Rd + k];
+        }
         if (stack_on) {
           pbp[c] = bpy[ye + k];
           pyl[c] = ys[k + d2 - 1];
-          if (d2 >= 2) pGs[c] = Cg[Rd2 + k + 1];
+          if (d2 >= 2 && (!cg_guard || d2 == 2 ||
+                          (l - 1 >= cljm1 && l - 1 <= chjm1 && k + 1 >= cli1 && k + 1 <= chi1)))
+            pGs[c] = Cg[Rd2 + k + 1];
         }
       }
     }
   };
-  if (m >= 1) fetch(1, R, 0);
-  for (int d2 = 1; d2 <= m; ++d2) {
+  if (d2_lo <= d2_hi) fetch(d2_lo, R, d2_lo >= 2 ? row_off(m, d2_lo - 2) : 0);
+  for (int d2 = d2_lo; d2 <= d2_hi; ++d2) {
     double cK0[CPL], cG0[CPL], cK1[CPL], cG1[CPL], cGs[CPL];
     float cbp[CPL];
     uint8_t cyl[CPL];
@@ -190,7 +217,7 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
       cyl[c] = pyl[c];
     }
     const int Rn = R + pad4(m + 1 - d2);
-    if (d2 + 1 <= m) fetch(d2 + 1, Rn, Rm1);
+    if (d2 + 1 <= d2_hi) fetch(d2 + 1, Rn, Rm1);
     // K3/G3 of (k+1, l): my next cell, or the next lane's first (span d2-1)
     double K3n[CPL], G3n[CPL];
 #pragma unroll
@@ -248,11 +275,13 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
         G1 += g2;
         K0 += K1;
         G0 += G1;
-        if (BAND && !on) K0 = G0 = K1 = G1 = k2 = g2 = k3 = g3 = 0.0;  // zero fill
-        cur[R + k] = K0;
-        cur[cp + R + k] = G0;
-        cur[2 * cp + R + k] = K1;
-        cur[3 * cp + R + k] = G1;
+        if (BAND && !on) K0 = G0 = K1 = G1 = k2 = g2 = k3 = g3 = 0.0;  // outside: zero state
+        if (on) {
+          cur[R + k] = K0;
+          cur[cp + R + k] = G0;
+          cur[2 * cp + R + k] = K1;
+          cur[3 * cp + R + k] = G1;
+        }
         K2[c] = k2;
         G2[c] = g2;
         K3[c] = k3;
@@ -260,7 +289,6 @@ __global__ void __launch_bounds__(256) sk_stem4d_kernel(Stem4dLaunch P) {
         if (d2 == m && i == 0 && j == n) P.out[pr.out_index] = K0;  // K0(0,n,0,m)
       }
     }
-    Rm2 = Rm1;
     Rm1 = R;
     R = Rn;
   }

@@ -726,7 +726,14 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // StemKernel::operator() (stem_kernel.h:52-55): partial_dp when ali_bound
   // > 0 or band > 0; ali_bound is a float option
   const float ali_bound = (float)kp->ali_bound;
-  const bool ali = ali_bound > 0.0f;
+  const bool ali = ali_bound > 0.0f;  // -a: residues must be ACGU
+  // Anchors come from the PairHMM only with the intended zerop.  As the
+  // reference builds today (ali_zerop_fixed 0) every posterior is NaN, no
+  // position is anchored and the constraints are [0, |y|] for every x
+  // position whatever the band (checked against the oracle's
+  // full NaN-propagating restatement), and partial_dp over the full range is
+  // full_dp operation for operation.
+  const bool ali_phmm = ali && kp->ali_zerop_fixed;
   // per-example tables of the examples this call touches
   struct Tab { int64_t bp = -1, chr = -1; };
   std::vector<Tab> tx(xs_->ex.size()), ty(ys_->ex.size());
@@ -824,14 +831,14 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     std::vector<int32_t> blo, bhi;
     size_t n_band = 0;
     int max_n1 = 1, max_m1 = 1;
-    if (ali) {
+    if (ali_phmm) {
       for (auto& p : prs) {
         p.band_off = (int64_t)n_band;
         n_band += (size_t)p.n + 1;
         max_n1 = std::max(max_n1, p.n + 1);
         max_m1 = std::max(max_m1, p.m + 1);
       }
-    } else if (kp->len_band > 0) {
+    } else if (!ali && kp->len_band > 0) {
       for (auto& p : prs) {
         p.band_off = (int64_t)blo.size();
         for (int i = 0; i <= p.n; ++i) {
@@ -850,8 +857,9 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
         for (int i = 0; i + d1 <= prs[p].n; ++i) items.push_back(make_int2((int)p, i));
     }
     ioff[maxn + 1] = (int64_t)items.size();
-    if (!ali) n_band = blo.size();
-    const size_t phmm_bytes = ali ? sk::phmm_scratch_bytes((int64_t)prs.size(), max_n1, max_m1) : 0;
+    if (!ali_phmm) n_band = blo.size();
+    const size_t phmm_bytes =
+        ali_phmm ? sk::phmm_scratch_bytes((int64_t)prs.size(), max_n1, max_m1) : 0;
     rc = ensure_scratch(ctx, std::max((size_t)bytes + 64, phmm_bytes));
     if (rc) return rc;
     if (Bt.cap_pairs < prs.size() || Bt.cap_items < items.size()) {
@@ -895,7 +903,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     L.band_lo = n_band ? Bt.band : nullptr;
     L.band_hi = n_band ? Bt.band + Bt.cap_band : nullptr;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
-    if (ali) {
+    if (ali_phmm) {
       sk::PhmmLaunch H;
       H.pairs = Bt.pairs;
       H.n_pairs = (int64_t)prs.size();

@@ -195,14 +195,18 @@ def test_oracle_alignment_constraints_shape(band):
     assert np.array_equal(lo, lo2) and np.array_equal(hi, hi2)
 
 
-def test_oracle_ali_as_built_equals_full_range():
-    """zerop_fixed = 0 with band 0: partial_dp over the full range."""
-    seqs = _indel_variants(3, 3, 22)
+def test_oracle_ali_as_built_equals_full_dp():
+    """zerop_fixed = 0: the NaN posteriors anchor nothing, the constraints are
+    the full range whatever the band, and partial_dp over the full range is
+    full_dp bit for bit -- what the engine runs for this mode."""
+    seqs = _indel_variants(3, 3, 22) + ["acgu", "a"]
     for a in seqs:
         for b in seqs:
-            k0 = po.stem4d(a.lower(), ska.fold(a), b.lower(), ska.fold(b), ali_bound=0.5)
-            kw = po.stem4d(a.lower(), ska.fold(a), b.lower(), ska.fold(b), band=1000)
-            assert k0 == kw
+            full = po.stem4d(a.lower(), ska.fold(a), b.lower(), ska.fold(b))
+            for band in (0, 2, 5):
+                k0 = po.stem4d(a.lower(), ska.fold(a), b.lower(), ska.fold(b), ali_bound=0.5,
+                               band=band)
+                assert k0 == full
 
 
 @pytest.mark.gpu

@@ -1,6 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
-tail -2 gpurun_out/smoke.log
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_stem4d.py -m gpu > gpurun_out/pytest_s4d.log 2>&1 || { tail -30 gpurun_out/pytest_s4d.log; exit 1; }
+tail -2 gpurun_out/pytest_s4d.log

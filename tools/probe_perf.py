@@ -16,7 +16,8 @@ ctx.upload(ds)
 kern = {"stem": ska.SuStemKernel(), "str": ska.StringKernel(), "ss": ska.SuStemStrKernel(),
         "bpla": ska.BPLAKernel(), "la": ska.BPLAKernel(noBP=True), "stem4d": ska.StemKernel4D(),
         "stem4d_ali": ska.StemKernel4D(ali_bound=0.5, ali_zerop_fixed=True),
-        "stem4d_ali0": ska.StemKernel4D(ali_bound=0.5)}[kind]
+        "stem4d_ali0": ska.StemKernel4D(ali_bound=0.5),
+        "stem4d_b10": ska.StemKernel4D(band=10)}[kind]
 iu = np.triu_indices(N)
 x, y = iu[0].astype(np.int32), iu[1].astype(np.int32)
 if len(sys.argv) > 4:  # limit the pair count (4-D kernel)
