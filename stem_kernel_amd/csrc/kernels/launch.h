@@ -100,12 +100,13 @@ int stem4d_cpl(int m);
 hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st);
 
 // PairHMM alignment constraints of a 4-D batch (-a, stem_kernel.cpp:14-81):
-// one thread per pair writes c_low/c_high (n+1 each at pair.band_off).
+// one wavefront per pair writes c_low/c_high (n+1 each at pair.band_off).
 struct PhmmLaunch {
   const Stem4dPair* pairs = nullptr;
   int64_t n_pairs = 0;
   const uint8_t* chars = nullptr;  // ACGU only (checked on the host)
-  char* scratch = nullptr;         // phmm_scratch_bytes(n_pairs, n1, m1)
+  char* scratch = nullptr;         // n_pairs * pair_bytes
+  size_t pair_bytes = 0;           // phmm_pair_bytes(n1, m1)
   int32_t n1 = 1, m1 = 1;          // max |x|+1, max |y|+1 of the launch
   float ali_bound = 0.0f;
   uint32_t band = 0;
@@ -113,7 +114,7 @@ struct PhmmLaunch {
   int32_t* band_lo = nullptr;
   int32_t* band_hi = nullptr;
 };
-size_t phmm_scratch_bytes(int64_t n_pairs, int n1, int m1);
+size_t phmm_pair_bytes(int n1, int m1);
 hipError_t launch_phmm(const PhmmLaunch& P, hipStream_t st);
 
 enum CombineMode : int32_t {

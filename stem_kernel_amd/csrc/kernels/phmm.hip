@@ -5,13 +5,10 @@
 //   MAP forward + traceback  phmm.cpp:117-236, Ribosum scores  phmm.cpp:247-320,
 //   LogValue<double> arithmetic  stem_kernel/log_value.h:55-389 (FAST_LOG1EXP0, :28).
 //
-// One thread per (x, y) pair of a 4-D batch: the PairHMM is O(|x||y|) per pair
-// against the 4-D DP's O(|x|^2 |y|^2), so it only has to stay out of the way
-// (it costs < 1 % of a batch).  Per-pair tables are interleaved across the
-// pairs of the launch (element e of pair t at e*P + t, laid out for the
-// launch's largest |x|, |y|), so the 64 lanes of a wave touch 512 contiguous
-// bytes per access.  The thread writes c_low / c_high (|x|+1 each) straight
-// into the band arrays the 4-D kernel reads, so nothing returns to the host.
+// One wavefront per (x, y) pair of a 4-D batch, sweeping 64-row strips of
+// the |x| x |y| tables along anti-diagonals (see sk_phmm_kernel).  Lane 0
+// writes c_low / c_high (|x|+1 each) straight into the band arrays the 4-D
+// kernel reads, so nothing returns to the host.
 //
 // Bit-level agreement with the host restatement: log1exp0 is the probcons
 // polynomial (no libm), evaluated without FMA contraction (this file is built
@@ -87,290 +84,312 @@ __device__ __forceinline__ void best3(double v0, double v1, double v2, double& b
   if (best < v2) best = v2, arg = 2;
 }
 
+// DPP: lane l receives lane l-1's value (lane 0 receives `low`), wave_shr:1
+__device__ __forceinline__ double shr1(double v, double low) {
+  const int rlo = __builtin_amdgcn_update_dpp(__double2loint(low), __double2loint(v), 0x138, 0xf, 0xf, false);
+  const int rhi = __builtin_amdgcn_update_dpp(__double2hiint(low), __double2hiint(v), 0x138, 0xf, 0xf, false);
+  return __hiloint2double(rhi, rlo);
+}
+// lane l receives lane l+1's value (lane 63 receives `high`), wave_shl:1
+__device__ __forceinline__ double shl1(double v, double high) {
+  const int rlo = __builtin_amdgcn_update_dpp(__double2loint(high), __double2loint(v), 0x130, 0xf, 0xf, false);
+  const int rhi = __builtin_amdgcn_update_dpp(__double2hiint(high), __double2hiint(v), 0x130, 0xf, 0xf, false);
+  return __hiloint2double(rhi, rlo);
+}
+
+// One WAVEFRONT per pair.  Rows 1..|x| are cut into strips of 64, lane l of
+// strip s owning row i = 64s + 1 + l; the strip sweeps anti-diagonals, lane l
+// handling column j = t - l at step t (t - (63 - l) counted from the right in
+// the backward pass), so a cell's row-above neighbours come from lane l-1 by
+// DPP (one and two steps old) and its left neighbour is the lane's own
+// previous output.  Row 0 (whose recurrences differ) is done by lane 0 alone.
+// The strip's boundary row lives in LDS.  Tables are stored skewed,
+// element (strip s, step t, state, lane) at ((s*T + t)*3 + state)*64 + lane,
+// so every store and load of a step is 512 contiguous bytes.
 __global__ void __launch_bounds__(64) sk_phmm_kernel(PhmmLaunch P) {
-  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (t >= P.n_pairs) return;
-  const Stem4dPair pr = P.pairs[t];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int pidx = blockIdx.x;
+  const int l = threadIdx.x;
+  const Stem4dPair pr = P.pairs[pidx];
   const int n = pr.n, m = pr.m;
-  const int64_t S = P.n_pairs, N1 = P.n1, M1 = P.m1;
-  double* FB = reinterpret_cast<double*>(P.scratch);  // 3 x N1 x M1: log fw, then posterior
-  double* BR = FB + 3 * N1 * M1 * S;                   // 2 rows x 3 x M1: backward
-  double* MR = BR + 6 * M1 * S;                        // 2 rows x 3 x M1: MAP forward
-  int32_t* PATH = reinterpret_cast<int32_t*>(MR + 6 * M1 * S);  // N1 + M1 steps
-  uint8_t* TR = reinterpret_cast<uint8_t*>(PATH + (N1 + M1) * S);  // N1 x M1, 2 bits per state
-#define FBA(s, i, j) FB[(((int64_t)(s) * N1 + (i)) * M1 + (j)) * S + t]
-#define BRA(r, s, j) BR[(((int64_t)(r) * 3 + (s)) * M1 + (j)) * S + t]
-#define MRA(r, s, j) MR[(((int64_t)(r) * 3 + (s)) * M1 + (j)) * S + t]
-#define TRA(i, j) TR[((int64_t)(i) * M1 + (j)) * S + t]
+  const int M1 = P.m1;
+  const int T = m + 64;          // steps of a strip
+  const int nS = (n + 63) / 64;  // strips
+  double* FBS = reinterpret_cast<double*>(P.scratch + (size_t)pidx * P.pair_bytes);
+  uint8_t* TRS = reinterpret_cast<uint8_t*>(FBS + (size_t)nS * T * 3 * 64);
+  // LDS: boundary row (3 x M1), row 0 (3 x M1), y codes (M1), path (N1 + M1)
+  double* buf = reinterpret_cast<double*>(smem);
+  double* row0 = buf + 3 * M1;
+  int32_t* yc = reinterpret_cast<int32_t*>(row0 + 3 * M1);
+  int32_t* path = yc + M1;
   const uint8_t* xs = P.chars + pr.x_chr;
   const uint8_t* ys = P.chars + pr.y_chr;
   const bool fx = P.zerop_fixed != 0;
   const double NEG = -__builtin_inf();
+#define SKW(s_, t_, st_) (((size_t)(s_) * T + (t_)) * 3 + (st_)) * 64 + l
+  for (int j = l; j < M1; j += 64) yc[j] = j < m ? base_code(ys[j]) : 0;
+  __syncthreads();
 
-  // Every pass streams its thread's previous row (and, backward, the forward
-  // values) from HBM/L2 in chunks, issuing the next chunk's loads before the
-  // current chunk's arithmetic, so the latency of a load is paid once per
-  // chunk rather than once per cell.
-  constexpr int CF = 4, CB = 4, CM = 4;
-
-  // ---- forward (phmm.cpp:10-50): log fw into FB
-  {
-    double f0 = 0.0, f1 = NEG, f2 = NEG;  // fw(., 0, 0): M = log 1
-    FBA(0, 0, 0) = f0, FBA(1, 0, 0) = f1, FBA(2, 0, 0) = f2;
-    for (int j = 1; j <= m; ++j) {  // row 0: M = IX = 0, IY from the left
+  // ---- forward (phmm.cpp:10-50), log values
+  double wlog = 0.0;  // fw[M][n][m]
+  if (l == 0) {       // row 0: M = IX = 0 past (0,0), IY from the left
+    double f0 = 0.0, f1 = NEG, f2 = NEG;
+    row0[0] = buf[0] = f0, row0[M1] = buf[M1] = f1, row0[2 * M1] = buf[2 * M1] = f2;
+    for (int j = 1; j <= m; ++j) {
       double y2 = NEG;
       y2 = lv_add(y2, f0 + kTrans[0][kIY], fx);
       y2 = lv_add(y2, f1 + kTrans[1][kIY], fx);
       y2 = lv_add(y2, f2 + kTrans[2][kIY], fx);
       f0 = NEG, f1 = NEG, f2 = y2;
-      FBA(0, 0, j) = f0, FBA(1, 0, j) = f1, FBA(2, 0, j) = f2;
+      row0[j] = buf[j] = f0, row0[M1 + j] = buf[M1 + j] = f1, row0[2 * M1 + j] = buf[2 * M1 + j] = f2;
     }
+    if (n == 0) wlog = row0[m];
   }
-  for (int i = 1; i <= n; ++i) {
-    const int xc = base_code(xs[i - 1]);
-    // column 0: M = IY = 0, IX from above
-    double u0 = FBA(0, i - 1, 0), u1 = FBA(1, i - 1, 0), u2 = FBA(2, i - 1, 0);  // (i-1, j-1)
-    double c0 = NEG, c1 = NEG, c2 = NEG;                                        // (i, j-1)
-    c1 = lv_add(c1, u0 + kTrans[0][kIX], fx);
-    c1 = lv_add(c1, u1 + kTrans[1][kIX], fx);
-    c1 = lv_add(c1, u2 + kTrans[2][kIX], fx);
-    FBA(0, i, 0) = c0, FBA(1, i, 0) = c1, FBA(2, i, 0) = c2;
-    double A0[CF], A1[CF], A2[CF], Q0[CF], Q1[CF], Q2[CF];  // (i-1, j) of this / next chunk
-    int Ay[CF], Ny[CF];
-    auto load = [&](int j0, double* B0, double* B1, double* B2, int* By) {
-#pragma unroll
-      for (int k = 0; k < CF; ++k) {
-        const int j = j0 + k;
-        B0[k] = B1[k] = B2[k] = 0.0;
-        By[k] = 0;
-        if (j <= m) {
-          B0[k] = FBA(0, i - 1, j), B1[k] = FBA(1, i - 1, j), B2[k] = FBA(2, i - 1, j);
-          By[k] = base_code(ys[j - 1]);
-        }
+  __syncthreads();
+  for (int s = 0; s < nS; ++s) {
+    const int i = 64 * s + 1 + l;
+    const bool row_ok = i <= n;
+    const int xc = row_ok ? base_code(xs[i - 1]) : 0;
+    double o0 = NEG, o1 = NEG, o2 = NEG;  // own output of the previous step: (i, j-1)
+    double d0 = NEG, d1 = NEG, d2 = NEG;  // lane l-1's output two steps ago: (i-1, j-1)
+    for (int t = 0; t < T; ++t) {
+      const int j = t - l;
+      // (i-1, j): lane l-1's previous output, lane 0 from the boundary row
+      const bool b0 = l == 0 && t <= m;
+      const double u0 = shr1(o0, b0 ? buf[t] : 0.0);
+      const double u1 = shr1(o1, b0 ? buf[M1 + t] : 0.0);
+      const double u2 = shr1(o2, b0 ? buf[2 * M1 + t] : 0.0);
+      double M = NEG, X = NEG, Y = NEG;
+      if (j == 0) {  // column 0: M = IY = 0, IX from above
+        X = lv_add(X, u0 + kTrans[0][kIX], fx);
+        X = lv_add(X, u1 + kTrans[1][kIX], fx);
+        X = lv_add(X, u2 + kTrans[2][kIX], fx);
+      } else {
+        const double e = kEmit[xc][yc[min(max(j - 1, 0), M1 - 1)]];
+        M = lv_add(M, d0 + (kTrans[0][kM] + e), fx);
+        X = lv_add(X, u0 + kTrans[0][kIX], fx);
+        Y = lv_add(Y, o0 + kTrans[0][kIY], fx);
+        M = lv_add(M, d1 + (kTrans[1][kM] + e), fx);
+        X = lv_add(X, u1 + kTrans[1][kIX], fx);
+        Y = lv_add(Y, o1 + kTrans[1][kIY], fx);
+        M = lv_add(M, d2 + (kTrans[2][kM] + e), fx);
+        X = lv_add(X, u2 + kTrans[2][kIX], fx);
+        Y = lv_add(Y, o2 + kTrans[2][kIY], fx);
       }
-    };
-    load(1, A0, A1, A2, Ay);
-    for (int j0 = 1; j0 <= m; j0 += CF) {
-      load(j0 + CF, Q0, Q1, Q2, Ny);
-#pragma unroll
-      for (int k = 0; k < CF; ++k) {
-        if (j0 + k <= m) {
-          const double e = kEmit[xc][Ay[k]];
-          const double v0 = A0[k], v1 = A1[k], v2 = A2[k];
-          double M = NEG, X = NEG, Y = NEG;
-          M = lv_add(M, u0 + (kTrans[0][kM] + e), fx);
-          X = lv_add(X, v0 + kTrans[0][kIX], fx);
-          Y = lv_add(Y, c0 + kTrans[0][kIY], fx);
-          M = lv_add(M, u1 + (kTrans[1][kM] + e), fx);
-          X = lv_add(X, v1 + kTrans[1][kIX], fx);
-          Y = lv_add(Y, c1 + kTrans[1][kIY], fx);
-          M = lv_add(M, u2 + (kTrans[2][kM] + e), fx);
-          X = lv_add(X, v2 + kTrans[2][kIX], fx);
-          Y = lv_add(Y, c2 + kTrans[2][kIY], fx);
-          FBA(0, i, j0 + k) = M, FBA(1, i, j0 + k) = X, FBA(2, i, j0 + k) = Y;
-          c0 = M, c1 = X, c2 = Y;
-          u0 = v0, u1 = v1, u2 = v2;
-        }
+      const bool ok = row_ok && j >= 0 && j <= m;
+      if (ok) {
+        FBS[SKW(s, t, 0)] = M, FBS[SKW(s, t, 1)] = X, FBS[SKW(s, t, 2)] = Y;
+        if (i == n && j == m) wlog = M;
+        if (l == 63) buf[j] = M, buf[M1 + j] = X, buf[2 * M1 + j] = Y;  // next strip's row above
       }
-#pragma unroll
-      for (int k = 0; k < CF; ++k) A0[k] = Q0[k], A1[k] = Q1[k], A2[k] = Q2[k], Ay[k] = Ny[k];
+      d0 = u0, d1 = u1, d2 = u2;
+      o0 = M, o1 = X, o2 = Y;
     }
+    __syncthreads();
   }
-  const double wlog = FBA(0, n, m);  // fw[M][|x|][|y|]
+  wlog = __shfl(wlog, n == 0 ? 0 : (n - 1) & 63, 64);
 
-  // ---- backward (phmm.cpp:52-93) in gather form, posterior fw*bk/w (:95-115)
-  // Contributions to bk(s,a,b) arrive in the reference's scatter order: from
-  // (a+1,b+1) [M], (a+1,b) [IX], (a,b+1) [IY] in the main loop, then the
-  // row-0 and column-0 loops, which also reset M,IX of row 0 and M,IY of
-  // column 0 after their last contribution.
-  for (int a = n; a >= 0; --a) {
-    const int r = a & 1, q = r ^ 1;
+  // ---- backward (phmm.cpp:52-93) in gather form + posterior (:95-115);
+  // contributions in the reference's scatter order (see the oracle): main
+  // loop (a+1,b+1) [M], (a+1,b) [IX], (a,b+1) [IY], then the column-0 loop
+  // (and, for row 0, the row-0 loop) with their resets.
+  for (int s = nS - 1; s >= 0; --s) {
+    const int a = 64 * s + 1 + l;
+    const bool row_ok = a <= n;
     const int xc = a < n ? base_code(xs[a]) : 0;
-    double c2 = NEG;  // bk(IY, a, b+1)
-    // per cell b: fw(s,a,b), bk(M,a+1,b+1), bk(IX,a+1,b), y code
-    double AF0[CB], AF1[CB], AF2[CB], AM[CB], AX[CB], NF0[CB], NF1[CB], NF2[CB], NM[CB], NX[CB];
-    int Ay[CB], Ny[CB];
-    auto load = [&](int b0, double* F0, double* F1, double* F2, double* BM, double* BX, int* By) {
+    double o0 = NEG, o1 = NEG, o2 = NEG;  // own previous output: (a, b+1)
+    double dM = NEG;                      // lane l+1's output two steps ago: bk(M, a+1, b+1)
+    for (int t = 0; t < T; ++t) {
+      const int b = m + 63 - l - t;
+      const bool b63 = l == 63 && b >= 0 && b <= m && a < n;
+      // (a+1, b): lane l+1's previous output, lane 63 from the boundary row
+      const double vM = shl1(o0, b63 ? buf[b] : 0.0);
+      const double vX = shl1(o1, b63 ? buf[M1 + b] : 0.0);
+      double acc[3];
 #pragma unroll
-      for (int k = 0; k < CB; ++k) {
-        const int b = b0 - k;
-        F0[k] = F1[k] = F2[k] = BM[k] = BX[k] = 0.0;
-        By[k] = 0;
-        if (b >= 0) {
-          F0[k] = FBA(0, a, b), F1[k] = FBA(1, a, b), F2[k] = FBA(2, a, b);
-          if (a < n) {
-            BX[k] = BRA(q, kIX, b);
-            if (b < m) BM[k] = BRA(q, kM, b + 1), By[k] = base_code(ys[b]);
-          }
+      for (int q = 0; q < 3; ++q) acc[q] = (q == kM && a == n && b == m) ? 0.0 : NEG;
+      if (a < n) {
+        if (b < m) {
+          const double e = kEmit[xc][yc[min(max(b, 0), M1 - 1)]];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) acc[q] = lv_add(acc[q], dM + (kTrans[q][kM] + e), fx);
+        }
+        if (b >= 1) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) acc[q] = lv_add(acc[q], vX + kTrans[q][kIX], fx);
         }
       }
-    };
-    load(m, AF0, AF1, AF2, AM, AX, Ay);
-    for (int b0 = m; b0 >= 0; b0 -= CB) {
-      load(b0 - CB, NF0, NF1, NF2, NM, NX, Ny);
+      if (b < m) {
 #pragma unroll
-      for (int k = 0; k < CB; ++k) {
-        const int b = b0 - k;
-        if (b >= 0) {
-          double acc[3];
+        for (int q = 0; q < 3; ++q) acc[q] = lv_add(acc[q], o2 + kTrans[q][kIY], fx);
+      }
+      if (b == 0) {  // column-0 loop: source (a+1, 0), then the reset
+        if (a < n) {
 #pragma unroll
-          for (int s = 0; s < 3; ++s) acc[s] = (s == kM && a == n && b == m) ? 0.0 : NEG;
-          const double nX = AX[k];
-          if (a < n) {
-            if (b < m) {
-              const double e = kEmit[xc][Ay[k]];
+          for (int q = 0; q < 3; ++q) acc[q] = lv_add(acc[q], vX + kTrans[q][kIX], fx);
+        }
+        acc[kM] = acc[kIY] = NEG;
+      }
+      const bool ok = row_ok && b >= 0 && b <= m;
+      if (ok) {
+        const int tf = b + l;  // forward step of cell (a, b)
 #pragma unroll
-              for (int s = 0; s < 3; ++s) acc[s] = lv_add(acc[s], AM[k] + (kTrans[s][kM] + e), fx);
-            }
-            if (b >= 1) {
+        for (int q = 0; q < 3; ++q) {
+          const size_t o = SKW(s, tf, q);
+          FBS[o] = exp((FBS[o] + acc[q]) - wlog);
+        }
+        if (l == 0) buf[b] = acc[0], buf[M1 + b] = acc[1], buf[2 * M1 + b] = acc[2];
+      }
+      dM = vM;
+      o0 = acc[0], o1 = acc[1], o2 = acc[2];
+    }
+    __syncthreads();
+  }
+  if (l == 0) {  // row 0 (a = 0): main loop from row 1, row-0 loop, column-0 loop
+    const int xc = n > 0 ? base_code(xs[0]) : 0;
+    double c2 = NEG;  // bk(IY, 0, b+1)
+    for (int b = m; b >= 0; --b) {
+      double acc[3];
 #pragma unroll
-              for (int s = 0; s < 3; ++s) acc[s] = lv_add(acc[s], nX + kTrans[s][kIX], fx);
-            }
-          }
-          if (a >= 1 && b < m) {
+      for (int q = 0; q < 3; ++q) acc[q] = (q == kM && n == 0 && b == m) ? 0.0 : NEG;
+      if (n >= 1) {
+        if (b < m) {
+          const double e = kEmit[xc][yc[b]];
 #pragma unroll
-            for (int s = 0; s < 3; ++s) acc[s] = lv_add(acc[s], c2 + kTrans[s][kIY], fx);
-          }
-          if (a == 0) {
-            if (b < m) {  // row-0 loop, source (0, b+1)
+          for (int q = 0; q < 3; ++q) acc[q] = lv_add(acc[q], buf[b + 1] + (kTrans[q][kM] + e), fx);
+        }
+        if (b >= 1) {
 #pragma unroll
-              for (int s = 0; s < 3; ++s) acc[s] = lv_add(acc[s], c2 + kTrans[s][kIY], fx);
-            }
-            if (b >= 1) {
-              acc[kM] = acc[kIX] = NEG;
-            } else if (n >= 1) {  // (0,0): column-0 loop, source (1, 0)
-#pragma unroll
-              for (int s = 0; s < 3; ++s) acc[s] = lv_add(acc[s], nX + kTrans[s][kIX], fx);
-            }
-          } else if (b == 0) {
-            if (a < n) {  // column-0 loop, source (a+1, 0)
-#pragma unroll
-              for (int s = 0; s < 3; ++s) acc[s] = lv_add(acc[s], nX + kTrans[s][kIX], fx);
-            }
-            acc[kM] = acc[kIY] = NEG;
-          }
-          BRA(r, 0, b) = acc[0], BRA(r, 1, b) = acc[1], BRA(r, 2, b) = acc[2];
-          FBA(0, a, b) = exp((AF0[k] + acc[0]) - wlog);
-          FBA(1, a, b) = exp((AF1[k] + acc[1]) - wlog);
-          FBA(2, a, b) = exp((AF2[k] + acc[2]) - wlog);
-          c2 = acc[2];
+          for (int q = 0; q < 3; ++q) acc[q] = lv_add(acc[q], buf[M1 + b] + kTrans[q][kIX], fx);
         }
       }
+      if (b < m) {
 #pragma unroll
-      for (int k = 0; k < CB; ++k) {
-        AF0[k] = NF0[k], AF1[k] = NF1[k], AF2[k] = NF2[k], AM[k] = NM[k], AX[k] = NX[k];
-        Ay[k] = Ny[k];
+        for (int q = 0; q < 3; ++q) acc[q] = lv_add(acc[q], c2 + kTrans[q][kIY], fx);
       }
+      if (b >= 1) {
+        acc[kM] = acc[kIX] = NEG;
+      } else if (n >= 1) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) acc[q] = lv_add(acc[q], buf[M1] + kTrans[q][kIX], fx);
+      }
+#pragma unroll
+      for (int q = 0; q < 3; ++q) row0[q * M1 + b] = exp((row0[q * M1 + b] + acc[q]) - wlog);
+      c2 = acc[2];
     }
   }
+  __syncthreads();
 
   // ---- MAP path over the posteriors: PairHMM::forward(fb, tr) (phmm.cpp:117-185)
-  {
-    double p0 = FBA(0, 0, 0), p1 = FBA(1, 0, 0), p2 = FBA(2, 0, 0);
-    MRA(0, 0, 0) = p0, MRA(0, 1, 0) = p1, MRA(0, 2, 0) = p2;
-    TRA(0, 0) = 0x3f;
+  if (l == 0) {  // row 0
+    double p0 = row0[0], p1 = row0[M1], p2 = row0[2 * M1];
+    buf[0] = p0, buf[M1] = p1, buf[2 * M1] = p2;
     for (int j = 1; j <= m; ++j) {
+      const double fy = row0[2 * M1 + j];
       double bst;
       int k;
-      const double fy = FBA(kIY, 0, j);
       best3(p0 + fy, p1 + fy, p2 + fy, bst, k);
       p0 = 0.0, p1 = 0.0, p2 = bst;
-      MRA(0, 0, j) = p0, MRA(0, 1, j) = p1, MRA(0, 2, j) = p2;
-      TRA(0, j) = (uint8_t)(3 | (3 << 2) | (k << 4));
+      buf[j] = p0, buf[M1 + j] = p1, buf[2 * M1 + j] = p2;
     }
   }
-  for (int i = 1; i <= n; ++i) {
-    const int r = i & 1, q = r ^ 1;
-    double u0 = MRA(q, 0, 0), u1 = MRA(q, 1, 0), u2 = MRA(q, 2, 0);  // (i-1, j-1)
-    double bst;
-    int kx;
-    const double fx0 = FBA(kIX, i, 0);
-    best3(u0 + fx0, u1 + fx0, u2 + fx0, bst, kx);
-    double c0 = 0.0, c1 = bst, c2 = 0.0;  // (i, j-1)
-    MRA(r, 0, 0) = c0, MRA(r, 1, 0) = c1, MRA(r, 2, 0) = c2;
-    TRA(i, 0) = (uint8_t)(3 | (kx << 2) | (3 << 4));
-    for (int j0 = 1; j0 <= m; j0 += CM) {
-      double V0[CM], V1[CM], V2[CM], PM[CM], PX[CM], PY[CM];
-#pragma unroll
-      for (int k = 0; k < CM; ++k) {
-        const int j = j0 + k;
-        V0[k] = V1[k] = V2[k] = PM[k] = PX[k] = PY[k] = 0.0;
-        if (j <= m) {
-          V0[k] = MRA(q, 0, j), V1[k] = MRA(q, 1, j), V2[k] = MRA(q, 2, j);  // (i-1, j)
-          PM[k] = FBA(kM, i, j), PX[k] = FBA(kIX, i, j), PY[k] = FBA(kIY, i, j);
-        }
+  __syncthreads();
+  for (int s = 0; s < nS; ++s) {
+    const int i = 64 * s + 1 + l;
+    const bool row_ok = i <= n;
+    double o0 = 0.0, o1 = 0.0, o2 = 0.0, d0 = 0.0, d1 = 0.0, d2 = 0.0;
+    for (int t = 0; t < T; ++t) {
+      const int j = t - l;
+      const bool b0 = l == 0 && t <= m;
+      const double u0 = shr1(o0, b0 ? buf[t] : 0.0);
+      const double u1 = shr1(o1, b0 ? buf[M1 + t] : 0.0);
+      const double u2 = shr1(o2, b0 ? buf[2 * M1 + t] : 0.0);
+      const bool ok = row_ok && j >= 0 && j <= m;
+      double fM = 0.0, fX = 0.0, fY = 0.0;
+      if (ok) fM = FBS[SKW(s, t, 0)], fX = FBS[SKW(s, t, 1)], fY = FBS[SKW(s, t, 2)];
+      double bm = 0.0, bx, by = 0.0;
+      int km = 3, kx, ky = 3;
+      if (j == 0) {
+        best3(u0 + fX, u1 + fX, u2 + fX, bx, kx);
+      } else {
+        best3(d0 + fM, d1 + fM, d2 + fM, bm, km);
+        best3(u0 + fX, u1 + fX, u2 + fX, bx, kx);
+        best3(o0 + fY, o1 + fY, o2 + fY, by, ky);
       }
-#pragma unroll
-      for (int k = 0; k < CM; ++k) {
-        const int j = j0 + k;
-        if (j <= m) {
-          double bm, bx, by;
-          int km, kx2, ky;
-          best3(u0 + PM[k], u1 + PM[k], u2 + PM[k], bm, km);
-          best3(V0[k] + PX[k], V1[k] + PX[k], V2[k] + PX[k], bx, kx2);
-          best3(c0 + PY[k], c1 + PY[k], c2 + PY[k], by, ky);
-          MRA(r, 0, j) = bm, MRA(r, 1, j) = bx, MRA(r, 2, j) = by;
-          TRA(i, j) = (uint8_t)(km | (kx2 << 2) | (ky << 4));
-          c0 = bm, c1 = bx, c2 = by;
-          u0 = V0[k], u1 = V1[k], u2 = V2[k];
-        }
+      if (ok) {
+        TRS[((size_t)s * T + t) * 64 + l] = (uint8_t)(km | (kx << 2) | (ky << 4));
+        if (l == 63) buf[j] = bm, buf[M1 + j] = bx, buf[2 * M1 + j] = by;
       }
+      d0 = u0, d1 = u1, d2 = u2;
+      o0 = bm, o1 = bx, o2 = by;
     }
+    __syncthreads();
   }
 
-  // ---- traceback (phmm.cpp:187-216), then the anchors (stem_kernel.cpp:40-67)
-  int len = 0;
-  {
-    int s = kM, x = n, y = m;
-    PATH[(int64_t)len++ * S + t] = (s << 30) | (x << 15) | y;
+  // ---- traceback (phmm.cpp:187-216) and anchors (stem_kernel.cpp:40-67)
+  if (l == 0) {
+    int len = 0;
+    int st = kM, x = n, y = m;
+    path[len++] = (st << 30) | (x << 15) | y;
     while (x != 0 && y != 0) {
-      const int code = (TRA(x, y) >> (2 * s)) & 3;
-      if (s == kM) --x, --y;
-      else if (s == kIX) --x;
+      const int sx = (x - 1) >> 6, lx = (x - 1) & 63;
+      const int code = (TRS[((size_t)sx * T + y + lx) * 64 + lx] >> (2 * st)) & 3;
+      if (st == kM) --x, --y;
+      else if (st == kIX) --x;
       else --y;
-      if (code == 3) break;  // unreachable: every interior cell has a predecessor
-      s = code;
-      PATH[(int64_t)len++ * S + t] = (s << 30) | (x << 15) | y;
+      if (code == 3) break;  // unreachable: interior cells always have a predecessor
+      st = code;
+      path[len++] = (st << 30) | (x << 15) | y;
     }
-  }
-  int32_t* clo = P.band_lo + pr.band_off;
-  int32_t* chi = P.band_hi + pr.band_off;
-  int low_x = 0, low_y = 0;
-  for (int k = len - 1; k >= 0; --k) {
-    const int32_t v = PATH[(int64_t)k * S + t];
-    const int s = (v >> 30) & 3, x = (v >> 15) & 0x7fff, y = v & 0x7fff;
-    if (s == kM && FBA(kM, x, y) >= (double)P.ali_bound) {
-      for (int i = low_x; i < x; ++i) clo[i] = low_y, chi[i] = y;
-      clo[x] = y, chi[x] = y;
-      low_x = x + 1, low_y = y;
-    }
-  }
-  for (int i = low_x; i <= n; ++i) clo[i] = low_y, chi[i] = m;
-  const int band = (int)P.band;
-  if (band > 0)
-    for (int i = 0; i <= n; ++i)
-      if (chi[i] - clo[i] < band * 2) {
-        const int j = (chi[i] + clo[i]) / 2;
-        clo[i] = j < band ? 0 : j - band;
-        chi[i] = j + band > m ? m : j + band;
+    int32_t* clo = P.band_lo + pr.band_off;
+    int32_t* chi = P.band_hi + pr.band_off;
+    int low_x = 0, low_y = 0;
+    for (int k = len - 1; k >= 0; --k) {
+      const int32_t v = path[k];
+      const int ps = (v >> 30) & 3, px = (v >> 15) & 0x7fff, py = v & 0x7fff;
+      if (ps != kM) continue;
+      double post;
+      if (px == 0) {
+        post = row0[py];
+      } else {
+        const int sx = (px - 1) >> 6, lx = (px - 1) & 63;
+        post = FBS[(((size_t)sx * T + py + lx) * 3 + kM) * 64 + lx];
       }
-#undef FBA
-#undef BRA
-#undef MRA
-#undef TRA
+      if (post >= (double)P.ali_bound) {
+        for (int i = low_x; i < px; ++i) clo[i] = low_y, chi[i] = py;
+        clo[px] = py, chi[px] = py;
+        low_x = px + 1, low_y = py;
+      }
+    }
+    for (int i = low_x; i <= n; ++i) clo[i] = low_y, chi[i] = m;
+    const int band = (int)P.band;
+    if (band > 0)
+      for (int i = 0; i <= n; ++i)
+        if (chi[i] - clo[i] < band * 2) {
+          const int j = (chi[i] + clo[i]) / 2;
+          clo[i] = j < band ? 0 : j - band;
+          chi[i] = j + band > m ? m : j + band;
+        }
+  }
+#undef SKW
 }
 
 }  // namespace
 
-size_t phmm_scratch_bytes(int64_t n_pairs, int n1, int m1) {
-  const int64_t c = (int64_t)n1 * m1;
-  return (size_t)n_pairs * (size_t)(8 * (3 * c + 12 * (int64_t)m1) + 4 * ((int64_t)n1 + m1) + c) + 256;
+size_t phmm_pair_bytes(int n1, int m1) {
+  const size_t nS = (size_t)(n1 - 1 + 63) / 64, T = (size_t)m1 - 1 + 64;
+  return (nS * T * (3 * 64 * 8 + 64) + 255) & ~(size_t)255;
 }
+
+size_t phmm_lds_bytes(int n1, int m1) { return (size_t)m1 * (6 * 8 + 4) + (size_t)(n1 + m1) * 4 + 16; }
 
 hipError_t launch_phmm(const PhmmLaunch& P, hipStream_t st) {
   if (P.n_pairs == 0) return hipSuccess;
-  const dim3 grid((unsigned)((P.n_pairs + 63) / 64)), block(64);
-  hipLaunchKernelGGL(sk_phmm_kernel, grid, block, 0, st, P);
+  const size_t lds = phmm_lds_bytes(P.n1, P.m1);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(sk_phmm_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sk_phmm_kernel, dim3((unsigned)P.n_pairs), dim3(64), lds, st, P);
   return hipGetLastError();
 }
 

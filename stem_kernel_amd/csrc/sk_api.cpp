@@ -859,7 +859,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     ioff[maxn + 1] = (int64_t)items.size();
     if (!ali_phmm) n_band = blo.size();
     const size_t phmm_bytes =
-        ali_phmm ? sk::phmm_scratch_bytes((int64_t)prs.size(), max_n1, max_m1) : 0;
+        ali_phmm ? prs.size() * sk::phmm_pair_bytes(max_n1, max_m1) : 0;
     rc = ensure_scratch(ctx, std::max((size_t)bytes + 64, phmm_bytes));
     if (rc) return rc;
     if (Bt.cap_pairs < prs.size() || Bt.cap_items < items.size()) {
@@ -911,6 +911,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       H.scratch = reinterpret_cast<char*>(ctx->scratch);
       H.n1 = max_n1;
       H.m1 = max_m1;
+      H.pair_bytes = sk::phmm_pair_bytes(max_n1, max_m1);
       H.ali_bound = ali_bound;
       H.band = kp->len_band;
       H.zerop_fixed = kp->ali_zerop_fixed ? 1 : 0;

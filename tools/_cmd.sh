@@ -2,3 +2,11 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_stem4d.py -m gpu > gpurun_out/pytest_s4d.log 2>&1 || { tail -30 gpurun_out/pytest_s4d.log; exit 1; }
 tail -2 gpurun_out/pytest_s4d.log
+: > gpurun_out/b10.log
+for k in stem4d_ali stem4d_b10; do
+  timeout -k 10 200 python -u tools/probe_perf.py 200 32 $k >> gpurun_out/b10.log 2>&1 || { tail -20 gpurun_out/b10.log; exit 1; }
+  echo "== $k" >> gpurun_out/b10.log
+done
+grep "pairs/s\|==" gpurun_out/b10.log
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ali -o ali -- python3 -u tools/probe_perf.py 200 24 stem4d_ali > gpurun_out/probe_ali.log 2>&1 || { tail -20 gpurun_out/probe_ali.log; exit 1; }
