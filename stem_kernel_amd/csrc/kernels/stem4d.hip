@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
   // A and B are read at cells inside their own planes' constraints (or at the
   // boundary cells of the approximations), and the stacking read of plane
   // (i+1,j-1) is guarded by that plane's constraints unless it is the fully
-  // initialised plane (j-1,j-1) or its diagonal row.
+  // initialised plane (j-1,j-1).
   const bool cg_guard = BAND && d1 >= 3;
 
   double K2[CPL], G2[CPL], K3[CPL], G3[CPL];
@@ -149,14 +149,14 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
     yk[c] = k < m ? ys[k] : 0;
   }
 
-  // d2 = 0: cells (l,l): K0 = 1, G0 = G0(i+1,j,l,l)*g, K1 = G1 = 0  (:313-316)
+  // d2 = 0: cells (l,l): K0 = 1, G0 = G0(i+1,j,l,l)*g, K1 = G1 = 0  (:313-316);
+  // partial DP: only l in [clj, chj] (the others are never read)
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int k = k0 + 64 * c;
-    if (k <= m) {
-      const bool on = !BAND || (k >= clj && k <= chj);
-      cur[k] = on ? 1.0 : 0.0;
-      cur[cp + k] = on ? B[cp + k] * g : 0.0;
+    if (k <= m && (!BAND || (k >= clj && k <= chj))) {
+      cur[k] = 1.0;
+      cur[cp + k] = B[cp + k] * g;
       cur[2 * cp + k] = 0.0;
       cur[3 * cp + k] = 0.0;
     }
@@ -194,9 +194,11 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
         if (stack_on) {
           pbp[c] = bpy[ye + k];
           pyl[c] = ys[k + d2 - 1];
-          if (d2 >= 2 && (!cg_guard || d2 == 2 ||
-                          (l - 1 >= cljm1 && l - 1 <= chjm1 && k + 1 >= cli1 && k + 1 <= chi1)))
-            pGs[c] = Cg[Rd2 + k + 1];
+          // cell (k+1, l-1) of plane (i+1, j-1): inside its constraints (on
+          // its diagonal row, l-1 inside them) unless that plane is (j-1,j-1)
+          const bool cg_on = !cg_guard || (l - 1 >= cljm1 && l - 1 <= chjm1 &&
+                                           (d2 == 2 || (k + 1 >= cli1 && k + 1 <= chi1)));
+          if (d2 >= 2 && cg_on) pGs[c] = Cg[Rd2 + k + 1];
         }
       }
     }

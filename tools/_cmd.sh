@@ -8,5 +8,3 @@ for k in stem4d_ali stem4d_b10; do
   echo "== $k" >> gpurun_out/b10.log
 done
 grep "pairs/s\|==" gpurun_out/b10.log
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ali -o ali -- python3 -u tools/probe_perf.py 200 24 stem4d_ali > gpurun_out/probe_ali.log 2>&1 || { tail -20 gpurun_out/probe_ali.log; exit 1; }
