@@ -987,6 +987,12 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
       for (int64_t k = 0; k < n; ++k) byy[pos[y[k]]++] = k;
     }
+    // within one y, costliest x first: the waves of a workgroup take the
+    // item's pairs round-robin, so equal-cost rounds and a cheap last round
+    for (int j = 0; j < ny; ++j)
+      std::stable_sort(byy.begin() + cnt[j], byy.begin() + cnt[j + 1], [&](int64_t a, int64_t b) {
+        return PX.ex_nl[x[a]] > PX.ex_nl[x[b]];
+      });
     ixs.resize(n);
     ioidx.resize(n);
     for (int64_t t = 0; t < n; ++t) {
@@ -1044,7 +1050,20 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       }
 #endif
       C.grid = ctx->n_cu * per_cu;
-      const int chunk = 2 * C.nwaves;
+      // Work item = up to `rounds` pairs per wave of one y.  A workgroup
+      // waits for its slowest wave at every item boundary, so items are as
+      // large as the balance allows: about two items per workgroup on
+      // average, at least two rounds (NS: 12 rounds, +4 % over 2).
+      int64_t class_pairs = 0;
+      for (int j = 0; j < ny; ++j)
+        if (sk::stem_maxk(std::max(PY.ex_nl[j], 1)) == maxk) class_pairs += cnt[j + 1] - cnt[j];
+#ifdef SK_ITEM_ROUNDS
+      const int64_t rounds = SK_ITEM_ROUNDS;
+#else
+      const int64_t rounds =
+          std::max<int64_t>(2, class_pairs / std::max<int64_t>(1, 2LL * C.grid * C.nwaves));
+#endif
+      const int64_t chunk = rounds * C.nwaves;
       struct It {
         int4 v;
         double cost;

@@ -1,10 +1,11 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_stem4d.py -m gpu > gpurun_out/pytest_s4d.log 2>&1 || { tail -30 gpurun_out/pytest_s4d.log; exit 1; }
-tail -2 gpurun_out/pytest_s4d.log
-: > gpurun_out/b10.log
-for k in stem4d_ali stem4d_b10; do
-  timeout -k 10 200 python -u tools/probe_perf.py 200 32 $k >> gpurun_out/b10.log 2>&1 || { tail -20 gpurun_out/b10.log; exit 1; }
-  echo "== $k" >> gpurun_out/b10.log
+: > gpurun_out/var_items.log
+for cfg in c2 c5; do
+for v in base r2; do
+  if [ $v = base ]; then L=""; else L=build/libsk_$v.so; fi
+  SK_LIB_PATH=$L timeout -k 10 300 python3 -u bench.py --config $cfg --no-cpu-baseline > gpurun_out/vb.log 2>&1 || { tail -20 gpurun_out/vb.log; exit 1; }
+  echo "$cfg $v $(tail -1 gpurun_out/vb.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["roofline"]["kernel_ms_per_launch"])')" >> gpurun_out/var_items.log
 done
-grep "pairs/s\|==" gpurun_out/b10.log
+done
+cat gpurun_out/var_items.log
