@@ -42,11 +42,11 @@ PEAK_FP64_TFS = 78.6    # FP64 vector
 
 # name -> kernel, n examples, length, slices, config id (seed 0x5EED0000+id)
 CONFIGS = {
-    "ns": dict(kernel="ss", n=4096, L=200, slices=64, cid=2, cpu_pairs=12288),
+    "ns": dict(kernel="ss", n=4096, L=200, slices=48, cid=2, cpu_pairs=12288),
     "c2": dict(kernel="ss", n=256, L=150, slices=4, cid=1, cpu_pairs=12288),
     "c3": dict(kernel="stem4d", n=1024, L=200, slices=2050, cid=2, cpu_pairs=32),
     "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=16, cid=3, cpu_pairs=196608),
-    "c5": dict(kernel="stem", n=8192, L=300, slices=1024, cid=4, cpu_pairs=4096),
+    "c5": dict(kernel="stem", n=8192, L=300, slices=128, cid=4, cpu_pairs=4096),
 }
 
 
