@@ -235,3 +235,18 @@ def test_stem4d_alignment_constraints_reject_non_acgu(gpu_ctx):
     with pytest.raises(ska.StemKernelError):
         gpu_ctx.gram(ds, ska.StemKernel4D(ali_bound=0.5))
     gpu_ctx.gram(ds, ska.StemKernel4D())  # without -a the residues are free
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("band", [0, 4])
+def test_stem4d_alignment_constraints_long(gpu_ctx, band):
+    """Sequences past 64 and 128 nt: several 64-row strips of the PairHMM
+    sweep and the 4-slot register class of the 4-D kernel, with anchored
+    constraints (oracle fast: partial_dp only visits constrained cells)."""
+    seqs = _indel_variants(21, 3, 150) + _indel_variants(22, 2, 75)
+    ds, _ = make_examples(seqs)
+    kern = ska.StemKernel4D(ali_bound=0.5, ali_zerop_fixed=True, band=band)
+    x = np.array([0, 1, 2, 0, 3, 4, 1], np.int32)
+    y = np.array([1, 0, 2, 2, 4, 3, 3], np.int32)
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    assert rel_err(got, _oracle(seqs, kern, list(zip(x, y)))) < TOL
