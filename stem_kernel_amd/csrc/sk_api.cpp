@@ -127,6 +127,10 @@ struct sk_context {
   void* work = nullptr;
   size_t work_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+  // side stream: the string kernel of a stem+string kind runs beside the
+  // persistent stem launches and fills the CUs their tails free
+  hipStream_t side = nullptr;
+  hipEvent_t evf = nullptr, evj = nullptr;
   double last_stem_ms = 0.0, last_str_ms = 0.0, last_cells = 0.0;
   int32_t last_launches = 0;
 };
@@ -1139,6 +1143,17 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   double* stem_out = (combine_mode(kp->kind) == sk::kCombineStem) ? out_dev : d_stem;
   double* str_out = (combine_mode(kp->kind) == sk::kCombineStr) ? out_dev : d_str;
 
+  // string kernel inputs first: with a stem part it forks to the side stream
+  // here, ahead of the stem launches
+  const bool side = stem && str;
+  if (str) {
+    SK_HIP(ctx, hipMemcpyAsync(d_px, x, nb * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_py, y, nb * 4, hipMemcpyHostToDevice, S));
+    if (side) {
+      SK_HIP(ctx, hipEventRecord(ctx->evf, S));
+      SK_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->evf, 0));
+    }
+  }
   if (stem) {
     SK_HIP(ctx, hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(int4),
                                hipMemcpyHostToDevice, S));
@@ -1214,8 +1229,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     ctx->last_launches = (int32_t)classes.size();
   }
   if (str) {
-    SK_HIP(ctx, hipMemcpyAsync(d_px, x, nb * 4, hipMemcpyHostToDevice, S));
-    SK_HIP(ctx, hipMemcpyAsync(d_py, y, nb * 4, hipMemcpyHostToDevice, S));
+    const hipStream_t SS = side ? ctx->side : S;
     sk::StrLaunch T;
     T.xset = xs_->dev;
     T.yset = ys_->dev;
@@ -1234,9 +1248,13 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     if (lds > 65536) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for string kernel LDS");
     const int per_cu = std::max(1, std::min<int>((int)(163840 / lds), 8));
     const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (n + w - 1) / w);
-    SK_HIP(ctx, hipEventRecord(ctx->ev2, S));
-    SK_HIP(ctx, sk::launch_str(T, (int)g, w, S));
-    SK_HIP(ctx, hipEventRecord(ctx->ev3, S));
+    SK_HIP(ctx, hipEventRecord(ctx->ev2, SS));
+    SK_HIP(ctx, sk::launch_str(T, (int)g, w, SS));
+    SK_HIP(ctx, hipEventRecord(ctx->ev3, SS));
+    if (side) {  // join before the combine
+      SK_HIP(ctx, hipEventRecord(ctx->evj, ctx->side));
+      SK_HIP(ctx, hipStreamWaitEvent(S, ctx->evj, 0));
+    }
   }
   const int32_t mode = combine_mode(kp->kind);
   if (mode != sk::kCombineStem && mode != sk::kCombineStr)
@@ -1348,6 +1366,10 @@ int sk_open(int device, void* hip_stream, sk_context** out) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return SK_ERR_HIP;
     c->own_stream = true;
   }
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evf, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess)
+    return SK_ERR_HIP;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess)
     return SK_ERR_HIP;
@@ -1364,6 +1386,9 @@ int sk_close(sk_context* ctx) {
   if (ctx->s4d.pairs) (void)hipFree(ctx->s4d.pairs);
   if (ctx->s4d.items) (void)hipFree(ctx->s4d.items);
   if (ctx->s4d.band) (void)hipFree(ctx->s4d.band);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  for (hipEvent_t e : {ctx->evf, ctx->evj})
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3})
     if (e) (void)hipEventDestroy(e);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
