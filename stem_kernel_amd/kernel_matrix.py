@@ -520,3 +520,22 @@ class KernelMatrix:
     def print(self, out=sys.stdout):
         """libsvm precomputed-kernel layout (kernel_matrix.cpp:756-770)."""
         out.write(format_libsvm(self.matrix, self.label))
+
+    def save(self, path: str) -> None:
+        """App's output file (common/framework.h:138-160): the libsvm text,
+        gzip-compressed when the name ends in ".gz" and bzip2 when ".bz2"."""
+        text = format_libsvm(self.matrix, self.label).encode()
+        if path.endswith(".gz"):
+            import gzip
+            with gzip.open(path, "wb") as f:
+                f.write(text)
+        elif path.endswith(".bz2"):
+            import bz2
+            with bz2.open(path, "wb") as f:
+                f.write(text)
+        else:
+            try:
+                with open(path, "wb") as f:
+                    f.write(text)
+            except OSError as e:
+                raise StemKernelError(-1, f"{path}: cannot open for writing") from e

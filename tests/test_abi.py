@@ -1,4 +1,5 @@
 """The C ABI library loads and exports every symbol include/stem_kernel.h
+import pytest
 declares; host-only entry points behave (no GPU needed)."""
 import os
 import re
@@ -69,3 +70,21 @@ def test_dataset_errors():
     else:
         raise AssertionError("wrong alignment accepted")
     assert len(ds) == 0
+
+
+def test_kernel_matrix_save_compressed(tmp_path):
+    """App's output (common/framework.h:138-160): .gz / .bz2 by file name."""
+    import bz2
+    import gzip
+    km = ska.KernelMatrix.__new__(ska.KernelMatrix)  # no GPU context needed to write
+    km.matrix = np.array([[1.0, 0.5], [0.5, 1.0]])
+    km.label = ["+1", "-1"]
+    want = ska.format_libsvm(km.matrix, km.label)
+    km.save(str(tmp_path / "k.txt"))
+    km.save(str(tmp_path / "k.txt.gz"))
+    km.save(str(tmp_path / "k.txt.bz2"))
+    assert (tmp_path / "k.txt").read_text() == want
+    assert gzip.open(tmp_path / "k.txt.gz", "rt").read() == want
+    assert bz2.open(tmp_path / "k.txt.bz2", "rt").read() == want
+    with pytest.raises(ska.StemKernelError, match="cannot open"):
+        km.save(str(tmp_path / "missing" / "k.txt"))
