@@ -1,10 +1,10 @@
 """The C ABI library loads and exports every symbol include/stem_kernel.h
-import pytest
 declares; host-only entry points behave (no GPU needed)."""
 import os
 import re
 
 import numpy as np
+import pytest
 
 import stem_kernel_amd as ska
 from stem_kernel_amd import _lib
