@@ -297,7 +297,7 @@ def main():
         except Exception:
             pass
         cpu = None
-        if not a.no_cpu_baseline:
+        if not a.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             cpu = cpu_baseline(cfg, data, a.cpu_pairs)
         kname = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
                  "stem4d": "sk_stem4d_kernel", "bpla": "sk_bpla_kernel"}[kind]
