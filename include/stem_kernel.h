@@ -236,6 +236,17 @@ int sk_format_libsvm(const double *matrix, int32_t rows, int32_t cols,
  * Vienna pf_fold; out gets n*(n-1)/2 doubles in the packed layout above. */
 int sk_fold_synthetic(const char *seq, int32_t n, int32_t no_gu, double *out);
 
+/* BPLA gradients, the bpla_optimizer's per-pair step: for k < n_pairs,
+ * value[k] = BPLAKernel::compute_gradients(xs[x[k]], ys[y[k]], score_table,
+ * {alpha, beta, gap, ext}, d) and grad[4k..4k+3] = d (d/d alpha, beta, gap,
+ * ext).  Replaces bpla_kernel/bpla_kernel.cpp:385-401 (BPLA_Forward :178-243,
+ * BPLA_Backward :245-305, BPLA_ForwardBackword :325-383) as called from
+ * bpla_kernel/bpla_optimizer.cpp:52-255.  Uses kp->alpha/beta/gap/ext and
+ * kp->score_table; examples need base pairs.  Host buffers; synchronous. */
+int sk_bpla_gradients(sk_context *ctx, sk_dataset *xs, sk_dataset *ys, const sk_kernel_params *kp,
+                      const int32_t *x, const int32_t *y, int64_t n_pairs, double *value,
+                      double *grad);
+
 /* ---------------------------------------------------------------- example files
  * The readers DataLoader<MData>::get (stem_kernel_lite/data.cpp:547-586) pulls
  * examples from, with the reference grammars' exact acceptance (Boost.Spirit

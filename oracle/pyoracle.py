@@ -74,6 +74,9 @@ def oracle():
         L.orc_alignment_constraints.restype = C.c_int
         L.orc_alignment_constraints.argtypes = [C.c_char_p, C.c_char_p, C.c_float, C.c_uint,
                                                 C.c_int, _U, _U]
+        L.orc_bpla_gradients.restype = C.c_double
+        L.orc_bpla_gradients.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_double,
+                                         C.c_double, C.c_double, _D, _D]
         L.orc_naive_string.restype = C.c_double
         L.orc_naive_string.argtypes = [C.c_char_p, C.c_char_p, C.c_double]
         _o = L
@@ -246,3 +249,13 @@ def alignment_constraints(x: str, y: str, ali_bound: float, band=0, zerop_fixed=
                                           lo.ctypes.data_as(_U), hi.ctypes.data_as(_U)):
         raise ValueError("unknown nucleotide")
     return lo, hi
+
+
+def bpla_gradients(x: OMData, y: OMData, alpha, beta, gap, ext, table16):
+    """BPLAKernel::compute_gradients (bpla_kernel.cpp:385-401): (value,
+    [d_alpha, d_beta, d_gap, d_ext], backward total)."""
+    t = np.ascontiguousarray(table16, dtype=np.float64)
+    d = np.zeros(5)
+    v = oracle().orc_bpla_gradients(x.h, y.h, alpha, beta, gap, ext, t.ctypes.data_as(_D),
+                                    d.ctypes.data_as(_D))
+    return v, d[:4].copy(), float(d[4])

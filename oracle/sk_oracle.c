@@ -923,6 +923,130 @@ double orc_bpla(const orc_mdata *x, const orc_mdata *y, int no_bp, int sw, doubl
   return r;
 }
 
+/* ---- BPLA gradients (the bpla_optimizer's per-pair step) ----------------
+ * BPLAKernel::compute_gradients (bpla_kernel/bpla_kernel.cpp:385-401):
+ * BPLA_Forward (:178-243) and BPLA_Backward (:245-305) over the states
+ * M, IX, IY, LX, LY, RX, RY, then BPLA_ForwardBackword (:325-383), which sums
+ * d(value)/d(alpha, beta, gap, ext) over the cells.  Scores are
+ * alpha*(pr*pr' + pl*pl') + pu*pu'*LAScore with the float products as written.
+ * Returns the forward value 1 + M + RX + RY at (|x|, |y|). */
+enum { G_M = 0, G_IX, G_IY, G_LX, G_LY, G_RX, G_RY, G_N };
+
+double orc_bpla_gradients(const orc_mdata *x, const orc_mdata *y, double alpha, double beta,
+                          double gap, double ext, const double *table16, double *d4) {
+  if (!x->bpp || !y->bpp) return NAN; /* the reference indexes empty vectors */
+  la_score S;
+  memset(&S, 0, sizeof(S));
+  S.x = x;
+  S.y = y;
+  S.table = table16;
+  const int n = x->len, m = y->len, W = m + 1;
+  float *w = (float *)malloc(sizeof(float) * 3 * (size_t)(n + m + 1));
+  float *xl = w, *xr = xl + n, *xu = xr + n, *yl = xu + n, *yr = yl + m, *yu = yr + m;
+  orc_bpla_weights(x, xl, xr, xu);
+  orc_bpla_weights(y, yl, yr, yu);
+  const size_t cells = (size_t)(n + 1) * (m + 1);
+  double *F = (double *)calloc(G_N * cells, sizeof(double));
+  double *B = (double *)calloc(G_N * cells, sizeof(double));
+#define T3(T, s, i, j) T[(size_t)(s) * cells + (size_t)(i) * W + (j)]
+  const double beta_gap = exp(beta * gap), beta_ext = exp(beta * ext);
+  /* BPLA_Forward */
+  T3(F, G_M, 0, 0) = 1;
+  T3(F, G_LX, 0, 0) = 1;
+  T3(F, G_LY, 0, 0) = 1;
+  for (int i = 1; i <= n; ++i) T3(F, G_LX, i, 0) += T3(F, G_LX, i - 1, 0);
+  for (int j = 1; j <= m; ++j) T3(F, G_LY, 0, j) += T3(F, G_LY, 0, j - 1);
+  for (int i = 1; i <= n; ++i)
+    for (int j = 1; j <= m; ++j) {
+      const double s = alpha * (double)(xr[i - 1] * yr[j - 1] + xl[i - 1] * yl[j - 1]) +
+                       (double)(xu[i - 1] * yu[j - 1]) * la_score_fn(&S, i - 1, j - 1);
+      const double bs = exp(beta * s);
+      T3(F, G_M, i, j) += bs * T3(F, G_M, i - 1, j - 1);
+      T3(F, G_M, i, j) += bs * T3(F, G_IX, i - 1, j - 1);
+      T3(F, G_M, i, j) += bs * T3(F, G_IY, i - 1, j - 1);
+      T3(F, G_M, i, j) += bs * T3(F, G_LX, i - 1, j - 1);
+      T3(F, G_M, i, j) += bs * T3(F, G_LY, i - 1, j - 1);
+      T3(F, G_IX, i, j) += beta_gap * T3(F, G_M, i - 1, j);
+      T3(F, G_IX, i, j) += beta_ext * T3(F, G_IX, i - 1, j);
+      T3(F, G_IY, i, j) += beta_gap * T3(F, G_M, i, j - 1);
+      T3(F, G_IY, i, j) += beta_gap * T3(F, G_IX, i, j - 1);
+      T3(F, G_IY, i, j) += beta_ext * T3(F, G_IY, i, j - 1);
+      T3(F, G_LX, i, j) += T3(F, G_LX, i - 1, 0);
+      T3(F, G_LY, i, j) += T3(F, G_LX, i, j - 1);
+      T3(F, G_LY, i, j) += T3(F, G_LY, i, j - 1);
+      T3(F, G_RX, i, j) += T3(F, G_M, i - 1, j);
+      T3(F, G_RX, i, j) += T3(F, G_RX, i - 1, j);
+      T3(F, G_RY, i, j) += T3(F, G_M, i, j - 1);
+      T3(F, G_RY, i, j) += T3(F, G_RX, i, j - 1);
+      T3(F, G_RY, i, j) += T3(F, G_RY, i, j - 1);
+    }
+  /* BPLA_Backward */
+  T3(B, G_M, n, m) = 1;
+  T3(B, G_RX, n, m) = 1;
+  T3(B, G_RY, n, m) = 1;
+  for (int i = n; i != 0; --i)
+    for (int j = m; j != 0; --j) {
+      const double s = alpha * (double)(xr[i - 1] * yr[j - 1] + xl[i - 1] * yl[j - 1]) +
+                       (double)(xu[i - 1] * yu[j - 1]) * la_score_fn(&S, i - 1, j - 1);
+      const double bs = exp(beta * s);
+      T3(B, G_M, i - 1, j - 1) += bs * T3(B, G_M, i, j);
+      T3(B, G_IX, i - 1, j - 1) += bs * T3(B, G_M, i, j);
+      T3(B, G_IY, i - 1, j - 1) += bs * T3(B, G_M, i, j);
+      T3(B, G_LX, i - 1, j - 1) += bs * T3(B, G_M, i, j);
+      T3(B, G_LY, i - 1, j - 1) += bs * T3(B, G_M, i, j);
+      T3(B, G_M, i - 1, j) += beta_gap * T3(B, G_IX, i, j);
+      T3(B, G_IX, i - 1, j) += beta_ext * T3(B, G_IX, i, j);
+      T3(B, G_M, i, j - 1) += beta_gap * T3(B, G_IY, i, j);
+      T3(B, G_IX, i, j - 1) += beta_gap * T3(B, G_IY, i, j);
+      T3(B, G_IY, i, j - 1) += beta_ext * T3(B, G_IY, i, j);
+      T3(B, G_LX, i - 1, 0) += T3(B, G_LX, i, j);
+      T3(B, G_LX, i, j - 1) += T3(B, G_LY, i, j);
+      T3(B, G_LY, i, j - 1) += T3(B, G_LY, i, j);
+      T3(B, G_M, i - 1, j) += T3(B, G_RX, i, j);
+      T3(B, G_RX, i - 1, j) += T3(B, G_RX, i, j);
+      T3(B, G_M, i, j - 1) += T3(B, G_RY, i, j);
+      T3(B, G_RX, i, j - 1) += T3(B, G_RY, i, j);
+      T3(B, G_RY, i, j - 1) += T3(B, G_RY, i, j);
+    }
+  for (int i = n; i != 0; --i) T3(B, G_LX, i - 1, 0) += T3(B, G_LX, i, 0);
+  for (int j = m; j != 0; --j) T3(B, G_LY, 0, j - 1) += T3(B, G_LY, 0, j);
+  /* BPLA_ForwardBackword: update_alpha_beta (:307-314), update_beta_gap_ext (:316-323) */
+  double da = 0.0, db = 0.0, dg = 0.0, de = 0.0;
+  for (int i = 1; i <= n; ++i)
+    for (int j = 1; j <= m; ++j) {
+      const double wp = (double)(xr[i - 1] * yr[j - 1] + xl[i - 1] * yl[j - 1]);
+      const double wu = (double)(xu[i - 1] * yu[j - 1]) * la_score_fn(&S, i - 1, j - 1);
+      const double bs = exp(beta * (alpha * wp + wu));
+      const double bm = T3(B, G_M, i, j);
+      const int src[5] = {G_M, G_IX, G_IY, G_LX, G_LY};
+      for (int t = 0; t < 5; ++t) {
+        const double v = T3(F, src[t], i - 1, j - 1) * bs * bm;
+        da += beta * wp * v;
+        db += (alpha * wp + wu) * v;
+      }
+      double v = T3(F, G_M, i - 1, j) * beta_gap * T3(B, G_IX, i, j);
+      db += gap * v, dg += beta * v;
+      v = T3(F, G_IX, i - 1, j) * beta_ext * T3(B, G_IX, i, j);
+      db += ext * v, de += beta * v;
+      v = T3(F, G_M, i, j - 1) * beta_gap * T3(B, G_IY, i, j);
+      db += gap * v, dg += beta * v;
+      v = T3(F, G_IX, i, j - 1) * beta_gap * T3(B, G_IY, i, j);
+      db += gap * v, dg += beta * v;
+      v = T3(F, G_IY, i, j - 1) * beta_ext * T3(B, G_IY, i, j);
+      db += ext * v, de += beta * v;
+    }
+  const double r = 1 + T3(F, G_M, n, m) + T3(F, G_RX, n, m) + T3(F, G_RY, n, m);
+  d4[0] = da, d4[1] = db, d4[2] = dg, d4[3] = de;
+  /* the backward pass's own total (1 + M + LX + LY at (0,0)) is the same
+   * partition function: d4[4] reports it as a consistency check */
+  d4[4] = 1 + T3(B, G_M, 0, 0) + T3(B, G_LX, 0, 0) + T3(B, G_LY, 0, 0);
+#undef T3
+  free(F);
+  free(B);
+  free(w);
+  return r;
+}
+
 /* ------------------------------------------------------------------ */
 /* 4-D stem kernel: StemKernel<double,BPMat>::full_dp
  * (stem_kernel/stem_kernel.cpp:282-351) with dp_init / dp_update (:85-111).

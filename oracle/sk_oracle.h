@@ -99,6 +99,13 @@ double orc_bpla(const orc_mdata *x, const orc_mdata *y, int no_bp, int sw, doubl
  * probabilities per aligned position); example built with use_bp. */
 void orc_bpla_weights(const orc_mdata *d, float *p_left, float *p_right, float *p_unpair);
 
+/* BPLAKernel::compute_gradients (bpla_kernel/bpla_kernel.cpp:178-401): the
+ * forward value and d4[0..3] = d/d(alpha, beta, gap, ext); d4[4] = the
+ * backward pass's total (equal to the value up to rounding).  Examples need
+ * base pairs. */
+double orc_bpla_gradients(const orc_mdata *x, const orc_mdata *y, double alpha, double beta,
+                          double gap, double ext, const double *table16, double *d4);
+
 /* 4-D stem kernel full_dp (stem_kernel/stem_kernel.cpp:282-351) of two
  * single sequences.  model 0: bpx/bpy are the strict-upper packed bpp of x
  * and y (PFWrapper pr; prob(i,i)=0); 1/2: NormalBasePair / WobbleBasePair

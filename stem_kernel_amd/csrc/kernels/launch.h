@@ -63,6 +63,24 @@ struct BplaLaunch {
   int32_t lds_max_len = 0;  // even, >= 64 (streamed strips)
 };
 
+// BPLA gradients (bpla_kernel.cpp:178-401): one thread per pair, forward and
+// backward tables interleaved in scratch (n_pairs * bpla_grad_pair_bytes)
+struct BplaGradLaunch {
+  DevSet xset, yset;
+  const double* table = nullptr;  // 16, x residue major
+  double alpha = 0.0, beta = 0.0, gap = 0.0, ext = 0.0;
+  double beta_gap = 0.0, beta_ext = 0.0;
+  const int32_t* xs = nullptr;
+  const int32_t* ys = nullptr;
+  int64_t n_pairs = 0;
+  int32_t n1 = 1, m1 = 1;  // max |x|+1, |y|+1 of the launch
+  double* scratch = nullptr;
+  double* value = nullptr;  // n_pairs
+  double* grad = nullptr;   // 4 * n_pairs: d/d(alpha, beta, gap, ext)
+};
+size_t bpla_grad_pair_bytes(int n1, int m1);
+hipError_t launch_bpla_grad(const BplaGradLaunch& P, hipStream_t st);
+
 // per-wave LDS of the BPLA kernel: 4 boundary rows + y columns (16-B aligned)
 __host__ __device__ inline size_t bpla_wave_lds_bytes(int maxlen) {
   const size_t b = (size_t)4 * (maxlen + 2) * 8 + (size_t)maxlen * 32;

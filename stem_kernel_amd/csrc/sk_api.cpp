@@ -1274,6 +1274,88 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   return SK_OK;
 }
 
+// BPLAKernel::compute_gradients over pairs (the bpla_optimizer's per-pair
+// step, bpla_kernel.cpp:385-401, bpla_optimizer.cpp:52-255): batches bounded
+// by scratch memory, one thread per pair.
+int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
+                   const int32_t* x, const int32_t* y, int64_t n, double* value, double* grad) {
+  if (!ctx || !xs_ || !ys_ || !kp || (n > 0 && (!x || !y || !value || !grad)))
+    return fail(ctx, SK_ERR_INVALID, "null argument");
+  int rc = check_set(ctx, xs_);
+  if (rc) return rc;
+  rc = check_set(ctx, ys_);
+  if (rc) return rc;
+  if (n <= 0) return n < 0 ? fail(ctx, SK_ERR_INVALID, "negative pair count") : SK_OK;
+  for (int64_t k = 0; k < n; ++k) {
+    if (x[k] < 0 || x[k] >= (int)xs_->ex.size() || y[k] < 0 || y[k] >= (int)ys_->ex.size())
+      return fail(ctx, SK_ERR_INVALID, "pair index out of range");
+    if (!xs_->ex[x[k]].has_bp || !ys_->ex[y[k]].has_bp)
+      return fail(ctx, SK_ERR_INVALID, "BPLA gradients need examples built with use_bp");
+  }
+  size_t free_b = 0, total_b = 0;
+  SK_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
+  const double budget = std::min(16e9, 0.5 * (double)free_b);
+  rc = ensure_work(ctx, 16 * 8 + 4096);
+  if (rc) return rc;
+  double* d_tb = static_cast<double*>(ctx->work);
+  hipStream_t S = ctx->stream;
+  SK_HIP(ctx, hipMemcpyAsync(d_tb, kp->score_table, 16 * 8, hipMemcpyHostToDevice, S));
+  int32_t* d_xy = nullptr;
+  double* d_out = nullptr;
+  SK_HIP(ctx, hipMalloc(&d_xy, (size_t)2 * n * sizeof(int32_t)));
+  SK_HIP(ctx, hipMalloc(&d_out, (size_t)5 * n * sizeof(double)));
+  SK_HIP(ctx, hipMemcpyAsync(d_xy, x, (size_t)n * 4, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, hipMemcpyAsync(d_xy + n, y, (size_t)n * 4, hipMemcpyHostToDevice, S));
+  double total_ms = 0.0;
+  for (int64_t b0 = 0; b0 < n && rc == SK_OK;) {
+    int n1 = 1, m1 = 1;
+    int64_t b1 = b0;
+    while (b1 < n) {
+      const int a1 = std::max(n1, xs_->ex[x[b1]].len + 1), c1 = std::max(m1, ys_->ex[y[b1]].len + 1);
+      if (b1 > b0 && (double)(b1 - b0 + 1) * sk::bpla_grad_pair_bytes(a1, c1) > budget) break;
+      n1 = a1, m1 = c1, ++b1;
+    }
+    const int64_t cnt = b1 - b0;
+    rc = ensure_scratch(ctx, (size_t)cnt * sk::bpla_grad_pair_bytes(n1, m1) + 64);
+    if (rc) break;
+    sk::BplaGradLaunch G;
+    G.xset = xs_->dev;
+    G.yset = ys_->dev;
+    G.table = d_tb;
+    G.alpha = kp->alpha;
+    G.beta = kp->beta;
+    G.gap = kp->gap;
+    G.ext = kp->ext;
+    G.beta_gap = std::exp(kp->beta * kp->gap);  // bpla_kernel.cpp:188-189
+    G.beta_ext = std::exp(kp->beta * kp->ext);
+    G.xs = d_xy + b0;
+    G.ys = d_xy + n + b0;
+    G.n_pairs = cnt;
+    G.n1 = n1;
+    G.m1 = m1;
+    G.scratch = ctx->scratch;
+    G.value = d_out + b0;
+    G.grad = d_out + n + 4 * b0;
+    SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
+    SK_HIP(ctx, sk::launch_bpla_grad(G, S));
+    SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
+    SK_HIP(ctx, hipStreamSynchronize(S));
+    float ms = 0.f;
+    SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    total_ms += ms;
+    b0 = b1;
+  }
+  if (rc == SK_OK) {
+    hipError_t e = hipMemcpy(value, d_out, (size_t)n * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(grad, d_out + n, (size_t)4 * n * 8, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = fail(ctx, SK_ERR_HIP, hipGetErrorString(e));
+  }
+  (void)hipFree(d_xy);
+  (void)hipFree(d_out);
+  ctx->last_stem_ms = total_ms;
+  return rc;
+}
+
 int pairs_host(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
                const int32_t* x, const int32_t* y, int64_t n, double* out) {
   if (n == 0) return SK_OK;
@@ -1621,6 +1703,12 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
 int sk_pairs_device(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp, const int32_t* x,
                     const int32_t* y, int64_t n_pairs, double* out_dev) {
   return run_pairs(ctx, ds, ds, kp, x, y, n_pairs, out_dev);
+}
+
+int sk_bpla_gradients(sk_context* ctx, sk_dataset* xs, sk_dataset* ys, const sk_kernel_params* kp,
+                      const int32_t* x, const int32_t* y, int64_t n_pairs, double* value,
+                      double* grad) {
+  return bpla_gradients(ctx, xs, ys, kp, x, y, n_pairs, value, grad);
 }
 
 int sk_pairs(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp, const int32_t* x,

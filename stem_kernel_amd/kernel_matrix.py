@@ -416,6 +416,24 @@ class Context:
                                  out.ctypes.data_as(C.POINTER(C.c_double))))
         return out
 
+    def bpla_gradients(self, ds: Dataset, kernel: "BPLAKernel", x, y, ys: Optional[Dataset] = None):
+        """BPLAKernel::compute_gradients for pairs (ds[x[k]], (ys or ds)[y[k]])
+        (bpla_kernel.cpp:385-401, the bpla_optimizer's per-pair step): returns
+        (values[n], grads[n, 4] = d/d(alpha, beta, gap, ext))."""
+        ys = ds if ys is None else ys
+        self.upload(ds)
+        self.upload(ys)
+        x = np.ascontiguousarray(x, dtype=np.int32)
+        y = np.ascontiguousarray(y, dtype=np.int32)
+        val = np.zeros(x.size, dtype=np.float64)
+        grad = np.zeros((x.size, 4), dtype=np.float64)
+        self._chk(lib().sk_bpla_gradients(self._h, ds.handle, ys.handle, C.byref(kernel.params),
+                                          x.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          y.ctypes.data_as(C.POINTER(C.c_int32)), x.size,
+                                          val.ctypes.data_as(C.POINTER(C.c_double)),
+                                          grad.ctypes.data_as(C.POINTER(C.c_double))))
+        return val, grad
+
     def pairs_device(self, ds: Dataset, kernel: _Kernel, x, y, out_ptr: int) -> None:
         self.upload(ds)
         x = np.ascontiguousarray(x, dtype=np.int32)
