@@ -1294,7 +1294,9 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
   }
   size_t free_b = 0, total_b = 0;
   SK_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
-  const double budget = std::min(16e9, 0.5 * (double)free_b);
+  // one thread per pair, latency-bound: throughput grows with the pairs in
+  // flight, so batches take most of the HBM
+  const double budget = std::min(96e9, 0.6 * (double)free_b);
   rc = ensure_work(ctx, 16 * 8 + 4096);
   if (rc) return rc;
   double* d_tb = static_cast<double*>(ctx->work);

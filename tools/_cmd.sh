@@ -2,5 +2,5 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_bpla_grad.py -m gpu > gpurun_out/pytest_grad.log 2>&1 || { tail -30 gpurun_out/pytest_grad.log; exit 1; }
 tail -3 gpurun_out/pytest_grad.log
-timeout -k 10 300 python -u tools/probe_grad.py 128 > gpurun_out/probe_grad.log 2>&1 || { tail -20 gpurun_out/probe_grad.log; exit 1; }
+timeout -k 10 300 python -u tools/probe_grad.py 256 > gpurun_out/probe_grad.log 2>&1 || { tail -20 gpurun_out/probe_grad.log; exit 1; }
 cat gpurun_out/probe_grad.log
