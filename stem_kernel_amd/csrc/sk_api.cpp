@@ -105,6 +105,10 @@ struct sk_dataset {
   DeviceBuffers buf;
   HostPack pack;
   std::string err;
+  // x-role leaf-column closed forms (sk_prep_kernel) for one loop_gap: they
+  // depend only on the dataset (immutable once uploaded) and loop_gap
+  double* prep = nullptr;
+  double prep_loop_gap = -1.0;
 };
 
 struct Stem4dBatch {
@@ -1100,7 +1104,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   const size_t nb = (size_t)n;
   size_t need = 0;
   need += 256 * 8 + 16 * 8 + (size_t)(max_len + 4) * 8 * 2;
-  need += (size_t)PX.nd_a.size() * 8 * 3 + 1024;  // L, SL, xr_SL
+  need += 1024;
   need += items.size() * sizeof(int4) + nb * (4 + 8) + nb * 8 * 2 + nb * 4 * 2 + 64 + 8 * 256;
   need += 16 * 256;
   rc = ensure_work(ctx, need);
@@ -1110,9 +1114,6 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   double* d_gp_loop = A.take<double>(max_len + 4);
   double* d_st = A.take<double>(16);
   double* d_gp_str = A.take<double>(max_len + 4);
-  double* d_L = A.take<double>(std::max<size_t>(PX.nd_a.size(), 1));
-  double* d_SL = A.take<double>(std::max<size_t>(PX.nd_a.size(), 1));
-  double* d_xSL = A.take<double>(std::max<size_t>(PX.nd_a.size(), 1));
   int4* d_items = A.take<int4>(std::max<size_t>(items.size(), 1));
   int32_t* d_ixs = A.take<int32_t>(std::max<size_t>(nb, 1));
   int64_t* d_oidx = A.take<int64_t>(std::max<size_t>(nb, 1));
@@ -1159,9 +1160,20 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
                                hipMemcpyHostToDevice, S));
     SK_HIP(ctx, hipMemcpyAsync(d_ixs, ixs.data(), nb * 4, hipMemcpyHostToDevice, S));
     SK_HIP(ctx, hipMemcpyAsync(d_oidx, ioidx.data(), nb * 8, hipMemcpyHostToDevice, S));
-    sk::DevParamNodes pn{d_L, d_SL, d_xSL};
     const double gap2 = kp->loop_gap * kp->loop_gap;
-    SK_HIP(ctx, sk::launch_prep(xs_->dev, pn, d_gp_loop, gap2, S));
+    const size_t nnd = std::max<size_t>(PX.nd_a.size(), 1);
+    if (!xs_->prep) {
+      void* p = nullptr;
+      SK_HIP(ctx, hipMalloc(&p, 3 * nnd * sizeof(double)));
+      xs_->prep = static_cast<double*>(p);
+      xs_->buf.ptrs.push_back(p);
+      xs_->prep_loop_gap = -1.0;
+    }
+    sk::DevParamNodes pn{xs_->prep, xs_->prep + nnd, xs_->prep + 2 * nnd};
+    if (!(xs_->prep_loop_gap == kp->loop_gap)) {  // once per dataset and loop_gap
+      SK_HIP(ctx, sk::launch_prep(xs_->dev, pn, d_gp_loop, gap2, S));
+      xs_->prep_loop_gap = kp->loop_gap;
+    }
     // one scratch buffer serves the class launches in turn (same stream)
     size_t scratch_need = 0;
     for (const StemClass& C : classes) {

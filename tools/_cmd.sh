@@ -1,6 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_bpla_grad.py -m gpu > gpurun_out/pytest_grad.log 2>&1 || { tail -30 gpurun_out/pytest_grad.log; exit 1; }
-tail -3 gpurun_out/pytest_grad.log
-timeout -k 10 300 python -u tools/probe_grad.py 256 > gpurun_out/probe_grad.log 2>&1 || { tail -20 gpurun_out/probe_grad.log; exit 1; }
-cat gpurun_out/probe_grad.log
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+: > gpurun_out/var_knobs.log
+for v in a b; do
+  timeout -k 10 300 python3 -u bench.py --no-cpu-baseline > gpurun_out/vb.log 2>&1 || { tail -20 gpurun_out/vb.log; exit 1; }
+  echo "$v $(tail -1 gpurun_out/vb.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["kernel_ms_per_launch"])')" >> gpurun_out/var_knobs.log
+done
+cat gpurun_out/var_knobs.log
