@@ -748,12 +748,19 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     }
     __syncthreads();
 
-    // static round-robin of the item's pairs over the waves (uniform loop)
-    for (int t = wave_u; t < item.z; t += nwaves) {
+    // the item's pairs (costliest first) go to whichever wave is free next
+    // (the first nwaves dealt statically; ctl[1] counts the pairs taken), so
+    // the workgroup waits at the item boundary for one pair, not a round
+    if (threadIdx.x == 0) ctl[1] = nwaves;
+    __syncthreads();
+    for (int t = wave_u; t < item.z;) {
       const int x = P.xs[item.y + t];
-      const double k =
-          stem_pair<MAXK>(P, Y, R, hb, co, gp, slab, x, lane);
+      const double k = stem_pair<MAXK>(P, Y, R, hb, co, gp, slab, x, lane);
       if (lane == 0) P.out[P.oidx[item.y + t]] = k;
+      int nt = 0;
+      // generic-pointer atomic on the LDS counter
+      if (lane == 0) nt = atomicAdd(reinterpret_cast<int*>(const_cast<int32_t*>((const int32_t*)ctl)) + 1, 1);
+      t = __builtin_amdgcn_readfirstlane(nt);
     }
   }
 }

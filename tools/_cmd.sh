@@ -4,7 +4,11 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 gpurun_out/pytest_gpu.log
 : > gpurun_out/var_knobs.log
 for v in a b; do
-  timeout -k 10 300 python3 -u bench.py --no-cpu-baseline > gpurun_out/vb.log 2>&1 || { tail -20 gpurun_out/vb.log; exit 1; }
+  timeout -k 10 200 python3 -u bench.py --no-cpu-baseline > gpurun_out/vb.log 2>&1 || { tail -20 gpurun_out/vb.log; exit 1; }
   echo "$v $(tail -1 gpurun_out/vb.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["kernel_ms_per_launch"])')" >> gpurun_out/var_knobs.log
+done
+for c in c2 c5; do
+  timeout -k 10 300 python3 -u bench.py --config $c --no-cpu-baseline > gpurun_out/vb.log 2>&1 || { tail -20 gpurun_out/vb.log; exit 1; }
+  echo "$c $(tail -1 gpurun_out/vb.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["kernel_ms_per_launch"])')" >> gpurun_out/var_knobs.log
 done
 cat gpurun_out/var_knobs.log
