@@ -66,3 +66,32 @@ def test_bpla_gradients_need_base_pairs(gpu_ctx):
     ds, _ = make_examples(["ACGUACGU", "ACGUAC"], use_bp=False)
     with pytest.raises(ska.StemKernelError):
         gpu_ctx.bpla_gradients(ds, ska.BPLAKernel(), [0], [1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("normalize", [False, True])
+def test_bpla_gradient_gram(gpu_ctx, normalize):
+    """CalcMatrix / CalcMatrixN of bpla_optimizer.cpp:52-255 over the GPU
+    gradients, against the same formulas over the oracle's."""
+    alns = _alns(51, 4, 35)
+    ds, om = make_examples(alns)
+    kern = ska.BPLAKernel()
+    K, G = gpu_ctx.bpla_gradient_gram(ds, kern, normalize=normalize)
+    n = len(alns)
+    rv, rg = _ref(om, kern, [(i, j) for i in range(n) for j in range(n)])
+    RK, RG = rv.reshape(n, n), rg.reshape(n, n, 4).transpose(2, 0, 1)
+    RK = np.triu(RK) + np.triu(RK, 1).T  # reference evaluates i <= j only
+    RG = np.array([np.triu(g) + np.triu(g, 1).T for g in RG])
+    if normalize:
+        dk, dg = np.diag(RK).copy(), np.array([np.diag(g) for g in RG])
+        sq = np.sqrt(np.outer(dk, dk))
+        NK = RK / sq
+        NG = np.array([RG[l] / sq - NK / 2 * (dg[l][:, None] / dk[:, None] + dg[l][None, :] / dk[None, :])
+                       for l in range(4)])
+        np.fill_diagonal(NK, 1.0)
+        for l in range(4):
+            np.fill_diagonal(NG[l], 0.0)
+        RK, RG = NK, NG
+    assert rel_err(K, RK) < 1e-6
+    for l in range(4):
+        assert np.max(np.abs(G[l] - RG[l])) <= 1e-6 * np.max(np.abs(RG[l])) + 1e-12
