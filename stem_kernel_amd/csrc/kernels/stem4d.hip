@@ -173,10 +173,12 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
     const int kmax = m - d2;
     const int e2 = d2 - 1;
     const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+    const int klo = max(cli, clj - d2), khi = min(min(chi, chj - d2), kmax);
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + 64 * c;
       const int l = k + d2;
+      if (BAND && (64 * c > khi || 64 * c + 63 < klo)) continue;  // whole slot outside
       pbp[c] = 0.0f;
       pGs[c] = 0.0;
       pyl[c] = 0;
@@ -231,8 +233,14 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
       G3n[c] = wave_shl1(G3[c], hg);
     }
     const int kmax = m - d2;
+    // partial DP: the row's cells inside the constraints, k in [klo, khi]
+    const int klo = max(cli, clj - d2), khi = min(min(chi, chj - d2), kmax);
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
+      if (BAND && (64 * c > khi || 64 * c + 63 < klo)) {  // whole slot outside (wave-uniform)
+        K2[c] = G2[c] = K3[c] = G3[c] = 0.0;
+        continue;
+      }
       const int k = k0 + 64 * c;
       if (k <= kmax) {
         const int l = k + d2;
