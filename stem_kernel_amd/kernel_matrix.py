@@ -440,33 +440,11 @@ class Context:
         i <= j, mirrored) or, with normalize, CalcMatrixN (:128-255;
         K/sqrt(K_ii K_jj) and its derivative, diagonal 1 and 0).  Returns
         (K[n, n], G[4, n, n]); one sk_bpla_gradients call over all pairs."""
+        from .shard import assemble_gradients
         n = len(ds)
         iu, ju = np.triu_indices(n)
         val, grad = self.bpla_gradients(ds, kernel, iu, ju)
-        K = np.zeros((n, n))
-        G = np.zeros((4, n, n))
-        if not normalize:
-            K[iu, ju] = val
-            K[ju, iu] = val
-            for l in range(4):
-                G[l, iu, ju] = grad[:, l]
-                G[l, ju, iu] = grad[:, l]
-            return K, G
-        d = iu == ju
-        dk = np.zeros(n)
-        dg = np.zeros((4, n))
-        dk[iu[d]] = val[d]
-        dg[:, iu[d]] = grad[d].T
-        off = ~d
-        i, j = iu[off], ju[off]
-        sq = np.sqrt(dk[i] * dk[j])
-        k = val[off] / sq
-        K[i, j] = K[j, i] = k
-        np.fill_diagonal(K, 1.0)
-        for l in range(4):
-            g = grad[off, l] / sq - k / 2 * (dg[l, i] / dk[i] + dg[l, j] / dk[j])
-            G[l, i, j] = G[l, j, i] = g
-        return K, G
+        return assemble_gradients(iu, ju, val, grad, n, normalize)
 
     def pairs_device(self, ds: Dataset, kernel: _Kernel, x, y, out_ptr: int) -> None:
         self.upload(ds)

@@ -101,3 +101,73 @@ def gpu_compute(ctx, ds, kernel, device):
         return out[: x.size]
 
     return f
+
+
+def assemble_gradients(x, y, val, grad, n: int, normalize: bool = False):
+    """The bpla_optimizer's Gram and gradient matrices from per-pair values
+    and d/d(alpha, beta, gap, ext) of the cells (x[k] <= y[k]) covering the
+    upper triangle: CalcMatrix (bpla_optimizer.cpp:52-126, mirrored) or, with
+    normalize, CalcMatrixN (:128-255: K/sqrt(K_ii K_jj), its derivative,
+    diagonal 1 and 0).  Returns (K[n, n], G[4, n, n])."""
+    x = np.asarray(x)
+    y = np.asarray(y)
+    val = np.asarray(val, dtype=np.float64)
+    grad = np.asarray(grad, dtype=np.float64).reshape(-1, 4)
+    K = np.zeros((n, n))
+    G = np.zeros((4, n, n))
+    if not normalize:
+        K[x, y] = val
+        K[y, x] = val
+        for l in range(4):
+            G[l, x, y] = grad[:, l]
+            G[l, y, x] = grad[:, l]
+        return K, G
+    d = x == y
+    dk = np.zeros(n)
+    dg = np.zeros((4, n))
+    dk[x[d]] = val[d]
+    dg[:, x[d]] = grad[d].T
+    off = ~d
+    i, j = x[off], y[off]
+    sq = np.sqrt(dk[i] * dk[j])
+    k = val[off] / sq
+    K[i, j] = K[j, i] = k
+    np.fill_diagonal(K, 1.0)
+    for l in range(4):
+        g = grad[off, l] / sq - k / 2 * (dg[l, i] / dk[i] + dg[l, j] / dk[j])
+        G[l, i, j] = G[l, j, i] = g
+    return K, G
+
+
+def distributed_gradient_gram(compute, n: int, normalize: bool = False, group=None, device=None):
+    """bpla_optimizer's Gram + gradient matrices over the process group (the
+    reference Bcasts every rank's cells over MPI, bpla_optimizer.cpp:62-104):
+    compute(x, y) returns (values[k], grads[k, 4]) for this rank's cells of
+    the folded row-block plan, then ONE all_gather_into_tensor of equal-sized
+    (cap, 5) buffers; every rank assembles the same matrices."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    x, y = rank_pairs(n, world, rank)
+    cap = max_pairs(n, world)
+    val, grad = compute(x, y)
+    v = torch.as_tensor(np.asarray(val, dtype=np.float64)) if not torch.is_tensor(val) else val
+    g = torch.as_tensor(np.asarray(grad, dtype=np.float64)) if not torch.is_tensor(grad) else grad
+    dev = v.device if device is None else device
+    buf = torch.zeros((cap, 5), dtype=torch.float64, device=dev)
+    buf[: x.size, 0] = v.to(dev)
+    buf[: x.size, 1:] = g.reshape(-1, 4).to(dev)
+    out = torch.empty((world * cap, 5), dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    parts = out.cpu().numpy().reshape(world, cap, 5)
+    xs, ys, vs, gs = [], [], [], []
+    for r in range(world):
+        rx, ry = rank_pairs(n, world, r)
+        xs.append(rx)
+        ys.append(ry)
+        vs.append(parts[r, : rx.size, 0])
+        gs.append(parts[r, : rx.size, 1:])
+    return assemble_gradients(np.concatenate(xs), np.concatenate(ys), np.concatenate(vs),
+                              np.concatenate(gs), n, normalize)

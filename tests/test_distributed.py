@@ -101,3 +101,52 @@ def test_rccl_world1_gpu_compute_matches_gram(gpu_ctx):
     finally:
         dist.destroy_process_group()
     np.testing.assert_allclose(g, ref, rtol=1e-12)
+
+
+def _grad_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import stem_kernel_amd as ska
+    from oracle import pyoracle as po
+    seqs = ska.random_sequences(6, 30, 0x5EED0006)
+    om = [po.OMData([s], [ska.fold(s)], 0.01) for s in seqs]
+    p = ska.BPLAKernel().params
+    t = np.array(list(p.score_table))
+
+    def compute(x, y):
+        r = [po.bpla_gradients(om[a], om[b], p.alpha, p.beta, p.gap, p.ext, t) for a, b in zip(x, y)]
+        return np.array([v for v, _, _ in r]), np.array([d for _, d, _ in r]).reshape(-1, 4)
+
+    K, G = shard.distributed_gradient_gram(compute, len(seqs), normalize=True)
+    dist.destroy_process_group()
+    q.put((rank, (K, G)))
+
+
+def test_gloo_world2_gradient_gram_matches_single_process():
+    """bpla_optimizer's Gram + gradient matrices (f4) over two gloo ranks equal
+    the single-process assembly of the same cells, bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    import stem_kernel_amd as ska
+    from oracle import pyoracle as po
+    seqs = ska.random_sequences(6, 30, 0x5EED0006)
+    om = [po.OMData([s], [ska.fold(s)], 0.01) for s in seqs]
+    p = ska.BPLAKernel().params
+    t = np.array(list(p.score_table))
+    n = len(seqs)
+    x, y = (a.astype(np.int32) for a in np.triu_indices(n))
+    r = [po.bpla_gradients(om[a], om[b], p.alpha, p.beta, p.gap, p.ext, t) for a, b in zip(x, y)]
+    K, G = shard.assemble_gradients(x, y, [v for v, _, _ in r], [d for _, d, _ in r], n, True)
+    for rank in (0, 1):
+        assert np.array_equal(res[rank][0], K) and np.array_equal(res[rank][1], G)
+    assert np.allclose(np.diag(K), 1.0) and np.all(G[:, np.arange(n), np.arange(n)] == 0.0)
