@@ -123,18 +123,6 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
 #define SK_MU 3
 #endif
-#ifndef SK_SW  // IY sweep chunk width in 64-edge groups
-#define SK_SW 2
-#endif
-#ifndef SK_CHUNK_A
-#define SK_CHUNK_A 8
-#endif
-#ifndef SK_CHUNK_G
-#define SK_CHUNK_G 4
-#endif
-#ifndef SK_CHUNK_M
-#define SK_CHUNK_M 4
-#endif
 
 #ifdef SK_STAMPS
 #define STAMP(i)                                                  \
