@@ -59,7 +59,7 @@ stamps:
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o -Wl,-rpath,/opt/rocm/lib
 .PHONY: stamps
 
-# experiment build: make variant NAME=x DEFS="-DSK_CHUNK_A=32 [-DSK_STAMPS]" -> build/libsk_x.so
+# experiment build: make variant NAME=x DEFS="-DSK_PW=3 [-DSK_STAMPS]" -> build/libsk_x.so
 variant:
 	@mkdir -p $(BUILD)/var/$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip -o $(BUILD)/var/$(NAME)/dag_stem.o
