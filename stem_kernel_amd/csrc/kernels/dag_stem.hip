@@ -120,8 +120,8 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_PW  // MATCH pass width in 64-node groups
 #define SK_PW 4
 #endif
-#ifndef SK_SEGSUM  // MATCH: lanes per group whose same-parent runs are summed before the atomic (4 or 16)
-#define SK_SEGSUM 4
+#ifndef SK_SEGSUM  // MATCH: same-parent runs summed per quad before the atomic (0 = off)
+#define SK_SEGSUM 1
 #endif
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
 #define SK_MU 3
@@ -456,40 +456,36 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
               // this round's reads into a branch)
               const double w = g[u] * rv[u] * (ok ? 1.0 : 0.0);
               const int h = ok ? (int)((e[u] >> 11) & 0x7ff) - q0 : lane;
-#if defined(SK_SEGSUM)
-              // Node-major edges put a parent's edges in adjacent lanes: each
-              // run is summed within its group of SK_SEGSUM lanes (DPP shifts,
-              // Hillis-Steele on contiguous keys) and only the run's last lane
-              // in the group issues the atomic.  Lanes past the range carry a
-              // unique negative key, so they neither join a run nor write.
-              const int key = ok ? h : -1 - lane;
-              const int gl = lane & (SK_SEGSUM - 1);
-              double sw = w;
-#define SK_SEG_STEP(N, CTRL)                                                                     \
-  {                                                                                             \
-    const int ks = __builtin_amdgcn_mov_dpp(key, CTRL, 0xf, 0xf, false);                         \
-    const double ws = __hiloint2double(                                                         \
-        __builtin_amdgcn_mov_dpp(__double2hiint(sw), CTRL, 0xf, 0xf, false),                     \
-        __builtin_amdgcn_mov_dpp(__double2loint(sw), CTRL, 0xf, 0xf, false));                    \
-    sw += (gl >= N && ks == key) ? ws : 0.0;                                                    \
-  }
-#if SK_SEGSUM == 4
-              SK_SEG_STEP(1, 0x90)  // quad_perm(0,0,1,2): lane-1
-              SK_SEG_STEP(2, 0x40)  // quad_perm(0,0,0,1): lane-2
-              const int kn = __builtin_amdgcn_mov_dpp(key, 0xF9, 0xf, 0xf, false);  // quad_perm(1,2,3,3)
-#else
-              SK_SEG_STEP(1, 0x111)  // row_shr:1
-              SK_SEG_STEP(2, 0x112)
-              SK_SEG_STEP(4, 0x114)
-              SK_SEG_STEP(8, 0x118)
-              const int kn = __builtin_amdgcn_mov_dpp(key, 0x101, 0xf, 0xf, false);  // row_shl:1
-#endif
-#undef SK_SEG_STEP
-              if (ok && (gl == SK_SEGSUM - 1 || kn != key))
-                __hip_atomic_fetch_add(&hb[h], sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#else
-              __hip_atomic_fetch_add(&hb[h], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#endif
+              if constexpr (SK_SEGSUM && MAXK <= 20) {
+                // Node-major edges put a parent's edges in adjacent lanes:
+                // each run is summed within its quad (DPP quad_perm,
+                // Hillis-Steele on contiguous keys) and only the run's last
+                // lane in the quad issues the atomic.  Lanes past the range
+                // carry a unique negative key, so they neither join a run nor
+                // write.  (Wider classes sit at the register cap: off there.)
+                const int key = ok ? h : -1 - lane;
+                const int ql = lane & 3;
+                double sw = w;
+                {  // lane - 1: quad_perm(0,0,1,2)
+                  const int ks = __builtin_amdgcn_mov_dpp(key, 0x90, 0xf, 0xf, false);
+                  const double ws = __hiloint2double(
+                      __builtin_amdgcn_mov_dpp(__double2hiint(sw), 0x90, 0xf, 0xf, false),
+                      __builtin_amdgcn_mov_dpp(__double2loint(sw), 0x90, 0xf, 0xf, false));
+                  sw += (ql >= 1 && ks == key) ? ws : 0.0;
+                }
+                {  // lane - 2: quad_perm(0,0,0,1)
+                  const int ks = __builtin_amdgcn_mov_dpp(key, 0x40, 0xf, 0xf, false);
+                  const double ws = __hiloint2double(
+                      __builtin_amdgcn_mov_dpp(__double2hiint(sw), 0x40, 0xf, 0xf, false),
+                      __builtin_amdgcn_mov_dpp(__double2loint(sw), 0x40, 0xf, 0xf, false));
+                  sw += (ql >= 2 && ks == key) ? ws : 0.0;
+                }
+                const int kn = __builtin_amdgcn_mov_dpp(key, 0xF9, 0xf, 0xf, false);  // lane + 1
+                if (ok && (ql == 3 || kn != key))
+                  __hip_atomic_fetch_add(&hb[h], sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+              } else {
+                __hip_atomic_fetch_add(&hb[h], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+              }
             }
           }
 #pragma unroll
