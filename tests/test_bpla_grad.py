@@ -95,3 +95,22 @@ def test_bpla_gradient_gram(gpu_ctx, normalize):
     assert rel_err(K, RK) < 1e-6
     for l in range(4):
         assert np.max(np.abs(G[l] - RG[l])) <= 1e-6 * np.max(np.abs(RG[l])) + 1e-12
+
+
+@pytest.mark.gpu
+def test_bpla_gradients_tiny_and_ragged(gpu_ctx):
+    """Edge cases of the per-pair tables: one- and two-column alignments
+    (the gap / extension derivatives are exactly zero there), and pairs whose
+    lengths differ 120-fold, within one batch."""
+    alns = [["A"], ["AC", "A-"], ["GGGAAACCC"], [ska.random_sequences(1, 120, 5)[0]],
+            ["GGGAAAUCC", "GG-AAAUCC", "GGGAAA-CC"]]
+    ds, om = make_examples(alns)
+    kern = ska.BPLAKernel()
+    n = len(alns)
+    x, y = (a.astype(np.int32) for a in np.triu_indices(n))
+    val, grad = gpu_ctx.bpla_gradients(ds, kern, x, y)
+    rv, rg = _ref(om, kern, list(zip(x, y)))
+    assert np.all(np.abs(val / rv - 1) < 1e-6)
+    for p in range(x.size):
+        floor = 1e-12 * np.max(np.abs(rg[p]))
+        assert np.all(np.abs(grad[p] - rg[p]) <= 1e-6 * np.abs(rg[p]) + floor), (x[p], y[p], grad[p], rg[p])
