@@ -278,6 +278,12 @@ int sk_random_sequences(uint64_t *state, int32_t n_seqs, int32_t len, char *out)
  * pairs (non-leaf nodes). */
 int sk_last_timing(const sk_context *ctx, double *stem_ms, double *string_ms,
                    double *cells, int32_t *launches);
+/* Kernel instantiations launched by the last compute call (parity-coverage
+ * diagnostic): *stem_maxk_mask has bit MAXK/4 set for every DAG stem register
+ * class run (MAXK = 4, 8, ..., 32 64-node slots per lane); *stem4d_mask has
+ * bit log2(CPL) set for every 4-D stem class run (CPL = 1, 2, 4, 8 cells per
+ * lane), shifted by 4 for the banded (partial_dp) variant. */
+int sk_last_classes(const sk_context *ctx, uint32_t *stem_maxk_mask, uint32_t *stem4d_mask);
 /* RIBOSUM85-60 tables as compiled into the library (pinning tests). */
 void sk_ribosum_tables(float *s16, float *p256);
 int sk_char2rna(int c);

@@ -82,6 +82,7 @@ SIGNATURES = {
     "sk_fold_synthetic": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, _F64P]),
     "sk_random_sequences": (C.c_int, [C.POINTER(C.c_uint64), C.c_int32, C.c_int32, C.c_char_p]),
     "sk_last_timing": (C.c_int, [_P, _F64P, _F64P, _F64P, _I32P]),
+    "sk_last_classes": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "sk_ribosum_tables": (None, [_F32P, _F32P]),
     "sk_char2rna": (C.c_int, [C.c_int]),
     "sk_bpla_gradients": (C.c_int, [_P, _P, _P, C.POINTER(KernelParams), _I32P, _I32P, C.c_int64,

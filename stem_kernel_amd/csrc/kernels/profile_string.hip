@@ -173,6 +173,12 @@ size_t str_lds_bytes(const StrLaunch& P, int nwaves) {
 }
 
 hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st) {
+  const size_t lds = str_lds_bytes(P, nwaves);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)sk_profile_string_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(sk_profile_string_kernel, dim3(grid), dim3(64 * nwaves),
                      str_lds_bytes(P, nwaves), st, P);
   return hipGetLastError();

@@ -137,6 +137,10 @@ struct sk_context {
   hipEvent_t evf = nullptr, evj = nullptr;
   double last_stem_ms = 0.0, last_str_ms = 0.0, last_cells = 0.0;
   int32_t last_launches = 0;
+  // kernel instantiations the last compute call launched (sk_last_classes):
+  // bit MAXK/4 per DAG stem register class; bit log2(CPL) (+4 when banded)
+  // per 4-D stem class
+  uint32_t last_stem_classes = 0, last_s4d_classes = 0;
 };
 
 namespace {
@@ -932,6 +936,8 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       L.items = Bt.items + ioff[d1];
       L.n_items = ioff[d1 + 1] - ioff[d1];
       SK_HIP(ctx, sk::launch_stem4d(L, cpl, S));
+      if (L.n_items) ctx->last_s4d_classes |= 1u << ((cpl == 1 ? 0 : cpl == 2 ? 1 : cpl == 4 ? 2 : 3) +
+                                                     (L.band_lo ? 4 : 0));
       ++launches;
     }
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
@@ -959,6 +965,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     return fail(ctx, SK_ERR_UNSUPPORTED, "unknown kernel kind");
   ctx->last_stem_ms = ctx->last_str_ms = ctx->last_cells = 0.0;
   ctx->last_launches = 0;
+  ctx->last_stem_classes = ctx->last_s4d_classes = 0;
   if (n == 0) return SK_OK;
   const int nx = (int)xs_->ex.size(), ny = (int)ys_->ex.size();
   for (int64_t k = 0; k < n; ++k)
@@ -1218,6 +1225,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.stamps = d_stamps;
 #endif
       SK_HIP(ctx, sk::launch_stem(SL, C.grid, C.nwaves, S));
+      ctx->last_stem_classes |= 1u << (C.maxk / 4);
     }
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
 #ifdef SK_STAMPS
@@ -1255,9 +1263,12 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     T.out = str_out;
     T.pair_counter = reinterpret_cast<unsigned long long*>(d_ctr + 8);
     T.lds_max_len = (std::max(PY.max_len, 1) + 1) & ~1;
-    const int w = 4;
+    // 4 waves per workgroup while their rows fit 64 KB of LDS, fewer for
+    // longer y (one wave's rows fit the CU's 160 KB up to L ~ 4,000)
+    int w = 4;
+    while (w > 1 && sk::str_lds_bytes(T, w) > 65536) w /= 2;
     const size_t lds = sk::str_lds_bytes(T, w);
-    if (lds > 65536) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for string kernel LDS");
+    if (lds > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for string kernel LDS");
     const int per_cu = std::max(1, std::min<int>((int)(163840 / lds), 8));
     const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (n + w - 1) / w);
     SK_HIP(ctx, hipEventRecord(ctx->ev2, SS));
@@ -1886,6 +1897,13 @@ int sk_last_timing(const sk_context* ctx, double* stem_ms, double* string_ms, do
   if (string_ms) *string_ms = ctx->last_str_ms;
   if (cells) *cells = ctx->last_cells;
   if (launches) *launches = ctx->last_launches;
+  return SK_OK;
+}
+
+int sk_last_classes(const sk_context* ctx, uint32_t* stem_maxk_mask, uint32_t* stem4d_mask) {
+  if (!ctx) return SK_ERR_INVALID;
+  if (stem_maxk_mask) *stem_maxk_mask = ctx->last_stem_classes;
+  if (stem4d_mask) *stem4d_mask = ctx->last_s4d_classes;
   return SK_OK;
 }
 

@@ -496,6 +496,15 @@ class Context:
         self._chk(lib().sk_last_timing(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return dict(stem_ms=a.value, string_ms=b.value, cells=c.value, launches=d.value)
 
+    def last_classes(self):
+        """Kernel instantiations the last compute call launched: the DAG stem
+        register classes (MAXK values) and the 4-D classes as (CPL, banded)."""
+        a, b = C.c_uint32(), C.c_uint32()
+        self._chk(lib().sk_last_classes(self._h, C.byref(a), C.byref(b)))
+        maxk = sorted(4 * k for k in range(32) if a.value >> k & 1)
+        s4d = sorted((1 << (k & 3), bool(k & 4)) for k in range(8) if b.value >> k & 1)
+        return dict(stem_maxk=maxk, stem4d=s4d)
+
 
 def format_libsvm(matrix: np.ndarray, labels: Sequence[str]) -> str:
     m = np.ascontiguousarray(matrix, dtype=np.float64)
