@@ -10,12 +10,17 @@ base-pairing probabilities, --basepair 0.01).  Units are Gram cells K(i,j),
 i <= j, exactly the cells the reference evaluates
 (common/kernel_matrix.cpp:44-55): 8,390,656 sequence pairs.
 
-A *step* is one slice of that upper triangle: the pairs are dealt round-robin
-into S equal slices, so every slice has the same cost mix.  With N GPUs (one
-process per GPU, RCCL), rank r computes slice (step*N + r) -- per-GPU work is
-fixed, so scaling is weak -- and the ranks all-gather the step's Gram entries
-over RCCL (the reference gathered to rank 0 with MPI point-to-point,
-kernel_matrix.cpp:225-261).  --full runs every slice of the Gram once.
+A *step* is one slice of that upper triangle: cell k (row-major i <= j) is in
+slice k % S, so every slice has the same cost mix.  With N GPUs (one process
+per GPU), rank r computes slice (step*N + r) -- per-GPU work is fixed, so
+scaling is weak -- and the ranks all-gather the step's Gram entries with the
+engine's own RCCL communicator (sk_comm_allgather).  S is a multiple of N, so
+rank r's slices are always cells k with k % N == r: the cells the product's
+sharded Gram (sk_gram_sharded, the reference MPI Gram's cyclic plan,
+kernel_matrix.cpp:210-224) gives rank r -- over S/N steps a rank computes
+exactly its share of the shipped plan.  --full times one call of the product
+path itself: sk_gram_sharded over all N ranks (cells, all-gather, host
+assembly of the whole mirrored matrix).
 
 Other SURVEY.md §8 configurations (--config): c2 ss_kernel 256 x L150,
 c3 4-D stem kernel 1024 x L200, c4 BPLA 2048 alignments L~200, c5 DAG stem
@@ -93,7 +98,7 @@ def c4_alignments(n, lo, hi, rows, seed):
 def build_inputs(cfg, a):
     import stem_kernel_amd as ska
     seed = 0x5EED0000 + cfg["cid"]
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     if cfg["kernel"] == "bpla":
         alns = c4_alignments(a.n, cfg["L"][0], cfg["L"][1], cfg["rows"], seed)
         return alns, ska.Dataset.synthetic_alignments(alns, th=0.01, threads=threads)
@@ -138,16 +143,28 @@ def roofline(kind, shapes, x, y, ms):
 
 
 # ------------------------------------------------------------------ CPU baseline
+def host_threads():
+    """Host cores this process may use: its CPU affinity, capped by
+    OMP_NUM_THREADS when set (the GPU box's per-job CPU share)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(cap))) if cap and cap.isdigit() else aff
+
+
 def cpu_baseline(cfg, data, n_pairs, seed=7):
     """The C oracle (plain-C restatement of the reference kernels, oracle/)
-    on a bounded random sample of the same Gram's pairs, host threads."""
+    on a bounded random sample of the same Gram's pairs, host threads.
+    Returns (baseline dict, sampled pairs, oracle values)."""
     from concurrent.futures import ThreadPoolExecutor
 
     import stem_kernel_amd as ska
     from oracle import pyoracle as po
     rng = np.random.default_rng(seed)
     kind = cfg["kernel"]
-    npool = min(len(data), 48)
+    npool = min(len(data), 48 if kind == "stem4d" else 512)
     idx = [int(i) for i in rng.choice(len(data), size=npool, replace=False)]
     kern = make_kernel(kind)
     p = kern.params
@@ -170,16 +187,18 @@ def cpu_baseline(cfg, data, n_pairs, seed=7):
     while len(pairs) < n_pairs:
         a, b = sorted(rng.choice(idx, size=2))
         pairs.append((int(a), int(b)))
-    cores = max(1, min(16, os.cpu_count() or 1))
+    cores = host_threads()
     t = time.perf_counter()
     with ThreadPoolExecutor(cores) as ex:  # ctypes releases the GIL
-        list(ex.map(one, pairs))
+        vals = np.array(list(ex.map(one, pairs)))
     dt = time.perf_counter() - t
     what = {"ss": "SuStemStrKernel", "stem": "SuStemKernel", "stem4d": "4-D StemKernel full_dp",
             "bpla": "BPLAKernel"}[kind]
     return {"value": n_pairs / dt, "unit": "sequence-pairs/sec", "cores": cores, "kind": "port",
+            "host_nproc": os.cpu_count(),
             "sample": f"{n_pairs} random pairs (i<=j) among {npool} of the {len(data)} examples, "
-                      f"{what} via the C oracle on {cores} threads, {dt:.1f}s wall"}
+                      f"{what} via the C oracle on {cores} threads (all host cores this job "
+                      f"may use: affinity capped by OMP_NUM_THREADS), {dt:.1f}s wall"}, pairs, vals
 
 
 # ------------------------------------------------------------------ main
@@ -221,29 +240,38 @@ def main():
     iu, ju = np.triu_indices(a.n)
     iu = iu.astype(np.int32)
     ju = ju.astype(np.int32)
+    # the engine's own RCCL communicator (sk_comm_init; torch only carries
+    # the 128-byte id from rank 0)
+    from stem_kernel_amd import shard
+    if dist_on:
+        shard.rccl_init(ctx)
+    else:
+        import ctypes
+        uid = ctypes.create_string_buffer(128)
+        ska.lib().sk_comm_unique_id(uid, 128)
+        ctx.comm_init(uid.raw, 0, 1)
     S = a.slices
-    n_slices_needed = (a.warmup + a.steps) * world
     if a.full:
-        S = max(world, S)
-        a.steps = -(-S // world)
-        a.warmup = 0
-        n_slices_needed = S
-    if n_slices_needed > S:
-        S = n_slices_needed
+        a.steps, a.warmup = 1, 0
+    n_slices_needed = (a.warmup + a.steps) * world
+    S = max(S, n_slices_needed)
+    S = -(-S // world) * world  # a multiple of N: rank r's slices are cells k % N == r
     slice_of = lambda s: (iu[s::S], ju[s::S])
     per = int(np.ceil(iu.size / S))
-    out = torch.empty(per, dtype=torch.float64, device=dev)
+    out = torch.zeros(per, dtype=torch.float64, device=dev)
     gathered = torch.empty(per * world, dtype=torch.float64, device=dev)
+    full_gram = [None]
 
     def run_step(step):
+        if a.full:  # the product path: sk_gram_sharded over all ranks
+            full_gram[0] = ctx.gram_sharded(ds, kern, normalize=False)
+            x, y = shard.rank_pairs(a.n, world, rank)
+            return x, y, ctx.last_timing()
         sl = step * world + rank
         x, y = slice_of(sl % S)
-        if a.full and sl >= S:
-            x, y = x[:0], y[:0]
         ctx.pairs_device(ds, kern, x, y, out.data_ptr())
         tm = ctx.last_timing()
-        if dist_on:
-            dist.all_gather_into_tensor(gathered, out)
+        ctx.allgather(out.data_ptr(), per, gathered.data_ptr())
         return x, y, tm
 
     for w in range(a.warmup):
@@ -287,18 +315,29 @@ def main():
         ys = np.concatenate([w[1] for w in work])
         bound, ach, unit, peak, model, alg = roofline(kind, shapes, xs, ys, tot_ms)
         n_launch = max(1, int(np.sum(launches)))
-        traffic = None
+        traffic, traffic_src = None, None
         pmc_json = a.pmc_json or os.path.join(ROOT, "profiles", f"{kind}_traffic.json")
         try:
             with open(pmc_json) as f:
                 pm = json.load(f)
             if pm.get("length") == a.length and pm.get("kernel") == kind:
                 traffic = pm["hbm_bytes_per_cell"] * float(np.sum(cells)) / n_launch
+                traffic_src = (f"not measured in this run: {os.path.relpath(pmc_json, ROOT)} "
+                               f"(rocprofv3 FETCH_SIZE/WRITE_SIZE passes, {pm.get('source', '?')}) "
+                               f"bytes per cell x this run's cells per launch")
         except Exception:
             pass
-        cpu = None
+        cpu, parity = None, None
         if not a.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-            cpu = cpu_baseline(cfg, data, a.cpu_pairs)
+            cpu, cpairs, cvals = cpu_baseline(cfg, data, a.cpu_pairs)
+            # the baseline's oracle values double as a parity check of the
+            # benched kernel classes on the same inputs (1e-6 relative)
+            cx = np.array([p[0] for p in cpairs], np.int32)
+            cy = np.array([p[1] for p in cpairs], np.int32)
+            got = ctx.pairs(ds, kern, cx, cy)
+            err = float(np.max(np.abs(got - cvals) / np.maximum(np.abs(cvals), 1e-300)))
+            parity = {"pairs": int(cx.size), "max_rel_err": err, "tol": 1e-6,
+                      "ok": bool(err < 1e-6), "against": "C oracle (cpu_baseline sample)"}
         kname = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
                  "stem4d": "sk_stem4d_kernel", "bpla": "sk_bpla_kernel"}[kind]
         kdesc = {
@@ -327,21 +366,27 @@ def main():
                             f"step = 1/{S} of the {iu.size} upper-triangle pairs per GPU",
                 "n_sequences": a.n, "length": cfg["L"], "pairs_per_step_per_gpu": per,
                 "kernel": kdesc, "basepair_th": 0.01,
-                "parallelism": f"gram-slices x{world} (RCCL all-gather)",
+                "parallelism": f"cyclic cell plan x{world} (sk_comm_allgather, RCCL)"
+                               + (" -- full Gram via sk_gram_sharded" if a.full else ""),
                 "mean_nodes": float(shapes[:, 0].mean()), "mean_edges": float(shapes[:, 1].mean()),
                 "mean_bpfreq": float(shapes[:, 2].mean()),
                 "host_build_s": round(t_build, 2), "upload_s": round(t_upload, 3),
             },
             "roofline": {
                 "bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
-                "traffic": traffic, "kernel": kname,
+                "traffic": traffic, "traffic_source": traffic_src, "kernel": kname,
                 "kernel_ms_per_launch": tot_ms / n_launch, "launches": n_launch,
                 "algorithmic_per_launch": alg / n_launch, "model": model,
             },
             "cpu_baseline": cpu,
+            "parity": parity,
             "cells_per_step": float(np.mean(cells)),
         }
         print(json.dumps(line), flush=True)
+        if parity is not None and not parity["ok"]:
+            print(f"PARITY FAILURE: max relative error {parity['max_rel_err']:.3g} > 1e-6",
+                  file=sys.stderr, flush=True)
+            sys.exit(3)
     if dist_on:
         dist.destroy_process_group()
 

@@ -221,6 +221,38 @@ int sk_test_matrix(sk_context *ctx, sk_dataset *test, sk_dataset *train,
                    const sk_kernel_params *kp, int norm_test, int normalize,
                    double *out, double *self_out);
 
+/* ---------------------------------------------------------------- multi-GPU
+ * One process (or host thread) per GPU, one context each.  The plan is the
+ * reference MPI Gram's: upper-triangle cell k (i <= j, row-major) belongs to
+ * rank k % world (CalcTrainMatrix::operator(), common/kernel_matrix.cpp:
+ * 210-224).  Each rank computes its cells into a device buffer of
+ * sk_shard_count(n, 0, world) doubles, one RCCL all-gather over xGMI joins
+ * them on every rank, and every rank assembles the mirrored (normalised)
+ * matrix -- the reference's Ssend/Recv to rank 0 and its scatter
+ * (:225-261, 495-527).  The result is bit-identical to sk_gram. */
+/* Cells of `rank` (host only, no GPU): count, and their (x, y) lists. */
+int64_t sk_shard_count(int32_t n, int32_t rank, int32_t world);
+int sk_shard_cells(int32_t n, int32_t rank, int32_t world, int32_t *x, int32_t *y);
+/* Host assembly: gathered = world buffers of per_rank doubles (rank-major,
+ * rank r's values in sk_shard_cells order); out = n*n, mirrored, normalised
+ * as kernel_matrix.cpp:560-571 when normalize. */
+int sk_shard_assemble(int32_t n, int32_t world, const double *gathered, int64_t per_rank,
+                      int normalize, double *out);
+/* RCCL communicator of the context: rank 0 calls sk_comm_unique_id and
+ * hands the 128 bytes to every rank (any channel: MPI_Bcast, a file, a
+ * socket); each rank calls sk_comm_init on its own context. */
+int sk_comm_unique_id(uint8_t *id, size_t id_bytes);
+int sk_comm_init(sk_context *ctx, const uint8_t *id, size_t id_bytes, int32_t rank, int32_t world);
+/* ncclAllGather of count doubles per rank on the context's stream
+ * (asynchronous; device buffers, recv_dev holds world*count). */
+int sk_comm_allgather(sk_context *ctx, const double *send_dev, int64_t count, double *recv_dev);
+/* The Gram over the communicator's ranks: every rank passes the same dataset
+ * and parameters and receives the whole n*n matrix in out (host).
+ * Replaces: KernelMatrix<double>::calculate under HAVE_MPI,
+ * common/kernel_matrix.cpp:186-261, 495-527. */
+int sk_gram_sharded(sk_context *ctx, sk_dataset *ds, const sk_kernel_params *kp, int normalize,
+                    double *out);
+
 /* ---------------------------------------------------------------- output */
 /* libsvm precomputed-kernel text: "label 0:(i+1) 1:K_i1 ... n:K_in \n" with
  * ostream default formatting (6 significant digits).  Writes into buf (NUL

@@ -82,6 +82,13 @@ SIGNATURES = {
     "sk_fold_synthetic": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, _F64P]),
     "sk_random_sequences": (C.c_int, [C.POINTER(C.c_uint64), C.c_int32, C.c_int32, C.c_char_p]),
     "sk_last_timing": (C.c_int, [_P, _F64P, _F64P, _F64P, _I32P]),
+    "sk_shard_count": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "sk_shard_cells": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, _I32P, _I32P]),
+    "sk_shard_assemble": (C.c_int, [C.c_int32, C.c_int32, _F64P, C.c_int64, C.c_int, _F64P]),
+    "sk_comm_unique_id": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "sk_comm_init": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_int32, C.c_int32]),
+    "sk_comm_allgather": (C.c_int, [_P, C.c_void_p, C.c_int64, C.c_void_p]),
+    "sk_gram_sharded": (C.c_int, [_P, _P, C.POINTER(KernelParams), C.c_int, _F64P]),
     "sk_last_classes": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "sk_ribosum_tables": (None, [_F32P, _F32P]),
     "sk_char2rna": (C.c_int, [C.c_int]),

@@ -141,7 +141,16 @@ struct sk_context {
   // bit MAXK/4 per DAG stem register class; bit log2(CPL) (+4 when banded)
   // per 4-D stem class
   uint32_t last_stem_classes = 0, last_s4d_classes = 0;
+  // RCCL communicator of sk_comm_init (ncclComm_t, csrc/host/shard.cpp)
+  void* comm = nullptr;
 };
+
+namespace sk {
+hipStream_t ctx_stream(sk_context* ctx) { return ctx->stream; }
+int ctx_device(sk_context* ctx) { return ctx->device; }
+void*& ctx_comm(sk_context* ctx) { return ctx->comm; }
+void comm_destroy(void* comm);
+}  // namespace sk
 
 namespace {
 
@@ -1397,6 +1406,10 @@ int pairs_host(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
 
 }  // namespace
 
+namespace sk {
+int ctx_fail(sk_context* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
+}  // namespace sk
+
 // =================================================================== ABI
 extern "C" {
 
@@ -1488,6 +1501,8 @@ int sk_close(sk_context* ctx) {
   if (!ctx) return SK_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  sk::comm_destroy(ctx->comm);
+  ctx->comm = nullptr;
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->work) (void)hipFree(ctx->work);
   if (ctx->s4d.pairs) (void)hipFree(ctx->s4d.pairs);
@@ -1754,25 +1769,12 @@ int sk_gram(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp, int nor
       xi.push_back(i);
       yi.push_back(j);
     }
-  std::vector<double> v(xi.size());
+  std::vector<double> v(std::max<size_t>(xi.size(), 1));
   int rc = pairs_host(ctx, ds, ds, kp, xi.data(), yi.data(), (int64_t)xi.size(), v.data());
   if (rc) return rc;
-  size_t k = 0;
-  for (int i = 0; i < n; ++i)
-    for (int j = i; j < n; ++j, ++k) {
-      out[(size_t)i * n + j] = v[k];
-      if (i != j) out[(size_t)j * n + i] = v[k];
-    }
-  if (normalize && n > 0) {
-    // kernel_matrix.cpp:560-571
-    for (int i = 0; i + 1 < n; ++i)
-      for (int j = i + 1; j < n; ++j) {
-        out[(size_t)i * n + j] /= std::sqrt(out[(size_t)i * n + i] * out[(size_t)j * n + j]);
-        out[(size_t)j * n + i] = out[(size_t)i * n + j];
-      }
-    for (int i = 0; i < n; ++i) out[(size_t)i * n + i] = 1;
-  }
-  return SK_OK;
+  // mirror + normalise (kernel_matrix.cpp:560-571): the one-rank case of the
+  // sharded assembly (csrc/host/shard.cpp), so both give the same bits
+  return sk_shard_assemble(n, 1, v.data(), (int64_t)v.size(), normalize, out);
 }
 
 int sk_test_row(sk_context* ctx, sk_dataset* test, int t, sk_dataset* train,

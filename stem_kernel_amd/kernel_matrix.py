@@ -446,6 +446,27 @@ class Context:
         val, grad = self.bpla_gradients(ds, kernel, iu, ju)
         return assemble_gradients(iu, ju, val, grad, n, normalize)
 
+    def comm_init(self, uid: bytes, rank: int, world: int) -> None:
+        """This context's RCCL communicator (sk_comm_init); uid = the 128
+        bytes rank 0 drew with sk_comm_unique_id (see shard.rccl_init)."""
+        self._chk(lib().sk_comm_init(self._h, uid, len(uid), rank, world))
+
+    def allgather(self, send_ptr: int, count: int, recv_ptr: int) -> None:
+        """ncclAllGather of `count` doubles per rank on the context's stream
+        (sk_comm_allgather; device pointers)."""
+        self._chk(lib().sk_comm_allgather(self._h, send_ptr, count, recv_ptr))
+
+    def gram_sharded(self, ds: Dataset, kernel: _Kernel, normalize: bool = False) -> np.ndarray:
+        """The Gram over this context's communicator (sk_gram_sharded): the
+        reference MPI Gram's cyclic cell plan, one RCCL all-gather, the whole
+        matrix on every rank (common/kernel_matrix.cpp:186-261, 495-527)."""
+        self.upload(ds)
+        n = len(ds)
+        out = np.zeros((n, n), dtype=np.float64)
+        self._chk(lib().sk_gram_sharded(self._h, ds.handle, C.byref(kernel.params),
+                                        int(normalize), out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
     def pairs_device(self, ds: Dataset, kernel: _Kernel, x, y, out_ptr: int) -> None:
         self.upload(ds)
         x = np.ascontiguousarray(x, dtype=np.int32)

@@ -1,75 +1,78 @@
-"""Multi-GPU Gram sharding (one process per GPU, torch.distributed / RCCL).
+"""Multi-GPU Gram sharding (one process per GPU).
 
-Every Gram cell K(i,j), i <= j, is independent (common/kernel_matrix.cpp:44-55),
-so the upper triangle is partitioned with no data-path collective: rank g
-takes the row blocks g and 2P-1-g of 2P equal row blocks (folding equalises
-the triangle area), computes its cells, and ONE all-gather of equal-sized
-buffers assembles the matrix on every rank.  The reference dealt cells
-cyclically to MPI ranks and gathered to rank 0 point-to-point
-(common/kernel_matrix.cpp:186-261, 495-527).
+Every Gram cell K(i,j), i <= j, is independent (common/kernel_matrix.cpp:44-55).
+The plan is the reference MPI Gram's: upper-triangle cell k (row-major) goes
+to rank k % P (CalcTrainMatrix::operator(), common/kernel_matrix.cpp:210-224),
+which gives every rank the same cost mix.  Each rank computes its cells into
+an equal-sized buffer, ONE all-gather joins the buffers on every rank, and
+every rank assembles the mirrored, normalised matrix (the reference's
+Ssend/Recv to rank 0 and replayed scatter, :225-261, 495-527).  Plan and
+assembly are the C ABI's (sk_shard_cells / sk_shard_assemble,
+csrc/host/shard.cpp), so a C++ host and this module produce the same bits.
 
-The partition is a pure function of (n, world), so the N-GPU Gram is
-bit-identical to the 1-GPU Gram.
+Two transports:
+
+* ``gram_rccl`` -- the product path: the engine's own RCCL communicator
+  (sk_comm_init), its cells written into a device buffer and all-gathered by
+  sk_gram_sharded inside the library; torch.distributed only hands the
+  128-byte RCCL id from rank 0 to the others.
+* ``distributed_gram`` -- any torch.distributed backend (gloo on CPU for the
+  multi-process tests, nccl = RCCL on GPUs) with a caller-supplied compute.
+
+The plan is a pure function of (n, world) and values depend only on the pair,
+so the N-GPU Gram is bit-identical to the 1-GPU Gram.
 """
 from __future__ import annotations
 
-import math
+import ctypes as C
 from typing import Callable, Tuple
 
 import numpy as np
 
+from ._lib import check, lib
 
-def folded_row_blocks(n: int, world: int, rank: int) -> np.ndarray:
-    """Rows owned by `rank`: blocks rank and 2*world-1-rank of 2*world."""
-    nb = 2 * world
-    edges = [round(n * b / nb) for b in range(nb + 1)]
-    rows = []
-    for b in (rank, nb - 1 - rank):
-        rows.extend(range(edges[b], edges[b + 1]))
-    return np.array(sorted(set(rows)), dtype=np.int32)
+
+def shard_count(n: int, world: int, rank: int) -> int:
+    """Cells of `rank` (sk_shard_count)."""
+    return int(lib().sk_shard_count(n, rank, world))
 
 
 def rank_pairs(n: int, world: int, rank: int) -> Tuple[np.ndarray, np.ndarray]:
-    """Upper-triangle cells (i <= j) of the rows `rank` owns, row-major."""
-    rows = folded_row_blocks(n, world, rank)
-    xs, ys = [], []
-    for i in rows:
-        xs.append(np.full(n - i, i, np.int32))
-        ys.append(np.arange(i, n, dtype=np.int32))
-    if not xs:
-        return np.zeros(0, np.int32), np.zeros(0, np.int32)
-    return np.concatenate(xs), np.concatenate(ys)
+    """Upper-triangle cells (i <= j) of `rank`, in cell order (sk_shard_cells)."""
+    m = shard_count(n, world, rank)
+    x = np.zeros(max(m, 1), np.int32)
+    y = np.zeros(max(m, 1), np.int32)
+    check(lib().sk_shard_cells(n, rank, world, x.ctypes.data_as(C.POINTER(C.c_int32)),
+                               y.ctypes.data_as(C.POINTER(C.c_int32))))
+    return x[:m], y[:m]
 
 
 def max_pairs(n: int, world: int) -> int:
-    return max(rank_pairs(n, world, r)[0].size for r in range(world))
+    """Equal buffer size of the all-gather: rank 0 has the most cells."""
+    return max(shard_count(n, world, 0), 1)
 
 
 def assemble(parts, n: int, world: int, normalize: bool = False) -> np.ndarray:
-    """Scatter every rank's values into the mirrored n x n matrix and
-    normalise as KernelMatrix::calculate does (kernel_matrix.cpp:560-571)."""
-    m = np.zeros((n, n), dtype=np.float64)
+    """Scatter the ranks' buffers (parts[r][:count_r]) into the mirrored n x n
+    matrix and normalise as KernelMatrix::calculate does
+    (kernel_matrix.cpp:560-571), through sk_shard_assemble."""
+    per = max_pairs(n, world)
+    g = np.zeros((world, per), np.float64)
     for r in range(world):
-        x, y = rank_pairs(n, world, r)
-        v = np.asarray(parts[r])[: x.size]
-        m[x, y] = v
-        m[y, x] = v
-    if normalize and n > 0:
-        out = m.copy()
-        for i in range(n - 1):
-            for j in range(i + 1, n):
-                out[i, j] = m[i, j] / math.sqrt(m[i, i] * m[j, j])
-                out[j, i] = out[i, j]
-        np.fill_diagonal(out, 1.0)
-        m = out
-    return m
+        v = np.asarray(parts[r], dtype=np.float64).ravel()
+        c = shard_count(n, world, r)
+        g[r, :c] = v[:c]
+    out = np.zeros((n, n), np.float64)
+    check(lib().sk_shard_assemble(n, world, g.ctypes.data_as(C.POINTER(C.c_double)), per,
+                                  int(normalize), out.ctypes.data_as(C.POINTER(C.c_double))))
+    return out
 
 
 def distributed_gram(compute: Callable[[np.ndarray, np.ndarray], "object"], n: int,
                      normalize: bool = False, group=None, device=None) -> np.ndarray:
-    """Gram over the default process group: compute(x, y) returns this rank's
-    values (a torch tensor on `device`, or host array for CPU/gloo), then one
-    all_gather_into_tensor of padded, equal-sized buffers."""
+    """Gram over a torch.distributed group: compute(x, y) returns this rank's
+    values (a torch tensor on `device`, or a host array), then one
+    all_gather_into_tensor of equal-sized buffers."""
     import torch
     import torch.distributed as dist
 
@@ -85,13 +88,35 @@ def distributed_gram(compute: Callable[[np.ndarray, np.ndarray], "object"], n: i
     buf[: x.size] = vals.to(dev)
     out = torch.empty(cap * world, dtype=torch.float64, device=dev)
     dist.all_gather_into_tensor(out, buf, group=group)
-    parts = out.cpu().numpy().reshape(world, cap)
-    return assemble(parts, n, world, normalize)
+    return assemble(out.cpu().numpy().reshape(world, cap), n, world, normalize)
+
+
+def rccl_init(ctx, group=None) -> None:
+    """Give `ctx` its own RCCL communicator over the ranks of a
+    torch.distributed group: rank 0 draws the id (sk_comm_unique_id), the
+    group broadcasts the 128 bytes, every rank calls sk_comm_init."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    obj = [None]
+    if rank == 0:
+        buf = C.create_string_buffer(128)
+        check(lib().sk_comm_unique_id(buf, 128))
+        obj[0] = buf.raw
+    dist.broadcast_object_list(obj, src=0, group=group)
+    ctx.comm_init(obj[0], rank, world)
+
+
+def gram_rccl(ctx, ds, kernel, normalize: bool = False) -> np.ndarray:
+    """The sharded Gram through the engine (sk_gram_sharded): every rank
+    passes the same dataset and gets the whole matrix."""
+    return ctx.gram_sharded(ds, kernel, normalize)
 
 
 def gpu_compute(ctx, ds, kernel, device):
     """compute() for distributed_gram: the HIP engine writing straight into a
-    device buffer (no host round trip before the RCCL all-gather)."""
+    device buffer (no host round trip before the all-gather)."""
     import torch
 
     def f(x, y):
@@ -143,8 +168,8 @@ def distributed_gradient_gram(compute, n: int, normalize: bool = False, group=No
     """bpla_optimizer's Gram + gradient matrices over the process group (the
     reference Bcasts every rank's cells over MPI, bpla_optimizer.cpp:62-104):
     compute(x, y) returns (values[k], grads[k, 4]) for this rank's cells of
-    the folded row-block plan, then ONE all_gather_into_tensor of equal-sized
-    (cap, 5) buffers; every rank assembles the same matrices."""
+    the cyclic plan, then ONE all_gather_into_tensor of equal-sized (cap, 5)
+    buffers; every rank assembles the same matrices."""
     import torch
     import torch.distributed as dist
 

@@ -1,8 +1,10 @@
 """Multi-process path on CPU: world_size-2 gloo over 127.0.0.1.
 
-The shard plan must cover the upper triangle exactly once, and the gathered,
-mirrored, normalised Gram must equal the single-process one (the compute
-function is the oracle here; on GPUs it is stem_kernel_amd.shard.gpu_compute).
+The shard plan (the reference MPI Gram's cyclic cell deal, sk_shard_cells)
+must cover the upper triangle exactly once, and the gathered, mirrored,
+normalised Gram must equal the single-process one bit for bit (the compute
+function is the oracle here; on GPUs it is the engine: sk_gram_sharded over
+its own RCCL communicator, or shard.gpu_compute).
 """
 import os
 import socket
@@ -23,8 +25,48 @@ def test_plan_covers_triangle_once(n, world):
         np.add.at(seen, (x, y), 1)
     assert np.array_equal(seen, np.triu(np.ones((n, n), int)))
     sizes = [shard.rank_pairs(n, world, r)[0].size for r in range(world)]
-    if n >= 8 * world:
-        assert max(sizes) / min(sizes) < 1.35  # folding balances the triangle
+    assert max(sizes) - min(sizes) <= 1  # cyclic deal: equal shares
+    # the reference's order: cell k of the row-major triangle to rank k % P
+    # (common/kernel_matrix.cpp:210-224)
+    iu, ju = np.triu_indices(n)
+    for r in range(world):
+        x, y = shard.rank_pairs(n, world, r)
+        assert np.array_equal(x, iu[r::world]) and np.array_equal(y, ju[r::world])
+
+
+def test_assemble_matches_reference_normalisation():
+    """sk_shard_assemble (threaded) against a literal restatement of
+    kernel_matrix.cpp:560-571, bit for bit, at a size where the host threads
+    split the rows."""
+    import math
+    rng = np.random.default_rng(3)
+    n, world = 600, 3
+    iu, ju = np.triu_indices(n)
+    vals = rng.uniform(0.5, 2.0, iu.size)
+    parts = [vals[r::world] for r in range(world)]
+    got = shard.assemble(parts, n, world, normalize=True)
+    m = np.zeros((n, n))
+    m[iu, ju] = vals
+    m[ju, iu] = vals
+    ref = m.copy()
+    for i in range(0, n - 1, 37):  # sampled rows of the reference's loop
+        for j in range(i + 1, n):
+            ref[i, j] = m[i, j] / math.sqrt(m[i, i] * m[j, j])
+        assert np.array_equal(got[i, i + 1:], ref[i, i + 1:])
+    assert np.all(np.diag(got) == 1.0) and np.array_equal(got, got.T)
+    raw = shard.assemble(parts, n, world, normalize=False)
+    assert np.array_equal(raw, m)
+
+
+def test_assemble_n8192_under_a_second():
+    import time
+    n, world = 8192, 8
+    per = shard.max_pairs(n, world)
+    parts = [np.ones(per) for _ in range(world)]
+    t = time.perf_counter()
+    out = shard.assemble(parts, n, world, normalize=True)
+    assert time.perf_counter() - t < 1.0 * max(1, 8 // (os.cpu_count() or 8))
+    assert out[0, 1] == 1.0
 
 
 def _free_port():
@@ -81,9 +123,10 @@ def test_gloo_world2_matches_single_process():
 
 
 @pytest.mark.gpu
-def test_rccl_world1_gpu_compute_matches_gram(gpu_ctx):
-    """The RCCL path (nccl backend, one rank) through the HIP engine writing
-    straight into the device buffer that is all-gathered."""
+def test_rccl_world1_matches_gram_bit_for_bit(gpu_ctx):
+    """Both RCCL paths at world 1 -- the engine's own communicator
+    (sk_gram_sharded) and torch's nccl backend around gpu_compute -- give
+    sk_gram's bits."""
     import torch
     import torch.distributed as dist
     import stem_kernel_amd as ska
@@ -98,9 +141,32 @@ def test_rccl_world1_gpu_compute_matches_gram(gpu_ctx):
     try:
         g = shard.distributed_gram(shard.gpu_compute(gpu_ctx, ds, kern, dev), len(seqs),
                                    normalize=True)
+        shard.rccl_init(gpu_ctx)
+        g2 = shard.gram_rccl(gpu_ctx, ds, kern, normalize=True)
     finally:
         dist.destroy_process_group()
-    np.testing.assert_allclose(g, ref, rtol=1e-12)
+    assert np.array_equal(g, ref)
+    assert np.array_equal(g2, ref)
+
+
+@pytest.mark.gpu
+def test_pair_values_independent_of_batch(gpu_ctx):
+    """A cell's value depends only on its pair, not on which other cells share
+    the launch or their order -- what makes the N-GPU Gram equal the 1-GPU
+    one bit for bit."""
+    import stem_kernel_amd as ska
+
+    seqs = ska.random_sequences(12, 200, 0x5EED0002)
+    ds = ska.Dataset.synthetic(seqs, th=0.01, threads=4)
+    kern = ska.SuStemStrKernel()
+    iu, ju = (a.astype(np.int32) for a in np.triu_indices(len(seqs)))
+    full = gpu_ctx.pairs(ds, kern, iu, ju)
+    perm = np.random.default_rng(1).permutation(iu.size)
+    shuf = gpu_ctx.pairs(ds, kern, iu[perm], ju[perm])
+    assert np.array_equal(shuf, full[perm])
+    for r in range(3):
+        part = gpu_ctx.pairs(ds, kern, iu[r::3], ju[r::3])
+        assert np.array_equal(part, full[r::3])
 
 
 def _grad_worker(rank, world, port, q):
