@@ -127,8 +127,8 @@ int sk_dataset_free(sk_dataset *ds);
  * p(i,j), 0<=i<j<n_r, at i*n_r - i*(i+1)/2 + (j-i-1).  This is the matrix
  * Vienna pf_fold would give the reference (common/bpmatrix.cpp:151-177).
  * th = --basepair.  use_bp = 0 builds MData(ma) (no DAG; string kernels only).
- * Replaces: new MData(ma, th, pf_scale, opts)  stem_kernel_lite/data.cpp:466-487
- * and DataLoader<MData>::get()  stem_kernel_lite/data.cpp:689-728. */
+ * Replaces: new MData(ma, th, pf_scale, opts)  stem_kernel_lite/data.cpp:324-345
+ * and DataLoader<MData>::get()  stem_kernel_lite/data.cpp:548-586. */
 int sk_dataset_add(sk_dataset *ds, const char *label, int n_rows,
                    const char *const *rows, const double *const *bpp_rows,
                    float th, int use_bp);

@@ -5,14 +5,14 @@
  *   ProfileSequence            common/profile.cpp:9-89
  *   char2rna                   common/rna.cpp:173-231
  *   BPMatrix averaging         common/bpmatrix.cpp:292-342, 399-417
- *   Profiler                   stem_kernel_lite/data.cpp:175-274
- *   DAGBuilder                 stem_kernel_lite/data.cpp:283-449
- *   find_root/find_max_parent  stem_kernel_lite/data.cpp:538-577
- *   fill_weight                stem_kernel_lite/data.cpp:579-595
- *   StemKernel::operator()     stem_kernel_lite/stem_kernel.cpp:49-130
- *   Simple/SubstNodeScore      stem_kernel_lite/score_table.cpp:193-232, 297-380
- *   SimpleEdgeScore            stem_kernel_lite/score_table.cpp:235-280
- *   StringKernel (profile)     stem_kernel_lite/string_kernel.cpp:46-168
+ *   Profiler                   stem_kernel_lite/data.cpp:33-132
+ *   DAGBuilder                 stem_kernel_lite/data.cpp:141-307
+ *   find_root/find_max_parent  stem_kernel_lite/data.cpp:396-435
+ *   fill_weight                stem_kernel_lite/data.cpp:437-453
+ *   StemKernel::operator()     stem_kernel_lite/stem_kernel.cpp:14-95
+ *   Simple/SubstNodeScore      stem_kernel_lite/score_table.cpp:14-53, 297-380
+ *   SimpleEdgeScore            stem_kernel_lite/score_table.cpp:56-101
+ *   StringKernel (profile)     stem_kernel_lite/string_kernel.cpp:10-132
  *   StringKernel (naive)       string_kernel/string_kernel.cpp:11-50
  * Loop orders and float/double intermediates follow the reference so that the
  * oracle reproduces its rounding; build with -ffp-contract=off.
@@ -61,7 +61,7 @@ void orc_ribosum_tables(float *s16, float *p256) {
   memcpy(p256, SK_RIBOSUM_P, sizeof(SK_RIBOSUM_P));
 }
 
-/* ProfileSequence::add_sequence(string, w=1) (profile.cpp:647-665) */
+/* ProfileSequence::add_sequence(string, w=1) (profile.cpp:55-73) */
 static void profile_add(float *prof5, int len, const char *s, float *n_seqs) {
   for (int i = 0; i != len; ++i) {
     int r = orc_char2rna((unsigned char)s[i]);
@@ -90,7 +90,7 @@ static double bpm_get(const bpmat *m, int i1, int j1) {
 }
 
 /* ------------------------------------------------------------------ */
-/* Profiler: stem_kernel_lite/data.cpp:175-274 */
+/* Profiler: stem_kernel_lite/data.cpp:33-132 */
 typedef struct {
   const char *seq;
   int len;           /* aligned length (seq_.size()) */
@@ -116,11 +116,11 @@ static void profiler_init(profiler *P, const char *seq, int len,
     P->idx[i] = NONE;
     P->nbp[i] = 1.0f;
   }
-  /* make_idxmap (data.cpp:226-234): GAP is '-' for std::string */
+  /* make_idxmap (data.cpp:84-92): GAP is '-' for std::string */
   uint32_t j = 0;
   for (int i = 0; i != len; ++i)
     if (seq[i] != '-') P->idx[i] = j++;
-  /* non_bp_profile (data.cpp:236-265) */
+  /* non_bp_profile (data.cpp:94-123) */
   if (bpm->n != len) {
     for (int i = 0; i != len; ++i) {
       if (P->idx[i] != NONE) {
@@ -256,7 +256,7 @@ typedef struct {
   orc_mdata *d;
 } dagbuilder;
 
-/* DAGBuilder::initialize (data.cpp:307-333) */
+/* DAGBuilder::initialize (data.cpp:165-191) */
 static void dag_initialize(dagbuilder *B) {
   int sz = B->sz;
   size_t ncell = (size_t)sz * (sz + 1) / 2;
@@ -335,7 +335,7 @@ static uint32_t tree_push(orc_mdata *d, const onode *n) {
 
 static uint32_t dag_build_helper(dagbuilder *B, uint32_t a, uint32_t b);
 
-/* make_loop (data.cpp:342-353) */
+/* make_loop (data.cpp:200-211) */
 static void dag_make_loop(dagbuilder *B, uint32_t a, uint32_t b) {
   onode nd;
   memset(&nd, 0, sizeof(nd));
@@ -347,11 +347,11 @@ static void dag_make_loop(dagbuilder *B, uint32_t a, uint32_t b) {
   nd.edges = (oedge *)malloc(sizeof(oedge));
   nd.n_edges = 1;
   nd.edges[0].to = ret;
-  nd.edges[0].gaps = b - a - 1; /* Edge(to, p_pos): dag.h:183-187 */
+  nd.edges[0].gaps = b - a - 1; /* Edge(to, p_pos): dag.h:29-33 */
   B->vt[cyk((int)a, (int)b)] = tree_push(B->d, &nd);
 }
 
-/* make_stem (data.cpp:355-371) */
+/* make_stem (data.cpp:213-229) */
 static void dag_make_stem(dagbuilder *B, uint32_t a, uint32_t b) {
   const plist cur = B->bp[cyk((int)a, (int)b)];
   onode nd;
@@ -365,13 +365,13 @@ static void dag_make_stem(dagbuilder *B, uint32_t a, uint32_t b) {
   for (int k = 0; k != cur.n; ++k) {
     uint32_t ret = dag_build_helper(B, cur.a[k], cur.b[k]);
     nd.edges[k].to = ret;
-    /* Edge(to, p_pos, c_pos): dag.h:176-181 */
+    /* Edge(to, p_pos, c_pos): dag.h:22-27 */
     nd.edges[k].gaps = (cur.a[k] - a - 1) + (b - cur.b[k] - 1);
   }
   B->vt[cyk((int)a, (int)b)] = tree_push(B->d, &nd);
 }
 
-/* build_helper (data.cpp:373-386) */
+/* build_helper (data.cpp:231-244) */
 static uint32_t dag_build_helper(dagbuilder *B, uint32_t a, uint32_t b) {
   if (B->vt[cyk((int)a, (int)b)] == NONE) {
     if (a == b) {
@@ -445,12 +445,12 @@ orc_mdata *orc_mdata_new(int n_rows, const char *const *rows,
   B.vt = (uint32_t *)malloc(sizeof(uint32_t) * (ncell ? ncell : 1));
   B.d = d;
   dag_initialize(&B);
-  /* build (data.cpp:293-302): heads of each i in reverse push order */
+  /* build (data.cpp:151-160): heads of each i in reverse push order */
   for (int i = 0; i != L; ++i)
     for (int k = B.head[i].n - 1; k >= 0; --k)
       dag_build_helper(&B, B.head[i].a[k], B.head[i].b[k]);
 
-  /* find_root (data.cpp:538-560) */
+  /* find_root (data.cpp:396-418) */
   char *is_root = (char *)malloc(d->n_nodes ? d->n_nodes : 1);
   memset(is_root, 1, d->n_nodes);
   for (int i = 0; i != d->n_nodes; ++i)
@@ -462,7 +462,7 @@ orc_mdata *orc_mdata_new(int n_rows, const char *const *rows,
   for (int i = 0; i != d->n_nodes; ++i)
     if (is_root[i]) d->root[c++] = (uint32_t)i;
   free(is_root);
-  /* find_max_parent (data.cpp:562-577) */
+  /* find_max_parent (data.cpp:420-435) */
   d->max_pa = (uint32_t *)malloc(sizeof(uint32_t) * (d->n_nodes ? d->n_nodes : 1));
   for (int i = 0; i != d->n_nodes; ++i) d->max_pa[i] = NONE;
   for (int i = 0; i != d->n_nodes; ++i)
@@ -470,7 +470,7 @@ orc_mdata *orc_mdata_new(int n_rows, const char *const *rows,
       uint32_t t = d->tree[i].edges[e].to;
       if (d->max_pa[t] == NONE || d->max_pa[t] < (uint32_t)i) d->max_pa[t] = (uint32_t)i;
     }
-  /* fill_weight (data.cpp:579-595) */
+  /* fill_weight (data.cpp:437-453) */
   d->weight = (float *)malloc(sizeof(float) * (L ? L : 1));
   for (int i = 0; i != L; ++i) {
     float v = 0.0f, t = 0.0f;
@@ -564,7 +564,7 @@ void orc_mdata_bpp(const orc_mdata *d, double *packed) {
 }
 
 /* ------------------------------------------------------------------ */
-/* StemKernel<ST,MData>::operator() (stem_kernel_lite/stem_kernel.cpp:49-130)
+/* StemKernel<ST,MData>::operator() (stem_kernel_lite/stem_kernel.cpp:14-95)
  * with SubstScoreTable (subst=1) or SimpleScoreTable (subst=0). */
 typedef struct {
   int subst;
@@ -575,7 +575,7 @@ typedef struct {
 } stem_params;
 
 static double *gap_powers(double gap, int n) {
-  /* SimpleEdgeScore::initialize (score_table.cpp:239-256): g[k]=g[k-1]*gap */
+  /* SimpleEdgeScore::initialize (score_table.cpp:60-77): g[k]=g[k-1]*gap */
   double *g = (double *)malloc(sizeof(double) * (n > 1 ? n : 1));
   g[0] = 1.0;
   for (int k = 1; k < n; ++k) g[k] = g[k - 1] * gap;
@@ -677,7 +677,7 @@ double orc_su_stem(const orc_mdata *x, const orc_mdata *y, double loop_gap,
   S.subst = 1;
   S.gap = loop_gap;
   S.band = band;
-  /* SubstNodeScore ctor (score_table.cpp:297-313) */
+  /* SubstNodeScore ctor (score_table.cpp:118-134) */
   for (int k = 0; k != 256; ++k) S.co_subst[k] = exp(SK_RIBOSUM_P[k] * beta);
   return stem_dp(&S, x, y);
 }

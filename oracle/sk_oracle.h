@@ -29,13 +29,13 @@ extern "C" {
 
 typedef struct orc_mdata orc_mdata;
 
-/* MData ctor (stem_kernel_lite/data.cpp:466-487) for one example of n_rows
+/* MData ctor (stem_kernel_lite/data.cpp:324-345) for one example of n_rows
  * aligned rows (equal length).  bpp_rows[r] is the base-pairing-probability
  * matrix of row r AFTER erase_gap (length n_r = #non-gap chars), packed as the
  * strict upper triangle, row-major: p(i,j), 0<=i<j<n_r at
  * index i*n_r - i*(i+1)/2 + (j-i-1).  (Stands for Vienna pf_fold output,
  * common/bpmatrix.cpp:166-173.)  th = --basepair threshold.
- * use_bp=0 gives MData(ma) (no DAG, empty weight; data.cpp:489-494). */
+ * use_bp=0 gives MData(ma) (no DAG, empty weight; data.cpp:347-352). */
 orc_mdata *orc_mdata_new(int n_rows, const char *const *rows,
                          const double *const *bpp_rows, float th, int use_bp);
 void orc_mdata_free(orc_mdata *d);
@@ -55,7 +55,7 @@ void orc_mdata_edges(const orc_mdata *d, uint32_t *to, uint32_t *gaps);
 void orc_mdata_bpfreq(const orc_mdata *d, uint32_t *code, float *p);
 int orc_mdata_n_roots(const orc_mdata *d);
 void orc_mdata_roots(const orc_mdata *d, uint32_t *roots);
-/* per-position weight (fill_weight, data.cpp:579-595) and profile columns
+/* per-position weight (fill_weight, data.cpp:437-453) and profile columns
  * (ProfileSequence, common/profile.cpp) float[L][5], n_seqs */
 void orc_mdata_weight(const orc_mdata *d, float *w);
 void orc_mdata_profile(const orc_mdata *d, float *prof5, float *n_seqs);
@@ -65,15 +65,15 @@ void orc_mdata_profile(const orc_mdata *d, float *prof5, float *n_seqs);
 void orc_mdata_bpp(const orc_mdata *d, double *packed);
 
 /* ---- kernels: each returns K(x,y) with x = row example, y = column ---- */
-/* StemKernel<SubstScoreTable> (stem_kernel_lite/stem_kernel.cpp:49-130,
- * score_table.cpp:297-380) == SuStemKernel(loop_gap, beta, band) */
+/* StemKernel<SubstScoreTable> (stem_kernel_lite/stem_kernel.cpp:14-95,
+ * score_table.cpp:118-201) == SuStemKernel(loop_gap, beta, band) */
 double orc_su_stem(const orc_mdata *x, const orc_mdata *y, double loop_gap,
                    double beta, unsigned band);
 /* StemKernel<SimpleScoreTable> == SiStemKernel(loop_gap, stack, covar, band)
- * (def_kernel.h:238-260, score_table.cpp:193-232) */
+ * (def_kernel.h:11-33, score_table.cpp:14-53) */
 double orc_si_stem(const orc_mdata *x, const orc_mdata *y, double loop_gap,
                    double stack, double covar, unsigned band);
-/* StringKernel<double,MData> (stem_kernel_lite/string_kernel.cpp:46-168):
+/* StringKernel<double,MData> (stem_kernel_lite/string_kernel.cpp:10-132):
  * ribosum=1 -> ctor(gap, alpha); ribosum=0 -> ctor(gap, match, mismatch) */
 double orc_profile_string(const orc_mdata *x, const orc_mdata *y, double gap,
                           int ribosum, double alpha, double match,

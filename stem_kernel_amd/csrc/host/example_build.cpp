@@ -1,10 +1,10 @@
 // Host preprocessing for one example: profile, averaged bp matrix, per-row
 // unpaired probabilities and the stem DAG.  Restates the reference's
-//   MData(ma, th, pf_scale, opts)   stem_kernel_lite/data.cpp:466-487
-//   Profiler                        stem_kernel_lite/data.cpp:175-274
-//   DAGBuilder                      stem_kernel_lite/data.cpp:283-449
-//   find_root / find_max_parent     stem_kernel_lite/data.cpp:538-577
-//   fill_weight                     stem_kernel_lite/data.cpp:579-595
+//   MData(ma, th, pf_scale, opts)   stem_kernel_lite/data.cpp:324-345
+//   Profiler                        stem_kernel_lite/data.cpp:33-132
+//   DAGBuilder                      stem_kernel_lite/data.cpp:141-307
+//   find_root / find_max_parent     stem_kernel_lite/data.cpp:396-435
+//   fill_weight                     stem_kernel_lite/data.cpp:437-453
 //   average_matrix                  common/bpmatrix.cpp:306-342
 // with the same float/double intermediates, so node order, edge order,
 // node weights and bp frequencies come out bit-identical.  Unlike the
@@ -116,7 +116,7 @@ class DagBuilder {
  private:
   static size_t cell(int i, int j) { return (size_t)j * (j + 1) / 2 + (size_t)i; }
 
-  // Bottom-up scan of the bp matrix (DAGBuilder::initialize, data.cpp:307-333).
+  // Bottom-up scan of the bp matrix (DAGBuilder::initialize, data.cpp:165-191).
   // cand[i] holds ch(i, j) for the current column j, prev[i] ch(i, j-1).
   void scan() {
     head_.assign(n_, PosList());
@@ -191,7 +191,7 @@ class DagBuilder {
   }
 
   // post-order construction (build_helper / make_leaf / make_loop / make_stem,
-  // data.cpp:335-386); returns the node id of (a, b).
+  // data.cpp:193-244); returns the node id of (a, b).
   uint32_t visit(uint32_t a, uint32_t b) {
     uint32_t& slot = visit_[cell((int)a, (int)b)];
     if (slot != kNone) return slot;

@@ -19,7 +19,7 @@ struct Example {
   // ProfileSequence of all rows (common/profile.cpp): [len][5], n_seqs
   std::vector<float> prof5;
   float n_seqs = 0.f;
-  // fill_weight (data.cpp:579-595)
+  // fill_weight (data.cpp:437-453)
   std::vector<float> pos_weight;
   // averaged bp matrix over the aligned length (packed strict upper)
   std::vector<double> bpp;
@@ -38,7 +38,7 @@ struct Example {
 };
 
 // Builds an Example from aligned rows and per-row (gap-erased) bpp matrices.
-// Restates MData(ma, th, ...) (stem_kernel_lite/data.cpp:466-487).
+// Restates MData(ma, th, ...) (stem_kernel_lite/data.cpp:324-345).
 void build_example(Example& ex, int n_rows, const char* const* rows,
                    const double* const* bpp_rows, float th, bool use_bp);
 

@@ -1,7 +1,7 @@
 // DAG stem-kernel DP on CDNA4 (gfx950).
 //
-// Reference: StemKernel<ST,MData>::operator()  stem_kernel_lite/stem_kernel.cpp:49-130
-// with SubstNodeScore / SimpleNodeScore / SimpleEdgeScore  score_table.cpp:193-380.
+// Reference: StemKernel<ST,MData>::operator()  stem_kernel_lite/stem_kernel.cpp:14-95
+// with SubstNodeScore / SimpleNodeScore / SimpleEdgeScore  score_table.cpp:14-201.
 //
 // Reformulation (exact in real arithmetic):
 //   * The reference carries four tables K0,G0 (|Vx|x|Vy|) and K1,G1 (rows).
@@ -140,7 +140,7 @@ __device__ __forceinline__ void wave_sync() {
 #define STAMP(i) do {} while (0)
 #endif
 
-// node_score(xx,yy,i,j): score_table.cpp:343-380 (Subst) / 193-232 (Simple);
+// node_score(xx,yy,i,j): score_table.cpp:162-201 (Subst) / 193-232 (Simple);
 // co[] holds exp(beta*ribosum) or the match/mismatch table.
 // General case (several bp-freq entries or gap columns; rare): the y
 // entries are read from HBM.
@@ -504,10 +504,10 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
             H = (xloop ? xeg0 : xSL) * gl_v[j];
           double vs;
           if (x_one && (ndc >> 24) != 0u) {
-            // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:350-364)
+            // co[a][b][c][d]*cx*cy, no gap columns (score_table.cpp:171-185)
             vs = co_v[j] * xpf * (double)__uint_as_float(nd[j].w);
           } else {
-            // general bp-frequency lists / gap columns (score_table.cpp:343-380)
+            // general bp-frequency lists / gap columns (score_table.cpp:162-201)
             const int qq = on ? q : top;
             vs = H != 0.0 ? match_node_score(co, s, xbb, xb0, xnbf, ys, Y, ys.yn_b[Y.nb + qq] >> 16,
                                              nda >> 24, xwg, gap2 * (double)__uint_as_float(nd[j].z),

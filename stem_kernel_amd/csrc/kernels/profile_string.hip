@@ -1,7 +1,7 @@
 // Profile string-alignment kernel on CDNA4 (gfx950).
 //
 // Reference: StringKernel<double,MData>::operator()
-//   stem_kernel_lite/string_kernel.cpp:102-168 (DP), :81-100 (subst_score),
+//   stem_kernel_lite/string_kernel.cpp:66-132 (DP), :81-100 (subst_score),
 //   ctors :46-70 (exp(alpha*ribosum_s) or match/mismatch).
 //
 // Systolic schedule: one wavefront per (x,y) pair; lane l owns DP row

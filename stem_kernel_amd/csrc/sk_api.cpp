@@ -587,7 +587,7 @@ int32_t combine_mode(int k) {
 }
 
 std::vector<double> gap_powers(double g, int n) {
-  // SimpleEdgeScore::initialize (score_table.cpp:239-256): g[k] = g[k-1]*gap
+  // SimpleEdgeScore::initialize (score_table.cpp:60-77): g[k] = g[k-1]*gap
   std::vector<double> v(std::max(n, 1));
   v[0] = 1.0;
   for (int k = 1; k < n; ++k) v[k] = v[k - 1] * g;
@@ -707,7 +707,7 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
 }
 
 // 4-D stem kernel: per example, the lowercased sequence (the loader's
-// ToLower, common/example.cpp:29-36) and BPMat::prob(a, b) for a <= b by
+// ToLower, common/example.cpp:26-34) and BPMat::prob(a, b) for a <= b by
 // diagonal e = b - a (prob(a,a) = 0), as float (stem_kernel.cpp:320, 328).
 void stem4d_tables(const Example& X, const sk_kernel_params* kp, std::vector<float>& bp,
                    std::vector<uint8_t>& chr) {

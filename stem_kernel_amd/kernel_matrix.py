@@ -8,7 +8,7 @@ Names, argument meaning and defaults follow the reference:
   ``stem_kernel_lite/ss_kernel.h`` (StemStrKernel == SuStemStrKernel);
 * ``Dataset`` -- the ExampleSet of (label, MData) that ``App::load_examples``
   builds (``common/framework.h:308-353``; ``MData`` ctor
-  ``stem_kernel_lite/data.cpp:466-487``);
+  ``stem_kernel_lite/data.cpp:324-345``);
 * ``KernelMatrix`` -- ``common/kernel_matrix.h:13-108``: ``calculate`` (train
   Gram / test x train), ``calculate_row`` (test row), ``diagonal``, ``print``.
 
@@ -105,7 +105,7 @@ class _Kernel:
 
 
 class SuStemKernel(_Kernel):
-    """SuStemKernel(loop_gap, beta, len_band)  def_kernel.h:262-283 (--no-string)."""
+    """SuStemKernel(loop_gap, beta, len_band)  def_kernel.h:35-57 (--no-string)."""
     kind = _lib.SU_STEM
 
     def __init__(self, loop_gap=0.2, beta=0.3, len_band=10):
@@ -113,7 +113,7 @@ class SuStemKernel(_Kernel):
 
 
 class SiStemKernel(_Kernel):
-    """SiStemKernel(loop_gap, stack, covar, len_band)  def_kernel.h:238-260."""
+    """SiStemKernel(loop_gap, stack, covar, len_band)  def_kernel.h:11-33."""
     kind = _lib.SI_STEM
 
     def __init__(self, loop_gap=0.2, stack=1.3, covar=0.8, len_band=10):
@@ -135,7 +135,7 @@ class StringKernel(_Kernel):
 
 
 class SuStemStrKernel(_Kernel):
-    """SuStemStrKernel(alpha, beta, loop_gap, gap, len_band)  def_kernel.h:313-338;
+    """SuStemStrKernel(alpha, beta, loop_gap, gap, len_band)  def_kernel.h:86-111;
     identical to StemStrKernel<SubstScoreTable> of ss_kernel.h:9-38."""
     kind = _lib.SU_STEM_STR
 
@@ -204,7 +204,7 @@ class StemKernel4D(_Kernel):
 
 class SiStemStrKernel(_Kernel):
     """SiStemStrKernel(loop_gap, stack, covar, gap, match, mismatch, len_band)
-    def_kernel.h:285-311 (--no-ribosum)."""
+    def_kernel.h:58-84 (--no-ribosum)."""
     kind = _lib.SI_STEM_STR
 
     def __init__(self, loop_gap=0.2, stack=1.3, covar=0.8, gap=0.8, match=1.0, mismatch=0.8,
@@ -214,7 +214,7 @@ class SiStemStrKernel(_Kernel):
 
 
 class LSuStemKernel(_Kernel):
-    """LSuStemKernel: beta*log(K_stem)  def_kernel.h:340-364 (--log --no-string)."""
+    """LSuStemKernel: beta*log(K_stem)  def_kernel.h:113-138 (--log --no-string)."""
     kind = _lib.LSU_STEM
 
     def __init__(self, loop_gap=0.2, beta=0.3, len_band=10):
@@ -222,7 +222,7 @@ class LSuStemKernel(_Kernel):
 
 
 class LSuStemStrKernel(_Kernel):
-    """LSuStemStrKernel: beta*log K_stem + alpha*log K_str  def_kernel.h:392-417 (--log)."""
+    """LSuStemStrKernel: beta*log K_stem + alpha*log K_str  def_kernel.h:165-190 (--log)."""
     kind = _lib.LSU_STEM_STR
 
     def __init__(self, alpha=0.2, beta=0.3, loop_gap=0.2, gap=0.8, len_band=10):

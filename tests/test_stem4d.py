@@ -5,7 +5,7 @@ Parity anchors: the reference's CLI default without Vienna runs
 NormalBasePair with bp_bound 1.0, which makes every kernel value 1
 (SURVEY.md §8c probe anchor); the -p path (bp_model 0) uses the dataset's
 base-pairing probabilities.  Sequences are lowercased as the reference loader
-does (common/example.cpp:29-36)."""
+does (common/example.cpp:26-34)."""
 import numpy as np
 import pytest
 
