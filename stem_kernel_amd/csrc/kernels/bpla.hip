@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(256) sk_bpla_kernel(BplaLaunch P) {
       const int owner = Lx == 0 ? 0 : ((Lx - 1) & 63);
       r = (Lx == 0 || Ly == 0) ? 1.0 : __shfl(result, owner, 64);
     }
-    if (lane == 0) P.out[pr] = r;
+    if (lane == 0) P.out[P.oidx ? P.oidx[pr] : (int64_t)pr] = r;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -253,6 +253,296 @@ size_t bpla_lds_bytes(const BplaLaunch& P, int nwaves) {
 hipError_t launch_bpla(const BplaLaunch& P, int grid, int nwaves, hipStream_t st) {
   hipLaunchKernelGGL(sk_bpla_kernel, dim3(grid), dim3(64 * nwaves), bpla_lds_bytes(P, nwaves), st,
                      P);
+  return hipGetLastError();
+}
+
+// ===========================================================================
+// Fast path for pairs whose profile columns are all dyadic (every entry a
+// multiple of 1/256: single sequences and alignments of 1, 2, 4, 8, ... rows,
+// IUPAC codes included).  There LAScore's float weight is n = xs * ys exactly
+// (dyadic_sum), so v / n = sum_l (u_l / xs) (y_l / ys): the per-position
+// factors are tabulated once per call (sk_bpla_tab_kernel) and a cell costs
+// four FMAs instead of 16 products and an FP64 divide.  Two identities of the
+// reference recurrences remove work per cell:
+//   - X2/Y2 only sum M: X2[i][j] = sum_{i'<i} M[i'][j] and Y2[i][j] =
+//     sum_{j'<j} (M[i][j'] + X2[i][j']), so 1 + X2[n][m] + Y2[n][m] + M[n][m]
+//     = 1 + sum over all cells of M (bpla_kernel.cpp:104-114): each lane sums
+//     its cells and one wave reduction ends the pair;
+//   - exp(beta * s) by a table-driven reduction (2^(j/64) in LDS) and a
+//     degree-5 Taylor polynomial (relative error ~1e-16), no special-case
+//     handling (|beta * s| stays far from the double range).
+// The sums run in another order than the reference's (all terms positive,
+// ~1e-15 relative); the score keeps the reference's float products
+// (BPLAScore, bpla_kernel.cpp:55-60).  A lane's next strip row is prefetched
+// from the operand table one strip ahead; the per-wave LDS holds the y
+// columns and the strip boundary row only (72 B per column).
+
+__global__ void __launch_bounds__(256) sk_bpla_tab_kernel(const float4* __restrict__ prof,
+                                                          const float4* __restrict__ lru,
+                                                          int64_t n, const double* __restrict__ tb,
+                                                          BplaPos* __restrict__ xrole,
+                                                          BplaPos* __restrict__ yrole) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const float4 c = prof[p];
+  const float4 w = lru[p];
+  const float s = dyadic_sum(c);
+  BplaPos X, Y;
+  const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const double u = tb[l] * (double)c.x + tb[4 + l] * (double)c.y + tb[8 + l] * (double)c.z +
+                     tb[12 + l] * (double)c.w;
+    X.v[l] = s > 0.0f ? u / (double)s : 0.0;
+    Y.v[l] = s > 0.0f ? (double)cv[l] / (double)s : 0.0;
+  }
+  X.pr = Y.pr = w.y;
+  X.pl = Y.pl = w.x;
+  X.pu = Y.pu = w.z;
+  X.dyadic = Y.dyadic = s >= 0.0f ? 1.0f : 0.0f;
+  xrole[p] = X;
+  yrole[p] = Y;
+}
+
+hipError_t launch_bpla_tab(const float4* prof, const float4* lru, int64_t n, const double* table,
+                           BplaPos* xrole, BplaPos* yrole, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sk_bpla_tab_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     prof, lru, n, table, xrole, yrole);
+  return hipGetLastError();
+}
+
+// exp(x), |x| << 700: x = (64m + j) ln2/64 + r, |r| <= ln2/128, e^r by its
+// Taylor series to degree 5 (truncation < 4e-17 relative), times 2^(j/64)
+// from an LDS table, times 2^m.
+__device__ __forceinline__ double fast_exp(double x, const double* etab, const double (&ec)[4]) {
+  const double k = __builtin_rint(x * 92.332482616893657);  // 64 / ln2
+  const int ki = (int)k;
+  double r = __builtin_fma(-k, 1.0830424693267560e-02, x);  // ln2/64, high part (exact k*hi)
+  r = __builtin_fma(-k, 2.9815858269852933e-12, r);         // ln2/64, low part
+  double p = ec[0];
+  p = __builtin_fma(p, r, ec[1]);
+  p = __builtin_fma(p, r, ec[2]);
+  p = __builtin_fma(p, r, ec[3]);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  return __builtin_amdgcn_ldexp(etab[ki & 63] * p, ki >> 6);
+}
+
+// 2^(j/64), j < 64, into the workgroup's exp table (first kBplaExpLds bytes)
+__device__ __forceinline__ void fill_exp_table(double* etab) {
+  if (threadIdx.x < 64) etab[threadIdx.x] = exp2((double)threadIdx.x / 64.0);
+  __syncthreads();
+}
+
+// One pair on one wavefront: ycol holds y's operand columns (LDS), bnd is the
+// wave's boundary row; returns K in every lane.
+template <bool SW, bool BP>
+__device__ __forceinline__ double bpla_fast_pair(const BplaLaunch& P, int x, int y,
+                                                 const BplaPos* ycol, double* bnd,
+                                                 const double* etab, int lane) {
+  const double alpha = P.alpha, beta = P.beta, gap = P.gap, ext = P.ext;
+  const double bg = P.beta_gap, be = P.beta_ext;
+  const int Lx = __builtin_amdgcn_readfirstlane(P.xset.ex_len[x]);
+  const int Ly = __builtin_amdgcn_readfirstlane(P.yset.ex_len[y]);
+  const int xpb = __builtin_amdgcn_readfirstlane(P.xset.ex_pos_base[x]);
+  const int Lys = max(Ly, 64);
+  for (int j = lane; j < 3 * (Lys + 1); j += 64) bnd[j] = 0.0;  // row 0
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nstrips = (Lx + 63) / 64;
+  int j = 1 - lane, i = lane + 1;
+  // byte offset of y column j-1 in ycol (advances with j)
+  unsigned yofs = (unsigned)(j - 1) * (unsigned)sizeof(BplaPos);
+  const char* ybase = reinterpret_cast<const char*>(ycol);
+  bool row_ok = i <= Lx;
+  // my row's operands and the next strip's (prefetched from the table)
+  BplaPos xr = P.xtab[xpb + (row_ok ? i - 1 : 0)];
+  BplaPos xnext = P.xtab[xpb + (i + 64 <= Lx ? i + 63 : 0)];
+  double lM = 0.0, lX = 0.0, lY = 0.0;  // (i, j-1): my previous output
+  double acc = 0.0;                      // sum of my M cells (exp) / max (SW)
+  // one step: d* = (i-1, j-1) received a step earlier; u* receives (i-1, j)
+  auto step = [&](double& dM, double& dX, double& dY, double& uM, double& uX, double& uY) {
+    // lane 0 takes row i-1 from the boundary row; row 0 is zero, and a
+    // strip's boundary column is written 63 steps before lane 0 reads it
+    const int jb = __builtin_amdgcn_readfirstlane(j);
+    const double* bj = bnd + 3 * (jb >= 1 && jb <= Ly ? jb : 0);
+    uM = wave_shr1(lM, bj[0]);
+    uX = wave_shr1(lX, bj[1]);
+    uY = wave_shr1(lY, bj[2]);
+    if (j >= 1 && j <= Ly) {
+      const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+      double s = xr.v[0] * yc.v[0];
+      s = __builtin_fma(xr.v[1], yc.v[1], s);
+      s = __builtin_fma(xr.v[2], yc.v[2], s);
+      s = __builtin_fma(xr.v[3], yc.v[3], s);
+      if (BP) {
+        // BPLAScore (bpla_kernel.cpp:55-60): float products as written
+        const float pp = __fadd_rn(__fmul_rn(xr.pr, yc.pr), __fmul_rn(xr.pl, yc.pl));
+        const float uu = __fmul_rn(xr.pu, yc.pu);
+        s = alpha * (double)pp + (double)uu * s;
+      }
+      const bool c1 = j == 1;  // column 0 is zero
+      double nM, nX, nY;
+      if (!SW) {
+        nM = fast_exp(beta * s, etab, P.ec) * (1.0 + dX + dY + dM);
+        nX = bg * uM + be * uX;
+        nY = c1 ? 0.0 : bg * (lM + lX) + be * lY;
+        if (row_ok) acc += nM;
+      } else {
+        nM = fmax(fmax(fmax(0.0, dM), dX), dY) + s;
+        nX = fmax(uM + gap, uX + ext);
+        // column 0 is zero: max(0 + gap, 0 + gap, 0 + ext)
+        nY = c1 ? fmax(gap, ext) : fmax(fmax(lM + gap, lX + gap), lY + ext);
+        if (row_ok) acc = fmax(acc, nM);
+      }
+      lM = nM;
+      lX = nX;
+      lY = nY;
+      if (lane == 63) {
+        double* bw = bnd + 3 * j;
+        bw[0] = nM;
+        bw[1] = nX;
+        bw[2] = nY;
+      }
+    }
+    yofs += (unsigned)sizeof(BplaPos);
+    if (++j > Lys) {  // next strip: row i + 64, column 1
+      j = 1;
+      yofs = 0;
+      i += 64;
+      row_ok = i <= Lx;
+      xr = xnext;
+      if (i + 64 <= Lx) xnext = P.xtab[xpb + i + 63];
+      uM = uX = uY = 0.0;
+    }
+  };
+  double aM = 0.0, aX = 0.0, aY = 0.0, bM_ = 0.0, bX_ = 0.0, bY_ = 0.0;
+  const int T = (nstrips - 1) * Lys + ((Lx - 1) & 63) + Ly;
+  int t = 0;
+  for (; t + 1 < T; t += 2) {  // two steps, the d/u roles alternate
+    step(aM, aX, aY, bM_, bX_, bY_);
+    step(bM_, bX_, bY_, aM, aX, aY);
+  }
+  if (t < T) step(aM, aX, aY, bM_, bX_, bY_);
+  double r;
+  if (SW) {
+    for (int off = 32; off > 0; off >>= 1) acc = fmax(acc, __shfl_xor(acc, off, 64));
+    r = acc;
+  } else {
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    r = 1.0 + acc;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return r;
+}
+
+// Pairs dealt one per wave: each wave stages its own y columns.
+template <bool SW, bool BP>
+__global__ void __launch_bounds__(256) sk_bpla_fast_kernel(BplaLaunch P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int maxlen = P.lds_max_len;  // even, >= 64
+  double* etab = reinterpret_cast<double*>(smem);
+  unsigned char* wbase = smem + kBplaExpLds + (size_t)wave * bpla_fast_wave_lds_bytes(maxlen);
+  BplaPos* ycol = reinterpret_cast<BplaPos*>(wbase);
+  double* bnd = reinterpret_cast<double*>(ycol + maxlen);
+  fill_exp_table(etab);
+  // the wave's next pair: lane 0 draws, the value goes through SGPRs
+  auto next_pair = [&]() {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(P.pair_counter, 1ull);
+    return (int64_t)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+                     (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v));
+  };
+  for (int64_t pr = next_pair(); pr < P.n_pairs; pr = next_pair()) {
+    const int x = __builtin_amdgcn_readfirstlane(P.xs[pr]);
+    const int y = __builtin_amdgcn_readfirstlane(P.ys[pr]);
+    const int Ly = P.yset.ex_len[y], ypb = P.yset.ex_pos_base[y];
+    for (int j = lane; j < Ly; j += 64) ycol[j] = P.ytab[ypb + j];
+    const double r = bpla_fast_pair<SW, BP>(P, x, y, ycol, bnd, etab, lane);
+    if (lane == 0) P.out[P.oidx ? P.oidx[pr] : (int64_t)pr] = r;
+  }
+}
+
+// Pairs grouped by y into items {first, count} of one y: a workgroup stages
+// the y columns once in LDS for all its waves, and its waves take the item's
+// pairs from an LDS counter.  Per wave only the boundary row (24 B per
+// column), so 16 waves fit a CU.
+template <bool SW, bool BP>
+__global__ void __launch_bounds__(512) sk_bpla_fast_items_kernel(BplaLaunch P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwaves = blockDim.x >> 6;
+  const int maxlen = P.lds_max_len;
+  double* etab = reinterpret_cast<double*>(smem);
+  int* sh = reinterpret_cast<int*>(smem + kBplaExpLds);  // [0] item, [1] in-item counter
+  BplaPos* ycol = reinterpret_cast<BplaPos*>(smem + kBplaExpLds + 16);
+  double* bnd = reinterpret_cast<double*>(ycol + maxlen) + (size_t)wave * 3 * (maxlen + 2);
+  fill_exp_table(etab);
+  for (;;) {
+    if (threadIdx.x == 0) {
+      sh[0] = (int)atomicAdd(P.pair_counter, 1ull);
+      sh[1] = 0;
+    }
+    __syncthreads();
+    const int it = __builtin_amdgcn_readfirstlane(sh[0]);
+    if (it >= P.n_items) break;
+    const int2 item0 = P.items[it];
+    const int2 item = make_int2(__builtin_amdgcn_readfirstlane(item0.x),
+                                __builtin_amdgcn_readfirstlane(item0.y));
+    const int y = __builtin_amdgcn_readfirstlane(P.ys[item.x]);
+    const int Ly = P.yset.ex_len[y], ypb = P.yset.ex_pos_base[y];
+    for (int j = threadIdx.x; j < Ly; j += blockDim.x) ycol[j] = P.ytab[ypb + j];
+    __syncthreads();
+    // the wave's next pair of the item: lane 0 draws, through an SGPR
+    auto next_k = [&]() {
+      int v = 0;
+      if (lane == 0) v = atomicAdd(&sh[1], 1);
+      return __builtin_amdgcn_readfirstlane(v);
+    };
+    for (int k = next_k(); k < item.y; k = next_k()) {
+      const int64_t pr = (int64_t)item.x + k;
+      const int x = __builtin_amdgcn_readfirstlane(P.xs[pr]);
+      const double r = bpla_fast_pair<SW, BP>(P, x, y, ycol, bnd, etab, lane);
+      if (lane == 0) P.out[P.oidx ? P.oidx[pr] : pr] = r;
+    }
+    (void)nwaves;
+    __syncthreads();
+  }
+}
+
+hipError_t launch_bpla_fast(const BplaLaunch& P, int grid, int nwaves, hipStream_t st) {
+  const bool items = P.items != nullptr;
+  const size_t lds = items ? bpla_items_lds_bytes(P.lds_max_len, nwaves)
+                           : kBplaExpLds + (size_t)nwaves * bpla_fast_wave_lds_bytes(P.lds_max_len);
+#define SK_BF(K, A, B)                                                                       \
+  do {                                                                                       \
+    hipError_t e = hipFuncSetAttribute((const void*)K<A, B>,                                 \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    if (e != hipSuccess) return e;                                                           \
+    hipLaunchKernelGGL((K<A, B>), dim3(grid), dim3(64 * nwaves), lds, st, P);                \
+  } while (0)
+#define SK_BF2(K)                      \
+  if (P.sw) {                          \
+    if (P.bp) SK_BF(K, true, true);    \
+    else SK_BF(K, true, false);        \
+  } else {                             \
+    if (P.bp) SK_BF(K, false, true);   \
+    else SK_BF(K, false, false);       \
+  }
+  if (items) {
+    SK_BF2(sk_bpla_fast_items_kernel)
+  } else {
+    SK_BF2(sk_bpla_fast_kernel)
+  }
+#undef SK_BF2
+#undef SK_BF
   return hipGetLastError();
 }
 

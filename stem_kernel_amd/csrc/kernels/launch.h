@@ -48,8 +48,27 @@ struct StrLaunch {
   int32_t lds_max_len = 0;
 };
 
+// Per-position BPLA score operands, computed per call by sk_bpla_tab_kernel
+// (dyadic profile columns only, see bpla.hip): x role v = u_l / xs with
+// u_l = sum_k table[k][l] x_k, y role v = y_l / ys, so LAScore = sum_l
+// v_x[l] v_y[l]; pr, pl, pu: sqrt p_right, p_left, p_unpair.
+struct BplaPos {
+  double v[4];
+  float pr, pl, pu, dyadic;
+};
+static_assert(sizeof(BplaPos) == 48, "BplaPos is three 16-B loads");
+
 struct BplaLaunch {
   DevSet xset, yset;
+  const BplaPos* xtab = nullptr;  // fast kernel: x-role operands by x position
+  const BplaPos* ytab = nullptr;  // fast kernel: y-role operands by y position
+  const int64_t* oidx = nullptr;  // out[oidx[k]] = K(pair k) (nullptr: out[k])
+  // fast kernel, grouped by y: items {first pair, count} of pairs sharing y
+  const int2* items = nullptr;
+  int32_t n_items = 0;
+  // fast kernel's exp: Taylor coefficients 1/5!, 1/4!, 1/3!, 1/2! (kernel
+  // arguments, so they sit in SGPRs as FMA addends)
+  double ec[4] = {8.3333333333333332e-03, 4.1666666666666664e-02, 1.6666666666666666e-01, 0.5};
   const double* table = nullptr;  // 16: score table (x residue major)
   double alpha = 0.0, beta = 0.0, gap = 0.0, ext = 0.0;
   double beta_gap = 0.0, beta_ext = 0.0;  // exp(beta*gap), exp(beta*ext)
@@ -153,8 +172,24 @@ int stem_maxk(int max_nl);
 size_t str_lds_bytes(const StrLaunch& P, int nwaves);
 hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st);
 
+// fast kernels: a workgroup's LDS starts with the exp table 2^(j/64), j < 64
+constexpr size_t kBplaExpLds = 64 * 8;
+// grouped fast kernel: exp table | shared y columns | per wave boundary row
+__host__ __device__ inline size_t bpla_items_lds_bytes(int maxlen, int nwaves) {
+  return kBplaExpLds + 16 + (size_t)maxlen * sizeof(BplaPos) + (size_t)nwaves * 3 * (maxlen + 2) * 8;
+}
 size_t bpla_lds_bytes(const BplaLaunch& P, int nwaves);
 hipError_t launch_bpla(const BplaLaunch& P, int grid, int nwaves, hipStream_t st);
+// dyadic-profile fast path: per-call operand tables, then the DP
+hipError_t launch_bpla_tab(const float4* prof, const float4* lru, int64_t n, const double* table,
+                           BplaPos* xrole, BplaPos* yrole, hipStream_t st);
+// per-wave LDS of the fast kernel: y columns (BplaPos, maxlen) | boundary
+// row {M, X, Y} [maxlen + 2]
+__host__ __device__ inline size_t bpla_fast_wave_lds_bytes(int maxlen) {
+  const size_t b = (size_t)maxlen * sizeof(BplaPos) + (size_t)3 * (maxlen + 2) * 8;
+  return (b + 15) & ~(size_t)15;
+}
+hipError_t launch_bpla_fast(const BplaLaunch& P, int grid, int nwaves, hipStream_t st);
 
 hipError_t launch_combine(const double* stem, const double* str, double* out, int64_t n,
                           int32_t mode, double alpha, double beta, hipStream_t st);

@@ -69,6 +69,8 @@ float4 bpla_weight(const Example& X, int i) {
 struct HostPack {
   std::vector<int32_t> ex_nl, ex_node_base, ex_edge_base, ex_bpf_base, ex_lvl_base, ex_nlev,
       ex_len, ex_pos_base, ex_has_w;
+  // every profile entry of the example a multiple of 1/256 (BPLA fast path)
+  std::vector<uint8_t> ex_dyadic;
   std::vector<float> ex_nseqs;
   std::vector<uint32_t> nd_a, nd_b, nd_c;
   std::vector<float> nd_w, nd_nbp;
@@ -544,6 +546,15 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       P.pos_chr.push_back((uint8_t)X.rows[0][i]);
     }
     for (int i = 0; i < X.len; ++i) P.pos_lru.push_back(bpla_weight(X, i));
+    {
+      bool dy = true;  // the device's dyadic_sum test (bpla.hip), in host float
+      for (int i = 0; i < X.len; ++i)
+        for (int k = 0; k < 4; ++k) {
+          const float v = X.prof5[(size_t)i * 5 + k] * 256.0f;
+          dy = dy && v == std::rint(v);
+        }
+      P.ex_dyadic.push_back(dy ? 1 : 0);
+    }
     P.ex_node_base.push_back((int32_t)P.nd_a.size());
     P.ex_edge_base.push_back((int32_t)P.ed.size());
     P.ex_bpf_base.push_back((int32_t)P.bpf_code.size());
@@ -658,19 +669,86 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
     cells += (double)ex.len * (double)ey.len;
   }
   ctx->last_cells = cells;
+  const HostPack& PX = xs_->pack;
   const HostPack& PY = ys_->pack;
+  // pairs whose profiles are all dyadic take the fast kernel (tabulated
+  // LAScore factors); the rest the general one.  Fast pairs first, the
+  // permutation undone through oidx.
+  std::vector<int32_t> px, py;
+  std::vector<int64_t> oidx;
+  int64_t n_fast = 0;
+  const bool general_only = std::getenv("SK_BPLA_GENERAL") != nullptr;  // A/B switch
+  auto is_fast = [&](int64_t k) {
+    return !general_only && PX.ex_dyadic[x[k]] && PY.ex_dyadic[y[k]];
+  };
+  for (int64_t k = 0; k < n; ++k) n_fast += is_fast(k);
+  // fast pairs grouped by y (a workgroup stages one y for all its waves)
+  // when the y's repeat enough; else one pair per wave
+  constexpr int kItemWaves = 8;
+  std::vector<int2> items;
+  {
+    std::vector<int32_t> ycnt;
+    int64_t distinct = 0;
+    ycnt.assign(ys_->ex.size(), 0);
+    for (int64_t k = 0; k < n; ++k)
+      if (is_fast(k) && ycnt[y[k]]++ == 0) ++distinct;
+    const bool group = n_fast >= 4 * kItemWaves * std::max<int64_t>(distinct, 1) &&
+                       !std::getenv("SK_BPLA_NO_ITEMS");
+    const bool permute = n_fast != n || group;
+    if (permute && n_fast) {
+      px.reserve(n);
+      py.reserve(n);
+      oidx.reserve(n);
+      std::vector<int64_t> fast;
+      fast.reserve(n_fast);
+      for (int64_t k = 0; k < n; ++k)
+        if (is_fast(k)) fast.push_back(k);
+      if (group) std::stable_sort(fast.begin(), fast.end(), [&](int64_t a, int64_t b) { return y[a] < y[b]; });
+      for (int64_t k : fast) {
+        px.push_back(x[k]);
+        py.push_back(y[k]);
+        oidx.push_back(k);
+      }
+      for (int64_t k = 0; k < n; ++k)
+        if (!is_fast(k)) {
+          px.push_back(x[k]);
+          py.push_back(y[k]);
+          oidx.push_back(k);
+        }
+      if (group)  // runs of one y, at most 16 pairs per wave
+        for (int64_t a = 0; a < n_fast;) {
+          int64_t b = a;
+          while (b < n_fast && py[b] == py[a] && b - a < 16 * kItemWaves) ++b;
+          items.push_back(make_int2((int)a, (int)(b - a)));
+          a = b;
+        }
+      x = px.data();
+      y = py.data();
+    }
+  }
+  const bool permute = !oidx.empty();
   const size_t nb = (size_t)n;
-  int rc = ensure_work(ctx, 16 * 8 + nb * 8 + 2048);
+  const size_t npx = PX.pos_prof.size(), npy = ys_ == xs_ ? 0 : PY.pos_prof.size();
+  const size_t ntab = n_fast ? 2 * (npx + npy) : 0;
+  int rc = ensure_work(ctx, 16 * 8 + nb * 8 + (permute ? nb * 8 : 0) + ntab * sizeof(sk::BplaPos) +
+                                items.size() * sizeof(int2) + 8192);
   if (rc) return rc;
   Arena A{static_cast<char*>(ctx->work), 0, ctx->work_bytes};
   double* d_tb = A.take<double>(16);
   int32_t* d_px = A.take<int32_t>(nb);
   int32_t* d_py = A.take<int32_t>(nb);
+  int64_t* d_oidx = permute ? A.take<int64_t>(nb) : nullptr;
   unsigned long long* d_ctr = A.take<unsigned long long>(8);
+  sk::BplaPos* d_tab = ntab ? A.take<sk::BplaPos>(ntab) : nullptr;
+  int2* d_items = items.empty() ? nullptr : A.take<int2>(items.size());
+  if (d_items)
+    SK_HIP(ctx, hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(int2),
+                               hipMemcpyHostToDevice, ctx->stream));
   hipStream_t S = ctx->stream;
   SK_HIP(ctx, hipMemcpyAsync(d_tb, kp->score_table, 16 * 8, hipMemcpyHostToDevice, S));
   SK_HIP(ctx, hipMemcpyAsync(d_px, x, nb * 4, hipMemcpyHostToDevice, S));
   SK_HIP(ctx, hipMemcpyAsync(d_py, y, nb * 4, hipMemcpyHostToDevice, S));
+  if (permute) SK_HIP(ctx, hipMemcpyAsync(d_oidx, oidx.data(), nb * 8, hipMemcpyHostToDevice, S));
   SK_HIP(ctx, hipMemsetAsync(d_ctr, 0, 8 * sizeof(unsigned long long), S));
   sk::BplaLaunch T;
   T.xset = xs_->dev;
@@ -684,25 +762,75 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   T.beta_ext = std::exp(kp->beta * kp->ext);
   T.sw = sw ? 1 : 0;
   T.bp = bp ? 1 : 0;
-  T.xs = d_px;
-  T.ys = d_py;
-  T.n_pairs = n;
+  T.oidx = d_oidx;
   T.out = out_dev;
-  T.pair_counter = d_ctr;
-  T.lds_max_len = (std::max(PY.max_len, 64) + 1) & ~1;
-  const int w = 4;
-  const size_t lds = sk::bpla_lds_bytes(T, w);
-  if (lds > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
-  const int per_cu = std::max(1, std::min<int>((int)(163840 / lds), 8));
-  const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (n + w - 1) / w);
   SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
-  SK_HIP(ctx, sk::launch_bpla(T, (int)g, w, S));
+  if (n_fast) {
+    // x-role table of the x set, y-role table of the y set
+    sk::BplaPos* tx = d_tab;           // [npx] x role | [npx] y role
+    sk::BplaPos* ty = d_tab + npx;
+    SK_HIP(ctx, sk::launch_bpla_tab(xs_->dev.pos_prof, xs_->dev.pos_lru, (int64_t)npx, d_tb, tx,
+                                    d_tab + npx, S));
+    if (npy) {
+      ty = d_tab + 2 * npx + npy;      // [npy] x role (unused) | [npy] y role
+      SK_HIP(ctx, sk::launch_bpla_tab(ys_->dev.pos_prof, ys_->dev.pos_lru, (int64_t)npy, d_tb,
+                                      d_tab + 2 * npx, ty, S));
+    }
+    sk::BplaLaunch F = T;
+    F.xtab = tx;
+    F.ytab = ty;
+    F.xs = d_px;
+    F.ys = d_py;
+    F.n_pairs = n_fast;
+    F.pair_counter = d_ctr;
+    F.lds_max_len = (std::max(PY.max_len, 64) + 1) & ~1;
+    int w, per_cu;
+    int64_t units;
+    if (d_items) {  // y-grouped: 8-wave workgroups sharing the y columns
+      F.items = d_items;
+      F.n_items = (int32_t)items.size();
+      w = kItemWaves;
+      const size_t l = sk::bpla_items_lds_bytes(F.lds_max_len, w);
+      if (l > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
+      per_cu = std::max(1, std::min<int>((int)(163840 / l), 2));
+      units = F.n_items;
+    } else {
+      const size_t wl = sk::bpla_fast_wave_lds_bytes(F.lds_max_len);
+      if (wl > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
+      // as many waves per CU as the per-wave LDS allows (<= 16), in
+      // workgroups of up to 4
+      static const int wcap =
+          std::getenv("SK_BPLA_WAVES") ? std::atoi(std::getenv("SK_BPLA_WAVES")) : 16;
+      const int per_cu_w =
+          (int)std::max<size_t>(1, std::min<size_t>((size_t)wcap, (163840 - 2 * sk::kBplaExpLds) / wl));
+      w = std::min(4, per_cu_w);
+      per_cu = std::max(1, per_cu_w / w);
+      units = (n_fast + w - 1) / w;
+    }
+    const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, units);
+    SK_HIP(ctx, sk::launch_bpla_fast(F, (int)g, w, S));
+  }
+  if (n_fast < n) {
+    sk::BplaLaunch G = T;
+    G.xs = d_px + n_fast;
+    G.ys = d_py + n_fast;
+    G.oidx = d_oidx ? d_oidx + n_fast : nullptr;
+    G.n_pairs = n - n_fast;
+    G.pair_counter = d_ctr + 1;
+    G.lds_max_len = (std::max(PY.max_len, 64) + 1) & ~1;
+    const int w = 4;
+    const size_t lds = sk::bpla_lds_bytes(G, w);
+    if (lds > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
+    const int per_cu = std::max(1, std::min<int>((int)(163840 / lds), 8));
+    const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (G.n_pairs + w - 1) / w);
+    SK_HIP(ctx, sk::launch_bpla(G, (int)g, w, S));
+  }
   SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
   SK_HIP(ctx, hipStreamSynchronize(S));
   float ms = 0.f;
   SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_stem_ms = ms;
-  ctx->last_launches = 1;
+  ctx->last_launches = (n_fast ? 1 : 0) + (n_fast < n ? 1 : 0);
   return SK_OK;
 }
 

@@ -107,3 +107,23 @@ def test_bpla_normalized_and_predict(gpu_ctx, bpla_set):
     row = gpu_ctx.test_row(ds, 2, ds, kern)
     ref = np.array([po.kernel_value(9, om[i], om[2], kern.params) for i in range(len(om))])
     assert rel_err(row, ref) < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("noBP,SW", MODES)
+def test_bpla_y_grouped_items(gpu_ctx, bpla_set, noBP, SW, monkeypatch):
+    """Many pairs per y: the fast pairs go to the y-grouped kernel (a
+    workgroup stages one y for its waves); the non-dyadic ones (the 3-row
+    alignment) stay on the general kernel.  Same values as one pair per wave,
+    bit for bit, and as the oracle."""
+    ds, om = bpla_set
+    n = len(om)
+    kern = ska.BPLAKernel(noBP=noBP, SW=SW)
+    x = np.tile(np.arange(n, dtype=np.int32), 24)
+    y = np.repeat(np.array([0, 11, 12], np.int32), x.size // 3 + 1)[: x.size]
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    uniq = sorted(set(zip(x.tolist(), y.tolist())))
+    ref = {p: po.kernel_value(kern.params.kind, om[p[0]], om[p[1]], kern.params) for p in uniq}
+    assert rel_err(got, [ref[p] for p in zip(x.tolist(), y.tolist())]) < TOL
+    monkeypatch.setenv("SK_BPLA_NO_ITEMS", "1")
+    assert np.array_equal(gpu_ctx.pairs(ds, kern, x, y), got)
