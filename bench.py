@@ -10,17 +10,21 @@ base-pairing probabilities, --basepair 0.01).  Units are Gram cells K(i,j),
 i <= j, exactly the cells the reference evaluates
 (common/kernel_matrix.cpp:44-55): 8,390,656 sequence pairs.
 
-A *step* is one slice of that upper triangle: cell k (row-major i <= j) is in
-slice k % S, so every slice has the same cost mix.  With N GPUs (one process
-per GPU), rank r computes slice (step*N + r) -- per-GPU work is fixed, so
-scaling is weak -- and the ranks all-gather the step's Gram entries with the
-engine's own RCCL communicator (sk_comm_allgather).  S is a multiple of N, so
-rank r's slices are always cells k with k % N == r: the cells the product's
-sharded Gram (sk_gram_sharded, the reference MPI Gram's cyclic plan,
-kernel_matrix.cpp:210-224) gives rank r -- over S/N steps a rank computes
-exactly its share of the shipped plan.  --full times one call of the product
-path itself: sk_gram_sharded over all N ranks (cells, all-gather, host
-assembly of the whole mirrored matrix).
+A *step* is one slice of that upper triangle, 1/S of its cells per GPU.  The
+product's sharded Gram (sk_gram_sharded, the reference MPI Gram's cyclic plan,
+kernel_matrix.cpp:210-224) gives rank r of N the cells k % N == r (k =
+row-major index of cell (i, j), i <= j), and every slice is a subset of that
+plan, so over S/N steps a rank computes exactly its share of the shipped
+Gram.  DAG kernels (ns, c2, c5): the columns j (the y examples) are folded in
+pairs (j, n-1-j: n+1 cells per pair) and the pairs dealt round-robin to S/N
+column groups of equal cost; step t is column group t, rank r taking its
+cells k % N == r -- each y keeps the same share of its column as in the full
+Gram (about (j+1)/N pairs), so a step has the full Gram's composition.  Other
+kernels: cell k is in slice k % S and rank r computes slice (t*N + r).  Per-GPU
+work is fixed, so scaling is weak; the ranks all-gather the step's Gram
+entries with the engine's own RCCL communicator (sk_comm_allgather).  --full
+times one call of the product path itself: sk_gram_sharded over all N ranks
+(cells, all-gather, host assembly of the whole mirrored matrix).
 
 Other SURVEY.md §8 configurations (--config): c2 ss_kernel 256 x L150,
 c3 4-D stem kernel 1024 x L200, c4 BPLA 2048 alignments L~200, c5 DAG stem
@@ -256,8 +260,34 @@ def main():
     n_slices_needed = (a.warmup + a.steps) * world
     S = max(S, n_slices_needed)
     S = -(-S // world) * world  # a multiple of N: rank r's slices are cells k % N == r
-    slice_of = lambda s: (iu[s::S], ju[s::S])
-    per = int(np.ceil(iu.size / S))
+    G = S // world
+    if kind in ("ss", "stem") and G <= a.n // 2:
+        # folded column pairs dealt round-robin to G column groups
+        colg = np.empty(a.n, np.int64)
+        for p in range(a.n // 2):
+            colg[p] = colg[a.n - 1 - p] = p % G
+        if a.n % 2:
+            colg[a.n // 2] = (a.n // 2) % G
+        cell_g = colg[ju]
+        kcell = np.arange(iu.size, dtype=np.int64)
+        groups = {}
+
+        def slice_of_step(t):
+            g = t % G
+            if g not in groups:
+                groups[g] = np.flatnonzero(cell_g == g)
+            sel = groups[g]
+            sel = sel[kcell[sel] % world == rank]
+            return iu[sel], ju[sel]
+        per = max(int(np.count_nonzero(cell_g == g)) for g in range(G))
+        per = -(-per // world)
+        step_kind = f"column group (step mod {G}) of {G} folded-pair groups, cells k % {world} == rank"
+    else:
+        def slice_of_step(t):
+            s = (t * world + rank) % S
+            return iu[s::S], ju[s::S]
+        per = int(np.ceil(iu.size / S))
+        step_kind = f"cells k % {S} == step*{world} + rank"
     out = torch.zeros(per, dtype=torch.float64, device=dev)
     gathered = torch.empty(per * world, dtype=torch.float64, device=dev)
     full_gram = [None]
@@ -267,8 +297,7 @@ def main():
             full_gram[0] = ctx.gram_sharded(ds, kern, normalize=False)
             x, y = shard.rank_pairs(a.n, world, rank)
             return x, y, ctx.last_timing()
-        sl = step * world + rank
-        x, y = slice_of(sl % S)
+        x, y = slice_of_step(step)
         ctx.pairs_device(ds, kern, x, y, out.data_ptr())
         tm = ctx.last_timing()
         ctx.allgather(out.data_ptr(), per, gathered.data_ptr())
@@ -364,6 +393,7 @@ def main():
             "config": {
                 "workload": f"{a.config}: {a.n}x{a.n} {kdesc} Gram, L={cfg['L']}, "
                             f"step = 1/{S} of the {iu.size} upper-triangle pairs per GPU",
+                "step_cells": step_kind,
                 "n_sequences": a.n, "length": cfg["L"], "pairs_per_step_per_gpu": per,
                 "kernel": kdesc, "basepair_th": 0.01,
                 "parallelism": f"cyclic cell plan x{world} (sk_comm_allgather, RCCL)"

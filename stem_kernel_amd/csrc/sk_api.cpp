@@ -1202,40 +1202,49 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       }
 #endif
       C.grid = ctx->n_cu * per_cu;
-      // Work item = up to `rounds` pairs per wave of one y.  A workgroup
-      // waits for its slowest wave at every item boundary, so items are as
-      // large as the balance allows: about two items per workgroup on
-      // average, at least two rounds (NS: 12 rounds, +4 % over 2).
-      int64_t class_pairs = 0;
-      for (int j = 0; j < ny; ++j)
-        if (sk::stem_maxk(std::max(PY.ex_nl[j], 1)) == maxk) class_pairs += cnt[j + 1] - cnt[j];
-#ifdef SK_ITEM_ROUNDS
-      const int64_t rounds = SK_ITEM_ROUNDS;
-#else
-      const int64_t rounds =
-          std::max<int64_t>(2, class_pairs / std::max<int64_t>(1, 2LL * C.grid * C.nwaves));
-#endif
-      const int64_t chunk = rounds * C.nwaves;
-      struct It {
-        int4 v;
-        double cost;
-      };
-      std::vector<It> tmp;
+      // Work items = pairs of one y (the workgroup stages one y DAG in LDS
+      // and waits for its slowest wave at every item boundary, about half a
+      // pair per wave).  Guided self-scheduling: the y's are taken largest
+      // column first and each item is 1/(K * grid) of the class's remaining
+      // cost (at least one round of W pairs), so the first items are large
+      // (few boundaries) and the last ones a round each (short launch tail).
+      // Items are pulled in this order (K = 1.5; NS 161k pairs/s at K = 1,
+      // 160.8k at 1.5, 160.0k at 2, 157.2k at 8; C2 148k at 1.5, 140k at 1).
+      std::vector<int> ysel;
+      double class_cost = 0.0;
       for (int j = 0; j < ny; ++j) {
-        if (sk::stem_maxk(std::max(PY.ex_nl[j], 1)) != maxk) continue;
-        for (int64_t b = cnt[j]; b < cnt[j + 1]; b += chunk) {
-          const int64_t e = std::min<int64_t>(cnt[j + 1], b + chunk);
+        if (cnt[j + 1] == cnt[j] || sk::stem_maxk(std::max(PY.ex_nl[j], 1)) != maxk) continue;
+        ysel.push_back(j);
+        for (int64_t t = cnt[j]; t < cnt[j + 1]; ++t)
+          class_cost += (double)PX.ex_nl[x[byy[t]]] * (double)PY.ex_nl[j];
+      }
+      std::stable_sort(ysel.begin(), ysel.end(), [&](int a, int b) {
+        return cnt[a + 1] - cnt[a] > cnt[b + 1] - cnt[b];
+      });
+      double gss_k = 1.5;  // tuning knob: SK_GSS_K (items per workgroup at the start)
+      if (const char* e = std::getenv("SK_GSS_K")) gss_k = std::max(0.25, std::atof(e));
+      const double share = 1.0 / (gss_k * (double)C.grid);
+      double remaining = class_cost;
+      C.item_off = items.size();
+      for (int j : ysel) {
+        const double yw = (double)PY.ex_nl[j];
+        int64_t b = cnt[j];
+        while (b < cnt[j + 1]) {
+          const double target = remaining * share;
+          int64_t e = b;
           double cost = 0.0;
-          for (int64_t t = b; t < e; ++t)
-            cost += (double)PX.ex_nl[x[byy[t]]] * (double)PY.ex_nl[j];
-          tmp.push_back({make_int4(j, (int)b, (int)(e - b), 0), cost});
+          // whole rounds of W pairs until the target cost is reached
+          while (e < cnt[j + 1] && (e - b < C.nwaves || cost < target)) {
+            const int64_t re = std::min<int64_t>(cnt[j + 1], e + C.nwaves);
+            for (int64_t t = e; t < re; ++t) cost += (double)PX.ex_nl[x[byy[t]]] * yw;
+            e = re;
+          }
+          items.push_back(make_int4(j, (int)b, (int)(e - b), 0));
+          remaining -= cost;
+          b = e;
         }
       }
-      std::stable_sort(tmp.begin(), tmp.end(),
-                       [](const It& a, const It& b) { return a.cost > b.cost; });
-      C.item_off = items.size();
-      C.n_items = tmp.size();
-      for (auto& t : tmp) items.push_back(t.v);
+      C.n_items = items.size() - C.item_off;
       C.grid = (int)std::min<int64_t>(C.grid, std::max<int64_t>(1, (int64_t)C.n_items));
       classes.push_back(C);
     }
