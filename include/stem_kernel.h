@@ -312,7 +312,9 @@ int sk_last_timing(const sk_context *ctx, double *stem_ms, double *string_ms,
                    double *cells, int32_t *launches);
 /* Kernel instantiations launched by the last compute call (parity-coverage
  * diagnostic): *stem_maxk_mask has bit MAXK/4 set for every DAG stem register
- * class run (MAXK = 4, 8, ..., 32 64-node slots per lane); *stem4d_mask has
+ * class run (MAXK = 4, 8, ..., 32 64-node slots per lane) and bit 0 when the
+ * big-y kernel ran (y examples over 2,048 non-leaf nodes or with a stem edge
+ * gap over 1,023, which the register classes cannot hold); *stem4d_mask has
  * bit log2(CPL) set for every 4-D stem class run (CPL = 1, 2, 4, 8 cells per
  * lane), shifted by 4 for the banded (partial_dp) variant. */
 int sk_last_classes(const sk_context *ctx, uint32_t *stem_maxk_mask, uint32_t *stem4d_mask);

@@ -34,6 +34,29 @@ struct StemLaunch {
   unsigned long long* stamps = nullptr;  // diagnostic builds (SK_STAMPS) only
 };
 
+// DAG stem kernel for y examples the register classes cannot hold
+// (dag_stem_big.hip): one wavefront per pair, the y DAG in level order from
+// HBM (L2-resident), rows S and G1 in per-wave scratch next to the G0 slab.
+struct StemBigLaunch {
+  DevSet xset, yset;
+  DevParamNodes pn;
+  const double* co_subst = nullptr;
+  const double* gpow = nullptr;
+  int32_t n_gpow = 0;
+  double gap2 = 0.0;
+  uint32_t band = 0;
+  const int32_t* xs = nullptr;   // pair k: K(x = xs[k], y = ys[k]) -> out[oidx[k]]
+  const int32_t* ys = nullptr;
+  const int64_t* oidx = nullptr;
+  int64_t n_pairs = 0;
+  double* out = nullptr;
+  double* scratch = nullptr;     // per wave: (slots + 1) G0 rows, S, G1 (stride doubles each)
+  int64_t stride = 0;            // >= max y non-leaf nodes, multiple of 64
+  int64_t wave_doubles = 0;      // (slots + 3) * stride
+};
+hipError_t launch_stem_big(const StemBigLaunch& P, int grid, hipStream_t st);
+constexpr int kStemBigWaves = 4;  // waves per workgroup (independent pairs)
+
 struct StrLaunch {
   DevSet xset, yset;
   const double* st = nullptr;    // 16: exp(alpha*ribosum_s) or match/mismatch

@@ -71,6 +71,10 @@ struct HostPack {
       ex_len, ex_pos_base, ex_has_w;
   // every profile entry of the example a multiple of 1/256 (BPLA fast path)
   std::vector<uint8_t> ex_dyadic;
+  // y examples the register-class stem kernel cannot take (more than 2048
+  // non-leaf nodes, or a stem edge gap over 1023: its packed 11/11/10-bit
+  // records); they go to sk_dag_stem_big_kernel (level-order arrays)
+  std::vector<uint8_t> ex_big;
   std::vector<float> ex_nseqs;
   std::vector<uint32_t> nd_a, nd_b, nd_c;
   std::vector<float> nd_w, nd_nbp;
@@ -304,6 +308,7 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) Pw[X.edge_to[k]] += Pw[v];
 
     const int ebase = (int)P.ed.size(), bbase = (int)P.bpf_code.size();
+    bool big_gap = false;
     for (int k = 0; k < nl; ++k) {
       const int v = order[k];
       const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
@@ -325,11 +330,11 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       if (!loop) {
         for (uint32_t t = e0; t < e1; ++t) {
           const int c = nid[X.edge_to[t]];
-          if (c < 0 || X.edge_gaps[t] > 1023) {
-            // the stem kernel packs an edge as child:11 | parent:11 | gaps:10
-            err = c < 0 ? "unexpected DAG shape: stem with a leaf child" : "gap count exceeds 1023";
-            return SK_ERR_UNSUPPORTED;
+          if (c < 0 || X.edge_gaps[t] > 0xffff) {
+            err = c < 0 ? "unexpected DAG shape: stem with a leaf child" : "gap count exceeds 65535";
+            return c < 0 ? SK_ERR_INVALID : SK_ERR_UNSUPPORTED;
           }
+          big_gap |= X.edge_gaps[t] > 1023;
           P.ed.push_back(make_uint2((uint32_t)c | (X.edge_gaps[t] << 16), (uint32_t)k));
         }
       }
@@ -342,6 +347,9 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     for (int k = 0; k < nl; ++k) lv[level[order[k]] + 1]++;
     for (int l = 0; l < nlev; ++l) lv[l + 1] += lv[l];
     P.lvl.insert(P.lvl.end(), lv.begin(), lv.end());
+    // the register-class kernel's y records: child:11 | parent:11 | gaps:10
+    const bool big = nl > 2048 || big_gap;
+    P.ex_big.push_back(big ? 1 : 0);
 
     // y-role numbering for the stem kernel: nodes sorted by length (span
     // last - first), so the nodes inside a row's length band are one index
@@ -363,7 +371,13 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       // scheduling, priority = height of the parent (longest path up to a
       // root; the critical chain first), then the child's length; chunks
       // are padded with dummy records (child == parent: weight 0).
-      {
+      if (big) {  // no sweep schedule: the big-y kernel walks the levels
+        const int lmax = nl ? (int)(P.nd_b[nb0 + srt[nl - 1]] & 0xffff) : 0;
+        P.ex_ysc_base.push_back((int32_t)(P.ysc.size() / 64));
+        P.ex_ycs_base.push_back((int32_t)P.ycs.size());
+        for (int v = 0; v <= lmax + 1; ++v) P.ycs.push_back(0);
+        P.ex_nch.push_back(0);
+      } else {
         std::vector<uint32_t> er;       // records child:11 | parent:11 | gaps:10
         std::vector<int> epar, ech;
         std::vector<std::vector<int>> by_child(nl), parents(nl);
@@ -451,8 +465,8 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         P.yn_a.push_back(((uint32_t)P.ye2.size() - ye2_base) | (a & 0xffff0000u));
         for (uint32_t t = 0; t < ne; ++t) {
           const uint2 rec = P.ed[ebase + el + t];
-          P.ye2.push_back((uint32_t)pos[rec.x & 0xffff] | ((uint32_t)i << 11) |
-                          ((rec.x >> 16) << 22));
+          P.ye2.push_back(big ? 0u : (uint32_t)pos[rec.x & 0xffff] | ((uint32_t)i << 11) |
+                                         ((rec.x >> 16) << 22));
         }
         // c = loop leaf-edge gaps:16 | first bp-freq code:4 | single-entry flag
         // (one bp-freq entry, no gap column: the closed-form node score)
@@ -1129,6 +1143,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   std::vector<int4> items;
   std::vector<int32_t> ixs;
   std::vector<int64_t> ioidx;
+  std::vector<int32_t> big_x, big_y;  // pairs whose y goes to the big-y kernel
+  std::vector<int64_t> big_o;
+  int big_max_nl = 0;
   const int max_len = std::max(PX.max_len, PY.max_len);
   if (stem) {
     std::vector<int64_t> cnt(ny + 1, 0);
@@ -1151,15 +1168,39 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       ixs[t] = x[byy[t]];
       ioidx[t] = byy[t];
     }
-    for (int j = 0; j < ny; ++j)
-      if (cnt[j + 1] > cnt[j] && sk::stem_maxk(std::max(PY.ex_nl[j], 1)) < 0)
-        return fail(ctx, SK_ERR_UNSUPPORTED, "y example has more than 2048 non-leaf DAG nodes");
+    // y examples beyond the register classes (or forced there by the
+    // diagnostic SK_FORCE_BIG_Y=1) go to sk_dag_stem_big_kernel
+    const bool force_big = [] {
+      const char* e = std::getenv("SK_FORCE_BIG_Y");
+      return e && std::atoi(e) != 0;
+    }();
+    std::vector<uint8_t> ybig(ny, 0);
+    for (int j = 0; j < ny; ++j) ybig[j] = force_big || PY.ex_big[j] ? 1 : 0;
+    auto in_class = [&](int j, int maxk) {
+      return !ybig[j] && sk::stem_maxk(std::max(PY.ex_nl[j], 1)) == maxk;
+    };
+    {
+      std::vector<int64_t> bk;  // pairs dealt cyclically to the waves: costliest first
+      for (int j = 0; j < ny; ++j) {
+        if (!ybig[j] || cnt[j + 1] == cnt[j]) continue;
+        big_max_nl = std::max(big_max_nl, PY.ex_nl[j]);
+        for (int64_t t = cnt[j]; t < cnt[j + 1]; ++t) bk.push_back(byy[t]);
+      }
+      std::stable_sort(bk.begin(), bk.end(), [&](int64_t a, int64_t b) {
+        return (double)PX.ex_nl[x[a]] * PY.ex_nl[y[a]] > (double)PX.ex_nl[x[b]] * PY.ex_nl[y[b]];
+      });
+      for (int64_t k : bk) {
+        big_x.push_back(x[k]);
+        big_y.push_back(y[k]);
+        big_o.push_back(k);
+      }
+    }
     for (int maxk : {32, 28, 24, 20, 16, 12, 8, 4}) {
       StemClass C;
       C.maxk = maxk;
       bool any = false;
       for (int j = 0; j < ny; ++j) {
-        if (cnt[j + 1] == cnt[j] || sk::stem_maxk(std::max(PY.ex_nl[j], 1)) != maxk) continue;
+        if (cnt[j + 1] == cnt[j] || !in_class(j, maxk)) continue;
         any = true;
         C.max_nl = std::max(C.max_nl, PY.ex_nl[j]);
         C.max_edges = std::max(C.max_edges, PY.ex_edge_base[j + 1] - PY.ex_edge_base[j]);
@@ -1213,7 +1254,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       std::vector<int> ysel;
       double class_cost = 0.0;
       for (int j = 0; j < ny; ++j) {
-        if (cnt[j + 1] == cnt[j] || sk::stem_maxk(std::max(PY.ex_nl[j], 1)) != maxk) continue;
+        if (cnt[j + 1] == cnt[j] || !in_class(j, maxk)) continue;
         ysel.push_back(j);
         for (int64_t t = cnt[j]; t < cnt[j + 1]; ++t)
           class_cost += (double)PX.ex_nl[x[byy[t]]] * (double)PY.ex_nl[j];
@@ -1259,6 +1300,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   need += 256 * 8 + 16 * 8 + (size_t)(max_len + 4) * 8 * 2;
   need += 1024;
   need += items.size() * sizeof(int4) + nb * (4 + 8) + nb * 8 * 2 + nb * 4 * 2 + 64 + 8 * 256;
+  need += big_x.size() * (4 + 4 + 8) + 3 * 256;
   need += 16 * 256;
   rc = ensure_work(ctx, need);
   if (rc) return rc;
@@ -1275,6 +1317,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   int32_t* d_px = A.take<int32_t>(nb);
   int32_t* d_py = A.take<int32_t>(nb);
   int* d_ctr = A.take<int>(64);
+  int32_t* d_bx = A.take<int32_t>(std::max<size_t>(big_x.size(), 1));
+  int32_t* d_by = A.take<int32_t>(std::max<size_t>(big_x.size(), 1));
+  int64_t* d_bo = A.take<int64_t>(std::max<size_t>(big_x.size(), 1));
 
   // parameter tables
   std::vector<double> co(256), st(16);
@@ -1334,6 +1379,22 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       const int64_t slab = (int64_t)(PX.max_slots + 1) * 64 * C.maxk;
       scratch_need = std::max(scratch_need, (size_t)C.grid * C.nwaves * slab * sizeof(double));
     }
+    // big-y kernel: per wave S, G1 and the G0 slots, rows of `big_stride`
+    // doubles; as many waves as pairs, the grid, and a scratch budget allow
+    const int64_t big_stride = ((int64_t)std::max(big_max_nl, 1) + 63) / 64 * 64;
+    const int64_t big_wave = (int64_t)(PX.max_slots + 2) * big_stride;
+    int big_grid = 0;
+    if (!big_x.empty()) {
+      size_t free_b = 0, total_b = 0;
+      SK_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
+      const size_t budget = std::max<size_t>(std::min<size_t>(free_b / 2, (size_t)32 << 30),
+                                             (size_t)big_wave * 8 * sk::kStemBigWaves);
+      const int64_t by_mem = (int64_t)(budget / ((size_t)big_wave * 8 * sk::kStemBigWaves));
+      const int64_t by_pairs = ((int64_t)big_x.size() + sk::kStemBigWaves - 1) / sk::kStemBigWaves;
+      big_grid = (int)std::max<int64_t>(1, std::min<int64_t>({by_mem, by_pairs, (int64_t)ctx->n_cu * 8}));
+      scratch_need = std::max(scratch_need,
+                              (size_t)big_grid * sk::kStemBigWaves * (size_t)big_wave * sizeof(double));
+    }
     rc = ensure_scratch(ctx, std::max<size_t>(scratch_need, 64));
     if (rc) return rc;
 #ifdef SK_STAMPS
@@ -1373,6 +1434,31 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SK_HIP(ctx, sk::launch_stem(SL, C.grid, C.nwaves, S));
       ctx->last_stem_classes |= 1u << (C.maxk / 4);
     }
+    if (!big_x.empty()) {
+      const size_t nbig = big_x.size();
+      SK_HIP(ctx, hipMemcpyAsync(d_bx, big_x.data(), nbig * 4, hipMemcpyHostToDevice, S));
+      SK_HIP(ctx, hipMemcpyAsync(d_by, big_y.data(), nbig * 4, hipMemcpyHostToDevice, S));
+      SK_HIP(ctx, hipMemcpyAsync(d_bo, big_o.data(), nbig * 8, hipMemcpyHostToDevice, S));
+      sk::StemBigLaunch BL;
+      BL.xset = xs_->dev;
+      BL.yset = ys_->dev;
+      BL.pn = pn;
+      BL.co_subst = d_co;
+      BL.gpow = d_gp_loop;
+      BL.n_gpow = max_len + 2;
+      BL.gap2 = gap2;
+      BL.band = kp->len_band;
+      BL.xs = d_bx;
+      BL.ys = d_by;
+      BL.oidx = d_bo;
+      BL.n_pairs = (int64_t)nbig;
+      BL.out = stem_out;
+      BL.scratch = ctx->scratch;
+      BL.stride = big_stride;
+      BL.wave_doubles = big_wave;
+      SK_HIP(ctx, sk::launch_stem_big(BL, big_grid, S));
+      ctx->last_stem_classes |= 1u;
+    }
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
 #ifdef SK_STAMPS
     {
@@ -1392,7 +1478,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
                      C.maxk, C.max_nl, C.nwaves, C.grid, C.n_items);
     }
 #endif
-    ctx->last_launches = (int32_t)classes.size();
+    ctx->last_launches = (int32_t)classes.size() + (big_x.empty() ? 0 : 1);
   }
   if (str) {
     const hipStream_t SS = side ? ctx->side : S;

@@ -519,7 +519,8 @@ class Context:
 
     def last_classes(self):
         """Kernel instantiations the last compute call launched: the DAG stem
-        register classes (MAXK values) and the 4-D classes as (CPL, banded)."""
+        register classes (MAXK values; 0 = the big-y kernel, dag_stem_big.hip)
+        and the 4-D classes as (CPL, banded)."""
         a, b = C.c_uint32(), C.c_uint32()
         self._chk(lib().sk_last_classes(self._h, C.byref(a), C.byref(b)))
         maxk = sorted(4 * k for k in range(32) if a.value >> k & 1)
