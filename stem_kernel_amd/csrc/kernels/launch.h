@@ -154,6 +154,10 @@ struct Stem4dLaunch {
   double* out = nullptr;
   const int32_t* band_lo = nullptr;  // partial_dp band (nullptr: full_dp)
   const int32_t* band_hi = nullptr;
+  // |y| >= 512: per work item 2 x 2 boundary columns of kbound_stride / 4
+  // doubles each (stem4d.hip k tiles)
+  double* kbound = nullptr;
+  int64_t kbound_stride = 0;
 };
 
 int stem4d_cpl(int m);

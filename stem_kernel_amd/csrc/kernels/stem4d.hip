@@ -72,25 +72,32 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
   double* span_cur = P.scratch + pr.scratch_off + (int64_t)(d1 % 3) * (n + 1) * 4 * cp;
   double* __restrict__ cur = span_cur + (int64_t)i * 4 * cp;
   const double g = P.gap;
-  // lane owns k = lane + 64c: every state access of a wave instruction is
-  // 512 contiguous bytes
-  const int k0 = lane;
+  // k tiles of 64*CPL cells: lane owns k = kb + lane + 64c (every state
+  // access of a wave instruction is 512 contiguous bytes).  y longer than one
+  // tile (|y| >= 512 at CPL 8) is swept tile by tile, right to left: the
+  // only dependence across k is K3/G3 at (k+1, l) of span d2-1, which the
+  // tile to the right leaves in a per-plane boundary column (P.kbound).
+  constexpr int TW = 64 * CPL;
+  const int ntile = (m + TW) / TW;
 
   if (d1 == 0) {  // plane (j,j): K0 = 1, G0 = g^(l-k), K1 = G1 = 0  (:297-309)
-    int R = 0;
-    for (int d2 = 0; d2 <= m; ++d2) {
-      const double gd = P.gpow[d2];
+    for (int kt = 0; kt < ntile; ++kt) {
+      const int k0 = kt * TW + lane;
+      int R = 0;
+      for (int d2 = 0; d2 <= m; ++d2) {
+        const double gd = P.gpow[d2];
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const int k = k0 + 64 * c;
-        if (k <= m - d2) {
-          cur[R + k] = 1.0;
-          cur[cp + R + k] = gd;
-          cur[2 * cp + R + k] = 0.0;
-          cur[3 * cp + R + k] = 0.0;
+        for (int c = 0; c < CPL; ++c) {
+          const int k = k0 + 64 * c;
+          if (k <= m - d2) {
+            cur[R + k] = 1.0;
+            cur[cp + R + k] = gd;
+            cur[2 * cp + R + k] = 0.0;
+            cur[3 * cp + R + k] = 0.0;
+          }
         }
+        R += pad4(m + 1 - d2);
       }
-      R += pad4(m + 1 - d2);
     }
     if (n == 0 && lane == 0) P.out[pr.out_index] = 1.0;
     return;
@@ -139,6 +146,20 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
   // (i+1,j-1) is guarded by that plane's constraints unless it is the fully
   // initialised plane (j-1,j-1).
   const bool cg_guard = BAND && d1 >= 3;
+  // boundary columns of this plane: [2 parities][K3, G3][span d2]
+  double* kbnd = ntile > 1 ? P.kbound + it * P.kbound_stride : nullptr;
+  const int bstride = m + 1;
+
+  for (int kt = ntile - 1; kt >= 0; --kt) {
+  const int kb = kt * TW;
+  const int k0 = kb + lane;
+  double* bnd_w = kbnd ? kbnd + (int64_t)(kt & 1) * 2 * bstride : nullptr;        // for tile kt-1
+  const double* bnd_r = kbnd ? kbnd + (int64_t)((kt + 1) & 1) * 2 * bstride : nullptr;  // of tile kt+1
+  const bool has_right = kt + 1 < ntile;
+  if (bnd_w && lane == 0) {  // nothing swept below d2_lo: the state there is zero
+    bnd_w[max(d2_lo - 1, 0)] = 0.0;
+    bnd_w[bstride + max(d2_lo - 1, 0)] = 0.0;
+  }
 
   double K2[CPL], G2[CPL], K3[CPL], G3[CPL];
   uint8_t yk[CPL];
@@ -178,7 +199,7 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + 64 * c;
       const int l = k + d2;
-      if (BAND && (64 * c > khi || 64 * c + 63 < klo)) continue;  // whole slot outside
+      if (BAND && (kb + 64 * c > khi || kb + 64 * c + 63 < klo)) continue;  // whole slot outside
       pbp[c] = 0.0f;
       pGs[c] = 0.0;
       pyl[c] = 0;
@@ -224,11 +245,17 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
     if (d2 + 1 <= d2_hi) fetch(d2 + 1, Rn, Rm1);
     // K3/G3 of (k+1, l): my next cell, or the next lane's first (span d2-1)
     double K3n[CPL], G3n[CPL];
+    // the last slot's neighbour: the right tile's first cell, span d2-1
+    double rk = 0.0, rg = 0.0;
+    if (has_right) {
+      rk = bnd_r[d2 - 1];
+      rg = bnd_r[bstride + d2 - 1];
+    }
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       // lane 63's neighbour k+1 is lane 0 of the next slot
-      const double hk = c + 1 < CPL ? bcast_lane0(K3[c + 1 < CPL ? c + 1 : c]) : 0.0;
-      const double hg = c + 1 < CPL ? bcast_lane0(G3[c + 1 < CPL ? c + 1 : c]) : 0.0;
+      const double hk = c + 1 < CPL ? bcast_lane0(K3[c + 1 < CPL ? c + 1 : c]) : rk;
+      const double hg = c + 1 < CPL ? bcast_lane0(G3[c + 1 < CPL ? c + 1 : c]) : rg;
       K3n[c] = wave_shl1(K3[c], hk);
       G3n[c] = wave_shl1(G3[c], hg);
     }
@@ -237,7 +264,7 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
     const int klo = max(cli, clj - d2), khi = min(min(chi, chj - d2), kmax);
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      if (BAND && (64 * c > khi || 64 * c + 63 < klo)) {  // whole slot outside (wave-uniform)
+      if (BAND && (kb + 64 * c > khi || kb + 64 * c + 63 < klo)) {  // whole slot outside (wave-uniform)
         K2[c] = G2[c] = K3[c] = G3[c] = 0.0;
         continue;
       }
@@ -299,9 +326,19 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
         if (d2 == m && i == 0 && j == n) P.out[pr.out_index] = K0;  // K0(0,n,0,m)
       }
     }
+    if (bnd_w && lane == 0) {
+      bnd_w[d2] = K3[0];
+      bnd_w[bstride + d2] = G3[0];
+    }
     Rm1 = R;
     R = Rn;
   }
+  if (kbnd) {  // the next tile's lanes read what lane 0 stored
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  }  // k tiles
   if (m == 0 && i == 0 && j == n && lane == 0) P.out[pr.out_index] = 1.0;
 }
 
@@ -309,8 +346,7 @@ int stem4d_cpl(int m) {
   if (m + 1 <= 64) return 1;
   if (m + 1 <= 128) return 2;
   if (m + 1 <= 256) return 4;
-  if (m + 1 <= 512) return 8;
-  return -1;
+  return 8;  // tiles of 512 beyond
 }
 
 hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st) {

@@ -909,8 +909,6 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     if (X.n_rows != 1) return fail(ctx, SK_ERR_INVALID, "4-D stem kernel takes single sequences");
     if (kp->bp_model == 0 && !X.has_bp)
       return fail(ctx, SK_ERR_INVALID, "4-D stem kernel with bp_model 0 needs base pairs");
-    if (sk::stem4d_cpl(X.len) < 0)
-      return fail(ctx, SK_ERR_UNSUPPORTED, "4-D stem kernel: sequence longer than 511");
     stem4d_tables(X, kp, bp, chr);
     if (ali)  // PairHMM's char2rna asserts on anything else (phmm.cpp:247-258)
       for (int a = 0; a < X.len; ++a)
@@ -959,13 +957,18 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   SK_HIP(ctx, hipMemcpyAsync(d_ch, chall.data(), chall.size(), hipMemcpyHostToDevice, S));
   SK_HIP(ctx, hipMemcpyAsync(d_gp, gp.data(), gp.size() * 8, hipMemcpyHostToDevice, S));
   const int cpl = sk::stem4d_cpl(max_m);
+  // |y| >= 512: the kernel sweeps k tiles of 512 and hands each tile's first
+  // K3/G3 column to the next through per-item boundary columns
+  const bool ktiles = max_m + 1 > 64 * cpl;
+  const int64_t kb_stride = ktiles ? 4 * (int64_t)(max_m + 1) : 0;
   double total_ms = 0.0;
   int launches = 0;
   Stem4dBatch& Bt = ctx->s4d;
   for (int64_t b0 = 0; b0 < n;) {
     // pairs of this batch and their scratch
     std::vector<sk::Stem4dPair> prs;
-    double bytes = 0.0;
+    double bytes = 0.0;     // rings + boundary columns (the budget)
+    size_t ring_bytes = 0;  // rings only: pair p's at scratch_off, boundary columns after all
     int64_t b1 = b0;
     int maxn = 0;
     while (b1 < n && prs.size() < 4096) {
@@ -974,10 +977,12 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       p.n = xs_->ex[x[q]].len;
       p.m = ys_->ex[y[q]].len;
       p.plane_doubles = stem4d_plane_doubles(p.m);
-      const double pb = 3.0 * (p.n + 1) * 4.0 * (double)p.plane_doubles * 8.0;
+      const size_t rb = (size_t)3 * (p.n + 1) * 4 * (size_t)p.plane_doubles * 8;
+      const double pb = (double)rb + (double)(p.n + 1) * (double)kb_stride * 8.0;
       if (!prs.empty() && bytes + pb > budget) break;
-      p.scratch_off = (int64_t)(bytes / 8.0);
+      p.scratch_off = (int64_t)(ring_bytes / 8);
       bytes += pb;
+      ring_bytes += rb;
       p.x_bp = tx[x[q]].bp;
       p.x_chr = tx[x[q]].chr;
       p.y_bp = ty[y[q]].bp;
@@ -1023,7 +1028,9 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     if (!ali_phmm) n_band = blo.size();
     const size_t phmm_bytes =
         ali_phmm ? prs.size() * sk::phmm_pair_bytes(max_n1, max_m1) : 0;
-    rc = ensure_scratch(ctx, std::max((size_t)bytes + 64, phmm_bytes));
+    // boundary columns after the rings: at most the d1 = 0 launch's items
+    const size_t kb_bytes = ktiles ? (size_t)(ioff[1] - ioff[0]) * (size_t)kb_stride * 8 : 0;
+    rc = ensure_scratch(ctx, std::max(ring_bytes + kb_bytes + 64, phmm_bytes));
     if (rc) return rc;
     if (Bt.cap_pairs < prs.size() || Bt.cap_items < items.size()) {
       if (Bt.pairs) (void)hipFree(Bt.pairs);
@@ -1065,6 +1072,8 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     L.out = out_dev;
     L.band_lo = n_band ? Bt.band : nullptr;
     L.band_hi = n_band ? Bt.band + Bt.cap_band : nullptr;
+    L.kbound = ktiles ? ctx->scratch + ring_bytes / 8 : nullptr;
+    L.kbound_stride = kb_stride;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     if (ali_phmm) {
       sk::PhmmLaunch H;
