@@ -268,6 +268,42 @@ int sk_format_libsvm(const double *matrix, int32_t rows, int32_t cols,
  * Vienna pf_fold; out gets n*(n-1)/2 doubles in the packed layout above. */
 int sk_fold_synthetic(const char *seq, int32_t n, int32_t no_gu, double *out);
 
+/* McCaskill base-pairing probabilities on the GPU, one workgroup per
+ * sequence (csrc/kernels/fold.hip).  Replaces ViennaRNA pf_fold as the
+ * reference calls it: BPMatrix FOLD, common/bpmatrix.cpp:151-177 (per row of
+ * an alignment, :404-414), PFWrapper::fold, common/pf_wrapper.cpp:15-36.
+ * Loop model: the Turner-1999 core ViennaRNA 1.x compiles in (stacks,
+ * hairpin / bulge / interior initiation, Ninio asymmetry, terminal AU/GU,
+ * linear multiloop; no mismatch, dangle or special-loop tables: its
+ * parameter files are not available, so parity against ViennaRNA is
+ * unpinned -- DESIGN.md §9).  seqs[k]: any case, T as U, other characters
+ * never pair.  out: for each k in order, n_k(n_k-1)/2 doubles in the packed
+ * layout of sk_dataset_add, concatenated.  log_z (optional): ln Z per
+ * sequence.  flags: SK_FOLD_NO_GU (--noGU), SK_FOLD_NO_CLOSING_GU
+ * (--noClosingGU); SK_FOLD_NO_LONELY_PAIRS (--noLonelyPairs) is
+ * SK_ERR_UNSUPPORTED.  Sequences up to ~1,400 nt (SK_ERR_UNSUPPORTED when Z
+ * leaves the double range). */
+#define SK_FOLD_NO_GU 1
+#define SK_FOLD_NO_CLOSING_GU 2
+#define SK_FOLD_NO_LONELY_PAIRS 4
+int sk_fold_mccaskill(sk_context *ctx, int32_t n, const char *const *seqs, int32_t flags,
+                      double *out, double *log_z);
+/* n examples of n_rows equal-length rows (rows[i*n_rows + r]), built on
+ * n_threads host threads (0 = hardware concurrency) from the caller's
+ * per-row bpp (bpp_rows[i*n_rows + r], layout of sk_dataset_add; ignored
+ * when use_bp = 0).  Parallel form of the reference's load loop
+ * (common/framework.h:308-353 + DataLoader<MData>::get,
+ * stem_kernel_lite/data.cpp:548-586). */
+int sk_dataset_add_batch(sk_dataset *ds, int32_t n, int32_t n_rows, const char *const *rows,
+                         const double *const *bpp_rows, const char *const *labels, float th,
+                         int32_t use_bp, int32_t n_threads);
+/* Same, folding every gap-erased row with sk_fold_mccaskill on ctx's GPU
+ * first: the engine's whole input path (MData(ma, th, pf_scale, opts),
+ * data.cpp:324-345, with BPMatrix FOLD) without ViennaRNA. */
+int sk_dataset_add_folded(sk_context *ctx, sk_dataset *ds, int32_t n, int32_t n_rows,
+                          const char *const *rows, const char *const *labels, float th,
+                          int32_t fold_flags, int32_t n_threads);
+
 /* BPLA gradients, the bpla_optimizer's per-pair step: for k < n_pairs,
  * value[k] = BPLAKernel::compute_gradients(xs[x[k]], ys[y[k]], score_table,
  * {alpha, beta, gap, ext}, d) and grad[4k..4k+3] = d (d/d alpha, beta, gap,

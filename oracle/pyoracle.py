@@ -259,3 +259,48 @@ def bpla_gradients(x: OMData, y: OMData, alpha, beta, gap, ext, table16):
     v = oracle().orc_bpla_gradients(x.h, y.h, alpha, beta, gap, ext, t.ctypes.data_as(_D),
                                     d.ctypes.data_as(_D))
     return v, d[:4].copy(), float(d[4])
+
+
+# ------------------------------------------------------------------ McCaskill fold
+def _fold_lib():
+    L = oracle()
+    if not getattr(L, "_fold_bound", False):
+        L.orc_fold_mccaskill.restype = C.c_double
+        L.orc_fold_mccaskill.argtypes = [C.c_char_p, C.c_int, C.c_int, _D]
+        L.orc_fold_enum.restype = C.c_double
+        L.orc_fold_enum.argtypes = [C.c_char_p, C.c_int, C.c_int, _D, C.POINTER(C.c_long)]
+        L.orc_fold_structure_energy.restype = C.c_double
+        L.orc_fold_structure_energy.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.c_int, C.c_int]
+        L._fold_bound = True
+    return L
+
+
+def fold_mccaskill(seq: str, no_gu=False, no_closing_gu=False):
+    """(ln Z, packed bpp) of the restated McCaskill DP (fold_oracle.c)."""
+    n = len(seq)
+    bpp = np.zeros(max(n * (n - 1) // 2, 1))
+    lz = _fold_lib().orc_fold_mccaskill(seq.encode(), int(no_gu), int(no_closing_gu),
+                                        bpp.ctypes.data_as(_D))
+    return lz, bpp[: n * (n - 1) // 2]
+
+
+def fold_enum(seq: str, no_gu=False, no_closing_gu=False):
+    """(ln Z, packed bpp, number of structures) by exhaustive enumeration."""
+    n = len(seq)
+    bpp = np.zeros(max(n * (n - 1) // 2, 1))
+    cnt = C.c_long()
+    lz = _fold_lib().orc_fold_enum(seq.encode(), int(no_gu), int(no_closing_gu),
+                                   bpp.ctypes.data_as(_D), C.byref(cnt))
+    return lz, bpp[: n * (n - 1) // 2], cnt.value
+
+
+def fold_structure_energy(seq: str, dotbracket: str, no_gu=False, no_closing_gu=False) -> float:
+    st, pt = [], np.full(len(seq), -1, np.int32)
+    for k, c in enumerate(dotbracket):
+        if c == "(":
+            st.append(k)
+        elif c == ")":
+            i = st.pop()
+            pt[i], pt[k] = k, i
+    return _fold_lib().orc_fold_structure_energy(seq.encode(), pt.ctypes.data_as(C.POINTER(C.c_int)),
+                                                 int(no_gu), int(no_closing_gu))

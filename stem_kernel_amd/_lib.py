@@ -80,6 +80,12 @@ SIGNATURES = {
     "sk_format_libsvm": (C.c_int, [_F64P, C.c_int32, C.c_int32, C.POINTER(C.c_char_p),
                                    C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "sk_fold_synthetic": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, _F64P]),
+    "sk_fold_mccaskill": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_char_p), C.c_int32, _F64P, _F64P]),
+    "sk_dataset_add_batch": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_char_p),
+                                       C.POINTER(_F64P), C.POINTER(C.c_char_p), C.c_float,
+                                       C.c_int32, C.c_int32]),
+    "sk_dataset_add_folded": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.POINTER(C.c_char_p),
+                                        C.POINTER(C.c_char_p), C.c_float, C.c_int32, C.c_int32]),
     "sk_random_sequences": (C.c_int, [C.POINTER(C.c_uint64), C.c_int32, C.c_int32, C.c_char_p]),
     "sk_last_timing": (C.c_int, [_P, _F64P, _F64P, _F64P, _I32P]),
     "sk_shard_count": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),

@@ -181,6 +181,26 @@ struct PhmmLaunch {
 size_t phmm_pair_bytes(int n1, int m1);
 hipError_t launch_phmm(const PhmmLaunch& P, hipStream_t st);
 
+// McCaskill fold (fold.hip): one workgroup per sequence
+struct FoldSeq {
+  int64_t seq_off = 0;   // into codes
+  int64_t work_off = 0;  // into work: 10 n^2 + 2 (n + 1) doubles
+  int64_t out_off = 0;   // into out: n (n - 1) / 2 packed probabilities
+  int32_t n = 0, pad = 0;
+};
+struct FoldLaunch {
+  const FoldSeq* seqs = nullptr;
+  const int8_t* codes = nullptr;  // A C G U = 0..3, anything else -1
+  const double* tab = nullptr;    // Boltzmann factors, offsets below (host: fold_tables)
+  int32_t o_st = 0, o_hp = 0, o_bu = 0, o_in = 0, o_ni = 0, o_au = 0, o_ml = 0, o_scp = 0;
+  double log_sc = 0.0;            // ln of the per-nucleotide scale
+  int32_t no_gu = 0, no_closing_gu = 0;
+  double* work = nullptr;
+  double* out = nullptr;
+  double* log_z = nullptr;        // per sequence of the launch (nullptr: not wanted)
+};
+hipError_t launch_fold(const FoldLaunch& P, int n_seqs, hipStream_t st);
+
 enum CombineMode : int32_t {
   kCombineStem = 0,      // K = stem
   kCombineStr = 1,       // K = str

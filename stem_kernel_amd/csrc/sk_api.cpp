@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/stem_kernel.h"
+#include "host/fold_params.h"
 #include "host/sk_internal.h"
 #include "kernels/device_set.h"
 #include "kernels/launch.h"
@@ -2116,6 +2117,216 @@ int sk_fold_synthetic(const char* seq, int32_t n, int32_t no_gu, double* out) {
     return SK_ERR_ALLOC;
   }
   return SK_OK;
+}
+
+// ---------------------------------------------------------------- McCaskill fold (f1)
+namespace {
+
+// Boltzmann factor tables of fold.hip (host/fold_params.h), laid out in one
+// buffer; max_len bounds the hairpin and scale tables.
+void fold_tables(int max_len, sk::FoldLaunch& L, std::vector<double>& t) {
+  using namespace sk::foldp;
+  t.clear();
+  auto bz = [](double e) { return std::exp(-e / kT); };
+  L.o_st = (int32_t)t.size();
+  for (int a = 0; a < 7; ++a)
+    for (int b = 0; b < 7; ++b) t.push_back(a && b ? bz(stack37[a][b]) : 0.0);
+  L.o_hp = (int32_t)t.size();
+  for (int k = 0; k <= max_len + 1; ++k) {
+    if (k < 3) {
+      t.push_back(0.0);
+      continue;
+    }
+    double e = hairpin37[k <= 30 ? k : 30];
+    if (k > 30) e += lxc * std::log((double)k / 30.0);
+    t.push_back(bz(e));
+  }
+  L.o_bu = (int32_t)t.size();
+  for (int k = 0; k <= max_loop; ++k) t.push_back(k ? bz(bulge37[k]) : 0.0);
+  L.o_in = (int32_t)t.size();
+  for (int k = 0; k <= max_loop; ++k) t.push_back(k >= 2 ? bz(interior37[k]) : 0.0);
+  L.o_ni = (int32_t)t.size();
+  for (int k = 0; k <= max_loop; ++k) t.push_back(bz(std::min(max_ninio, ninio * k)));
+  L.o_au = (int32_t)t.size();
+  for (int k = 0; k < 7; ++k) t.push_back(k > 2 ? bz(terminal_au) : 1.0);
+  L.o_ml = (int32_t)t.size();
+  t.push_back(bz(ml_closing + ml_intern));
+  t.push_back(bz(ml_intern));
+  L.o_scp = (int32_t)t.size();
+  for (int k = 0; k <= max_len + 2; ++k) t.push_back(std::exp(log_sc * k));
+  L.log_sc = log_sc;
+}
+
+int8_t fold_code(char ch) {
+  switch (ch) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'U': case 'u': case 'T': case 't': return 3;
+    default: return -1;
+  }
+}
+
+}  // namespace
+
+int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32_t flags,
+                      double* out, double* log_z) {
+  if (!ctx || n < 0 || (n > 0 && (!seqs || !out))) return fail(ctx, SK_ERR_INVALID, "null argument");
+  if (flags & ~(SK_FOLD_NO_GU | SK_FOLD_NO_CLOSING_GU))
+    return fail(ctx, SK_ERR_UNSUPPORTED, "fold: only SK_FOLD_NO_GU / SK_FOLD_NO_CLOSING_GU");
+  if (n == 0) return SK_OK;
+  std::vector<int> len(n);
+  int max_len = 0;
+  for (int32_t k = 0; k < n; ++k) {
+    if (!seqs[k]) return fail(ctx, SK_ERR_INVALID, "null sequence");
+    len[k] = (int)std::strlen(seqs[k]);
+    max_len = std::max(max_len, len[k]);
+  }
+  sk::FoldLaunch L;
+  std::vector<double> tab;
+  fold_tables(max_len, L, tab);
+  L.no_gu = (flags & SK_FOLD_NO_GU) ? 1 : 0;
+  L.no_closing_gu = (flags & SK_FOLD_NO_CLOSING_GU) ? 1 : 0;
+  size_t free_b = 0, total_b = 0;
+  SK_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
+  const double budget = std::min(16e9, 0.4 * (double)free_b);
+  hipStream_t S = ctx->stream;
+  size_t out_host = 0;  // packed output offset of sequence k (host)
+  for (int32_t b0 = 0; b0 < n;) {
+    // batch: sequences whose tables fit the budget (at least one)
+    std::vector<sk::FoldSeq> sq;
+    std::vector<int8_t> codes;
+    size_t work = 0, outn = 0;
+    int32_t b1 = b0;
+    for (; b1 < n; ++b1) {
+      const size_t nn = (size_t)len[b1];
+      const size_t w = 10 * nn * nn + 2 * (nn + 1);
+      if (!sq.empty() && (double)(work + w) * 8.0 > budget) break;
+      sk::FoldSeq f;
+      f.seq_off = (int64_t)codes.size();
+      f.work_off = (int64_t)work;
+      f.out_off = (int64_t)outn;
+      f.n = (int32_t)nn;
+      for (size_t a = 0; a < nn; ++a) codes.push_back(fold_code(seqs[b1][a]));
+      work += w;
+      outn += nn > 1 ? nn * (nn - 1) / 2 : 0;
+      sq.push_back(f);
+    }
+    const int nb = b1 - b0;
+    size_t need = sq.size() * sizeof(sk::FoldSeq) + codes.size() + tab.size() * 8 +
+                  (outn + nb) * 8 + 6 * 256;
+    int rc = ensure_work(ctx, need);
+    if (rc) return rc;
+    rc = ensure_scratch(ctx, std::max<size_t>(work * 8, 64));
+    if (rc) return rc;
+    Arena A{static_cast<char*>(ctx->work), 0, ctx->work_bytes};
+    sk::FoldSeq* d_sq = A.take<sk::FoldSeq>(sq.size());
+    int8_t* d_codes = A.take<int8_t>(std::max<size_t>(codes.size(), 1));
+    double* d_tab = A.take<double>(tab.size());
+    double* d_out = A.take<double>(std::max<size_t>(outn, 1));
+    double* d_lz = A.take<double>(nb);
+    SK_HIP(ctx, hipMemcpyAsync(d_sq, sq.data(), sq.size() * sizeof(sk::FoldSeq), hipMemcpyHostToDevice, S));
+    if (!codes.empty())
+      SK_HIP(ctx, hipMemcpyAsync(d_codes, codes.data(), codes.size(), hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_tab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemsetAsync(ctx->scratch, 0, work * 8, S));
+    SK_HIP(ctx, hipMemsetAsync(d_out, 0, std::max<size_t>(outn, 1) * 8, S));
+    L.seqs = d_sq;
+    L.codes = d_codes;
+    L.tab = d_tab;
+    L.work = ctx->scratch;
+    L.out = d_out;
+    L.log_z = d_lz;
+    SK_HIP(ctx, sk::launch_fold(L, nb, S));
+    std::vector<double> lz(nb);
+    if (outn) SK_HIP(ctx, hipMemcpyAsync(out + out_host, d_out, outn * 8, hipMemcpyDeviceToHost, S));
+    SK_HIP(ctx, hipMemcpyAsync(lz.data(), d_lz, nb * 8, hipMemcpyDeviceToHost, S));
+    SK_HIP(ctx, hipStreamSynchronize(S));
+    for (int k = 0; k < nb; ++k) {
+      if (!std::isfinite(lz[k]))
+        return fail(ctx, SK_ERR_UNSUPPORTED, "fold: partition function out of double range (sequence too long)");
+      if (log_z) log_z[b0 + k] = lz[k];
+    }
+    out_host += outn;
+    b0 = b1;
+  }
+  return SK_OK;
+}
+
+namespace {
+// Threaded DAG builds of n examples of n_rows rows from per-row bpp (caller's
+// or folded), appended to ds; the parallel form of the reference's load loop
+// (common/framework.h:308-353 + DataLoader<MData>::get, data.cpp:548-586).
+int add_examples_threaded(sk_dataset* ds, int32_t n, int32_t n_rows, const char* const* rows,
+                          const double* const* bpp_rows, const char* const* labels, float th,
+                          int use_bp, int32_t n_threads) {
+  const size_t base = ds->ex.size();
+  try {
+    ds->ex.resize(base + n);
+    for (int32_t i = 0; i < n; ++i) ds->labels.emplace_back(labels && labels[i] ? labels[i] : "+1");
+  } catch (const std::bad_alloc&) {
+    return SK_ERR_ALLOC;
+  }
+  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  nt = std::max(1, std::min(nt, std::max<int32_t>(n, 1)));
+  std::atomic<int32_t> next(0), status(SK_OK);
+  auto work = [&]() {
+    for (;;) {
+      const int32_t i = next.fetch_add(1);
+      if (i >= n || status.load() != SK_OK) return;
+      try {
+        sk::build_example(ds->ex[base + i], n_rows, rows + (size_t)i * n_rows,
+                          use_bp ? bpp_rows + (size_t)i * n_rows : nullptr, th, use_bp != 0);
+      } catch (...) {
+        status.store(SK_ERR_INVALID);
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  if (status.load() != SK_OK) {
+    ds->ex.resize(base);
+    ds->labels.resize(base);
+  }
+  return status.load();
+}
+}  // namespace
+
+int sk_dataset_add_batch(sk_dataset* ds, int32_t n, int32_t n_rows, const char* const* rows,
+                         const double* const* bpp_rows, const char* const* labels, float th,
+                         int32_t use_bp, int32_t n_threads) {
+  if (!ds || n < 0 || n_rows < 1 || (n > 0 && (!rows || (use_bp && !bpp_rows)))) return SK_ERR_INVALID;
+  if (ds->uploaded) return SK_ERR_INVALID;
+  return add_examples_threaded(ds, n, n_rows, rows, bpp_rows, labels, th, use_bp, n_threads);
+}
+
+int sk_dataset_add_folded(sk_context* ctx, sk_dataset* ds, int32_t n, int32_t n_rows,
+                          const char* const* rows, const char* const* labels, float th,
+                          int32_t fold_flags, int32_t n_threads) {
+  if (!ctx || !ds || n < 0 || n_rows < 1 || (n > 0 && !rows)) return fail(ctx, SK_ERR_INVALID, "null argument");
+  if (ds->uploaded) return fail(ctx, SK_ERR_INVALID, "dataset already uploaded");
+  const size_t nr = (size_t)n * n_rows;
+  // fold the gap-erased, lower-cased rows (common/bpmatrix.cpp:404-414)
+  std::vector<std::string> erased(nr);
+  std::vector<const char*> eptr(nr);
+  std::vector<size_t> off(nr + 1, 0);
+  for (size_t r = 0; r < nr; ++r) {
+    if (!rows[r]) return fail(ctx, SK_ERR_INVALID, "null row");
+    for (const char* p = rows[r]; *p; ++p)
+      if (*p != '-') erased[r].push_back((char)std::tolower((unsigned char)*p));
+    eptr[r] = erased[r].c_str();
+    const size_t m = erased[r].size();
+    off[r + 1] = off[r] + (m > 1 ? m * (m - 1) / 2 : 0);
+  }
+  std::vector<double> bpp(std::max<size_t>(off[nr], 1));
+  int rc = sk_fold_mccaskill(ctx, (int32_t)nr, eptr.data(), fold_flags, bpp.data(), nullptr);
+  if (rc) return rc;
+  std::vector<const double*> bptr(nr);
+  for (size_t r = 0; r < nr; ++r) bptr[r] = bpp.data() + off[r];
+  rc = add_examples_threaded(ds, n, n_rows, rows, bptr.data(), labels, th, 1, n_threads);
+  return rc ? fail(ctx, rc, "example build failed") : SK_OK;
 }
 
 int sk_random_sequences(uint64_t* state, int32_t n_seqs, int32_t len, char* out) {

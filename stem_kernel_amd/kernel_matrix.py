@@ -321,6 +321,52 @@ class Dataset:
                                                   threads))
         return ds
 
+    def add_batch(self, alns: Sequence[Sequence[str]], bpp_rows=None, labels=None,
+                  th: float = 0.01, use_bp: bool = True, threads: int = 0) -> None:
+        """Append alignments of equal row count, built on host threads from
+        the caller's per-row bpp (``bpp_rows[i][r]``, packed, of the
+        gap-erased row; sk_dataset_add_batch)."""
+        n = len(alns)
+        nr = len(alns[0]) if n else 1
+        if any(len(a) != nr for a in alns):
+            raise ValueError("add_batch needs the same number of rows per alignment")
+        flat = [r.encode() for a in alns for r in a]
+        rarr = (C.c_char_p * max(len(flat), 1))(*flat)
+        larr = None if labels is None else (C.c_char_p * n)(*[l.encode() for l in labels])
+        keep, barr = [], None
+        if use_bp:
+            barr = (C.POINTER(C.c_double) * max(n * nr, 1))()
+            for i in range(n):
+                for r in range(nr):
+                    b = np.ascontiguousarray(bpp_rows[i][r], dtype=np.float64)
+                    if b.size == 0:
+                        b = np.zeros(1)
+                    keep.append(b)
+                    barr[i * nr + r] = b.ctypes.data_as(C.POINTER(C.c_double))
+        check(lib().sk_dataset_add_batch(self._h, n, nr, rarr, barr, larr, C.c_float(th),
+                                         int(use_bp), threads))
+
+    @classmethod
+    def folded(cls, ctx: "Context", alns, labels=None, th: float = 0.01, no_gu: bool = False,
+               no_closing_gu: bool = False, threads: int = 0):
+        """Examples whose rows are folded on ctx's GPU (sk_fold_mccaskill, the
+        engine's McCaskill in place of Vienna pf_fold) and built on host
+        threads (sk_dataset_add_folded).  ``alns``: sequences or alignments
+        of equal row count."""
+        alns = [[a] if isinstance(a, str) else list(a) for a in alns]
+        ds = cls()
+        n = len(alns)
+        nr = len(alns[0]) if n else 1
+        if any(len(a) != nr for a in alns):
+            raise ValueError("folded needs the same number of rows per alignment")
+        flat = [r.encode() for a in alns for r in a]
+        rarr = (C.c_char_p * max(len(flat), 1))(*flat)
+        larr = None if labels is None else (C.c_char_p * n)(*[l.encode() for l in labels])
+        flags = (1 if no_gu else 0) | (2 if no_closing_gu else 0)
+        ctx._chk(lib().sk_dataset_add_folded(ctx.handle, ds._h, n, nr, rarr, larr, C.c_float(th),
+                                             flags, threads))
+        return ds
+
     def __len__(self):
         return lib().sk_dataset_size(self._h)
 
@@ -393,6 +439,27 @@ class Context:
 
     def _chk(self, rc):
         return check(rc, self._h)
+
+    def fold(self, seqs: Sequence[str], no_gu: bool = False, no_closing_gu: bool = False,
+             log_z: bool = False):
+        """McCaskill base-pairing probabilities of every sequence on this GPU
+        (sk_fold_mccaskill): a list of packed upper triangles, plus ln Z per
+        sequence when ``log_z``."""
+        seqs = list(seqs)
+        n = len(seqs)
+        sizes = [len(s) * (len(s) - 1) // 2 for s in seqs]
+        out = np.zeros(max(sum(sizes), 1))
+        lz = np.zeros(max(n, 1))
+        sarr = (C.c_char_p * max(n, 1))(*[s.encode() for s in seqs])
+        flags = (1 if no_gu else 0) | (2 if no_closing_gu else 0)
+        self._chk(lib().sk_fold_mccaskill(self._h, n, sarr, flags,
+                                          out.ctypes.data_as(C.POINTER(C.c_double)),
+                                          lz.ctypes.data_as(C.POINTER(C.c_double))))
+        res, o = [], 0
+        for z in sizes:
+            res.append(out[o:o + z].copy())
+            o += z
+        return (res, lz[:n]) if log_z else res
 
     def upload(self, ds: Dataset):
         self._chk(lib().sk_dataset_upload(self._h, ds.handle))
