@@ -23,9 +23,17 @@ HDRS := $(wildcard $(ROOT)stem_kernel_amd/csrc/*/*.h) $(ROOT)include/stem_kernel
 HOST_OBJ := $(patsubst $(ROOT)stem_kernel_amd/csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC) $(API_SRC))
 HIP_OBJ := $(patsubst $(ROOT)stem_kernel_amd/csrc/%.hip,$(BUILD)/%.o,$(HIP_SRC))
 
-all: lib oracle
+all: lib cli oracle
 
 lib: $(LIB)
+
+# the reference's stem_kernel_lite CLI over the engine (host C++, links the library)
+CLI := $(ROOT)stem_kernel_amd/bin/stem_kernel_lite
+cli: $(CLI)
+$(CLI): $(ROOT)stem_kernel_amd/csrc/cli/stem_kernel_lite.cpp $(ROOT)include/stem_kernel_compat.hpp $(ROOT)include/stem_kernel.h $(LIB)
+	@mkdir -p $(dir $@)
+	g++ -O2 -std=c++17 -Wall -Wextra -I$(ROOT)include $< -L$(ROOT)stem_kernel_amd -lstem_kernel_amd -lz \
+	  -Wl,-rpath,'$$ORIGIN/..' -o $@
 
 $(BUILD)/%.o: $(ROOT)stem_kernel_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p $(dir $@)
@@ -46,10 +54,10 @@ oracle:
 	$(MAKE) -C $(ROOT)oracle
 
 clean:
-	rm -rf $(BUILD) $(LIB)
+	rm -rf $(BUILD) $(LIB) $(CLI)
 	$(MAKE) -C $(ROOT)oracle clean
 
-.PHONY: all lib oracle clean
+.PHONY: all lib cli oracle clean
 
 # diagnostic build with in-kernel phase stamps (never the shipped library)
 STAMPS_LIB := $(ROOT)build/libstem_kernel_amd_stamps.so

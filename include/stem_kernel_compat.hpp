@@ -30,12 +30,14 @@
 // over RCCL (sk_gram_sharded), every rank receiving the whole matrix.
 //
 // What differs, by necessity:
-//   - base-pairing probabilities: ViennaRNA's pf_fold is not part of the
-//     engine; MData folds each gap-erased, lowercased row
-//     with BPMatrix::Options::fold (default: sk_fold_synthetic, the
-//     Nussinov-Boltzmann stand-in) and averages alignment rows as the
-//     reference does (common/bpmatrix.cpp:306-342) -- plug a real folder in
-//     through that hook;
+//   - base-pairing probabilities: ViennaRNA's pf_fold is replaced by the
+//     engine's GPU McCaskill (sk_fold_mccaskill, SURVEY.md §8 f1: the
+//     Turner-1999 core loop model, parity against ViennaRNA unpinned); MData
+//     folds each gap-erased, lowercased row with it (honouring --noGU and
+//     --noClosingGU; --noLonelyPairs and --use-alifold are refused) and
+//     averages alignment rows as the reference does
+//     (common/bpmatrix.cpp:306-342).  BPMatrix::Options::fold plugs in any
+//     other folder (skc::synthetic_fold: the Nussinov-Boltzmann stand-in);
 //   - elapsed times are wall-clock seconds (the reference sums boost::timer
 //     CPU seconds);
 //   - errors are thrown as const char* like the reference, carrying the
@@ -85,9 +87,13 @@ struct BPMatrix {
          no_LonelyPairs = false;
     uint n_samples = 0;
     bool use_pf_scale_mfe = false;
-    FoldFn fold;  // empty: synthetic_fold
+    FoldFn fold;  // empty: the engine's GPU McCaskill (engine_fold)
   };
 };
+
+// the engine's GPU McCaskill fold of one example's rows (defined after Engine)
+inline void engine_fold(const std::vector<std::string>& rows, const BPMatrix::Options& opts,
+                        std::vector<std::vector<double>>& out);
 
 // The reference's MData (stem_kernel_lite/data.h:26-55) as the engine
 // consumes it: the alignment rows and each row's folded matrix; the DAG is
@@ -103,13 +109,20 @@ struct MData {
   MData(const std::list<std::string>& ma, float th_, float /*pf_scale*/,
         const BPMatrix::Options& opts)
       : rows(ma.begin(), ma.end()), th(th_), use_bp(true) {
+    std::vector<std::string> erased;
     for (const std::string& r : rows) {
       std::string s;
       for (char c : r)
         if (c != '-') s.push_back((char)std::tolower((unsigned char)c));
-      bpp.emplace_back();
-      if (opts.fold) opts.fold(s, opts.no_GU, bpp.back());
-      else synthetic_fold(s, opts.no_GU, bpp.back());
+      erased.push_back(s);
+    }
+    if (opts.fold) {
+      for (const std::string& s : erased) {
+        bpp.emplace_back();
+        opts.fold(s, opts.no_GU, bpp.back());
+      }
+    } else {
+      engine_fold(erased, opts, bpp);
     }
   }
   // MData(ma): no base-pairing information (string kernels only)
@@ -163,8 +176,10 @@ class DataLoader<MData> {
       else if (l.compare(0, 2, "a ") == 0) fmt = SK_FMT_MAF;
     }
     if (fmt < 0 || sk_seqfile_read(filename, fmt, &f_) != SK_OK) {
-      msg_ = std::string(filename) + ": no such file";
-      throw msg_.c_str();
+      // the message outlives this (never constructed) loader
+      static thread_local std::string msg;
+      msg = std::string(filename) + ": no such file";
+      throw msg.c_str();
     }
   }
   float th_;
@@ -172,7 +187,6 @@ class DataLoader<MData> {
   bool use_bp_;
   sk_seqfile* f_ = nullptr;
   int64_t next_ = 0;
-  std::string msg_;
 };
 
 // DataLoaderFactory<LD>  stem_kernel_lite/data.h:104-133
@@ -287,6 +301,33 @@ class Engine {
   sk_context* ctx_ = nullptr;
   std::map<uint64_t, std::unique_ptr<sk_dataset, int (*)(sk_dataset*)>> cache_;
 };
+
+inline void engine_fold(const std::vector<std::string>& rows, const BPMatrix::Options& opts,
+                        std::vector<std::vector<double>>& out) {
+  if (opts.no_LonelyPairs) throw "--noLonelyPairs is not supported by the engine's fold";
+  if (opts.alifold || opts.contrafold || opts.n_samples > 0)
+    throw "only the FOLD method (McCaskill per row) is supported by the engine";
+  std::vector<const char*> p;
+  size_t total = 0;
+  for (const std::string& s : rows) {
+    p.push_back(s.c_str());
+    total += s.size() > 1 ? s.size() * (s.size() - 1) / 2 : 0;
+  }
+  std::vector<double> all(std::max<size_t>(total, 1));
+  sk_context* ctx = Engine::get().ctx();
+  check(sk_fold_mccaskill(ctx, (int32_t)p.size(), p.data(),
+                          (opts.no_GU ? SK_FOLD_NO_GU : 0) | (opts.no_closingGU ? SK_FOLD_NO_CLOSING_GU : 0),
+                          all.data(), nullptr),
+        ctx);
+  out.clear();
+  size_t o = 0;
+  for (const std::string& s : rows) {
+    const size_t z = s.size() > 1 ? s.size() * (s.size() - 1) / 2 : 0;
+    out.emplace_back(all.begin() + o, all.begin() + o + z);
+    if (out.back().empty()) out.back().assign(1, 0.0);
+    o += z;
+  }
+}
 
 // ------------------------------------------------------------------ kernels
 // Each kernel carries its sk_kernel_params; operator() evaluates one pair on

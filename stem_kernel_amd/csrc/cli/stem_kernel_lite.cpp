@@ -1,0 +1,411 @@
+// stem_kernel_lite: the reference's kernel-matrix CLI (stem_kernel_lite/main.cpp
+// with common/framework.{h,cpp}'s Options, App::train / App::predict and
+// Output) over the MI355X engine, through the drop-in header
+// include/stem_kernel_compat.hpp.  Same flags, positional arguments, console
+// messages and output files:
+//
+//   stem_kernel_lite [options] output [label1 train1] ... [--test] [label1] [test1] ...
+//
+// Train mode writes the libsvm precomputed-kernel matrix of the training
+// examples (KernelMatrix::print, common/kernel_matrix.cpp:756-770; .gz via
+// zlib); predict mode (--test) writes one kernel row per test example
+// (Output::kernel_output, common/framework.cpp:193-209), optionally only the
+// support vectors of --model files (load_sv_index, libsvm/model.cpp:56-99),
+// and their self values to --norm (Output::norm_output).
+//
+// Differences, by necessity: base-pairing probabilities come from the
+// engine's GPU McCaskill (sk_fold_mccaskill) instead of ViennaRNA;
+// --noLonelyPairs, --use-alifold and --predict (libsvm's SVM, outside the
+// engine) are refused; .bz2 output is refused (no libbz2 headers here).  The
+// reference's default kernel (SuStemStr without --log) only estimates memory
+// and never runs App::execute (main.cpp:176-183, `//res = app.execute();`);
+// here every kernel choice computes its matrix.
+#include <zlib.h>
+
+#include <algorithm>
+#include <cctype>
+#include <chrono>
+#include <cmath>
+#include <functional>
+#include <memory>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../../include/stem_kernel_compat.hpp"
+
+namespace {
+
+struct Options {  // common/framework.h:37-62 + main.cpp:85-151
+  // framework Options
+  unsigned n_th = 1;
+  bool normalize = false;
+  std::string norm_output;
+  bool predict_only = false;
+  std::vector<std::string> trained_model_file, predict_output;
+  // folding (BPMatrix::Options)
+  skc::BPMatrix::Options bp;
+  // kernel
+  bool no_ribosum = false, no_string = false, use_log = false;
+  float th = 0.01f;
+  double beta = 0.3, loop_gap = 0.2, stack = 1.3, covar = 0.8;
+  unsigned len_band = 10;
+  double alpha = 0.2, gap = 0.8, str_match = 1.0, str_mismatch = 0.8;
+  // positional
+  std::string output;
+  bool predict_mode = false;
+  std::vector<std::string> labels, files, ts_labels, ts_files;
+  std::vector<unsigned> sv_index;
+};
+
+const char* kUsage =
+    "Options:\n"
+    "  -h [ --help ]               show this message\n"
+    "  -t [ --threads ] arg (=1)   set the number of threads\n"
+    "  -n [ --normalize ]          normalize the kernel matrix\n"
+    "  -x [ --norm ] arg           set the filename for norms of test examples\n"
+    "  --no-matrix                 do not output matrix\n"
+    "  --model arg                 the model file trained by svm-train if you already have\n"
+    "  --predict arg               output file name of prediction results\n\n"
+    "Kernel Options:\n"
+    "  --no-ribosum                do not use the RIBOSUM substitution matrix\n"
+    "  --no-string                 do not convolute the string kernel\n"
+    "  --log                       use the logarithm of the kernel\n\n"
+    "Options for the stem kernel:\n"
+    "  -p [ --basepair ] arg (=0.01)  set the threshold of basepairing probability\n"
+    "  -b [ --beta ] arg (=0.3)       weight of the RIBOSUM for the stem kernel\n"
+    "  -g [ --loop-gap ] arg (=0.2)   gap weight for loop regions\n"
+    "  -s [ --stack ] arg (=1.3)      match weight for stacking base pairs (with --no-ribosum)\n"
+    "  -v [ --covariant ] arg (=0.8)  substitution (covariant) weight for base pairs (with\n"
+    "                                 --no-ribosum)\n"
+    "  --length-band arg (=10)        the band of difference of the length between bases\n\n"
+    "Options for the string kernel:\n"
+    "  -a [ --alpha ] arg (=0.2)      weight of the RIBOSUM for the string kernel\n"
+    "  -G [ --gap ] arg (=0.8)        gap weight for the string kernel\n"
+    "  --match arg (=1.0)             match weight for the string kernel (with --no-ribosum)\n"
+    "  --mismatch arg (=0.8)          substitution (mismatch) weight for the string kernel (with\n"
+    "                                 --no-ribosum)\n\n"
+    "Folding Options:\n"
+    "  --noGU                      disallow GU wobble base-pairs\n"
+    "  --noClosingGU               disallow closing GU base-pairs\n"
+    "  --noLonelyPairs             disallow lonely base-pairs (not supported by the engine)\n"
+    "  --use-alifold               use pf_alifold (not supported by the engine)\n"
+    "  --pf-scale                  calculate appropriciate pf_scales using MFE (no effect)\n";
+
+// boost::program_options-like parsing with allow_unregistered(): known
+// options are consumed (long "--name value" / "--name=value", short "-x
+// value" / "-xvalue"), everything else -- including "--test" -- is kept in
+// order as extra arguments (main.cpp:152-163).
+bool parse(int argc, char** argv, Options& o, std::vector<std::string>& extra, bool& help) {
+  struct Opt {
+    const char* name;
+    char shrt;
+    bool takes_value;
+    std::function<void(const std::string&)> set;
+  };
+  auto to_f = [](const std::string& v) { return std::stod(v); };
+  std::vector<Opt> opts = {
+      {"help", 'h', false, [&](const std::string&) { help = true; }},
+      {"threads", 't', true, [&](const std::string& v) { o.n_th = (unsigned)std::stoul(v); }},
+      {"normalize", 'n', false, [&](const std::string&) { o.normalize = true; }},
+      {"norm", 'x', true, [&](const std::string& v) { o.norm_output = v; }},
+      {"no-matrix", 0, false, [&](const std::string&) { o.predict_only = true; }},
+      {"model", 0, true, [&](const std::string& v) { o.trained_model_file.push_back(v); }},
+      {"predict", 0, true, [&](const std::string& v) { o.predict_output.push_back(v); }},
+      {"no-ribosum", 0, false, [&](const std::string&) { o.no_ribosum = true; }},
+      {"no-string", 0, false, [&](const std::string&) { o.no_string = true; }},
+      {"log", 0, false, [&](const std::string&) { o.use_log = true; }},
+      {"basepair", 'p', true, [&](const std::string& v) { o.th = (float)to_f(v); }},
+      {"beta", 'b', true, [&](const std::string& v) { o.beta = to_f(v); }},
+      {"loop-gap", 'g', true, [&](const std::string& v) { o.loop_gap = to_f(v); }},
+      {"stack", 's', true, [&](const std::string& v) { o.stack = to_f(v); }},
+      {"covariant", 'v', true, [&](const std::string& v) { o.covar = to_f(v); }},
+      {"length-band", 0, true, [&](const std::string& v) { o.len_band = (unsigned)std::stoul(v); }},
+      {"alpha", 'a', true, [&](const std::string& v) { o.alpha = to_f(v); }},
+      {"gap", 'G', true, [&](const std::string& v) { o.gap = to_f(v); }},
+      {"match", 0, true, [&](const std::string& v) { o.str_match = to_f(v); }},
+      {"mismatch", 0, true, [&](const std::string& v) { o.str_mismatch = to_f(v); }},
+      {"noGU", 0, false, [&](const std::string&) { o.bp.no_GU = true; }},
+      {"noClosingGU", 0, false, [&](const std::string&) { o.bp.no_closingGU = true; }},
+      {"noLonelyPairs", 0, false, [&](const std::string&) { o.bp.no_LonelyPairs = true; }},
+      {"use-alifold", 0, false, [&](const std::string&) { o.bp.alifold = true; }},
+      {"pf-scale", 0, false, [&](const std::string&) { o.bp.use_pf_scale_mfe = true; }},
+  };
+  for (int k = 1; k < argc; ++k) {
+    const std::string a = argv[k];
+    const Opt* hit = nullptr;
+    std::string val;
+    bool inline_val = false;
+    if (a.size() > 2 && a[0] == '-' && a[1] == '-') {
+      std::string name = a.substr(2);
+      const size_t eq = name.find('=');
+      if (eq != std::string::npos) {
+        val = name.substr(eq + 1);
+        name = name.substr(0, eq);
+        inline_val = true;
+      }
+      for (const Opt& p : opts)
+        if (name == p.name) hit = &p;
+    } else if (a.size() >= 2 && a[0] == '-' && a[1] != '-' && !std::isdigit((unsigned char)a[1])) {
+      for (const Opt& p : opts)
+        if (p.shrt && a[1] == p.shrt) hit = &p;
+      if (hit && a.size() > 2) {
+        val = a.substr(2);
+        inline_val = true;
+      }
+    }
+    if (!hit) {  // unregistered: an extra argument
+      extra.push_back(a);
+      continue;
+    }
+    if (hit->takes_value) {
+      if (!inline_val) {
+        if (k + 1 >= argc) {
+          std::cerr << "the required argument for option '--" << hit->name << "' is missing" << std::endl;
+          return false;
+        }
+        val = argv[++k];
+      }
+      try {
+        hit->set(val);
+      } catch (...) {
+        std::cerr << "the argument ('" << val << "') for option '--" << hit->name << "' is invalid"
+                  << std::endl;
+        return false;
+      }
+    } else {
+      hit->set("");
+    }
+  }
+  return true;
+}
+
+// Options::parse_extra_args (common/framework.cpp:48-93)
+void parse_extra_args(Options& o, const std::vector<std::string>& extra) {
+  o.output = extra[0];
+  size_t x = extra.size();
+  for (size_t k = 0; k < extra.size(); ++k)
+    if (extra[k] == "--test") x = k;
+  o.predict_mode = x != extra.size();
+  for (size_t i = 1; i + 1 < x + (o.predict_mode ? 0 : 1) && i + 1 < extra.size(); i += 2) {
+    o.labels.push_back(extra[i]);
+    o.files.push_back(extra[i + 1]);
+  }
+  if (o.predict_mode)
+    for (size_t i = x + 1; i + 1 < extra.size(); i += 2) {
+      o.ts_labels.push_back(extra[i]);
+      o.ts_files.push_back(extra[i + 1]);
+    }
+}
+
+// load_sv_index (libsvm/model.cpp:56-99): the "SV" section's "coef 0:idx"
+// lines, 1-based -> 0-based, merged over models, sorted, unique
+void load_sv_index(std::vector<unsigned>& sv, const std::vector<std::string>& models) {
+  static std::string err;
+  for (const std::string& m : models) {
+    std::ifstream in(m);
+    if (!in) {
+      err = m + ": no such file";
+      throw err.c_str();
+    }
+    std::string line;
+    bool in_sv = false, seen = false;
+    while (std::getline(in, line)) {
+      if (!in_sv) {
+        if (line == "SV") in_sv = seen = true;
+        continue;
+      }
+      std::istringstream ls(line);
+      std::string coef, idx;
+      ls >> coef >> idx;
+      if (idx.compare(0, 2, "0:") != 0) {
+        err = m + ": bad format";
+        throw err.c_str();
+      }
+      sv.push_back((unsigned)std::stoul(idx.substr(2)) - 1);
+    }
+    if (!seen) {
+      err = m + ": bad format";
+      throw err.c_str();
+    }
+  }
+  std::sort(sv.begin(), sv.end());
+  sv.erase(std::unique(sv.begin(), sv.end()), sv.end());
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void write_text(const std::string& path, const std::string& text) {
+  static std::string err;
+  if (path.size() >= 4 && path.compare(path.size() - 4, 4, ".bz2") == 0) {
+    err = path + ": bzip2 output is not available in this build";
+    throw err.c_str();
+  }
+  if (path.size() >= 3 && path.compare(path.size() - 3, 3, ".gz") == 0) {
+    gzFile g = gzopen(path.c_str(), "wb");
+    if (!g || gzwrite(g, text.data(), (unsigned)text.size()) != (int)text.size() || gzclose(g) != Z_OK) {
+      err = path + ": cannot open for writing";
+      throw err.c_str();
+    }
+    return;
+  }
+  std::ofstream out(path);
+  if (!out) {
+    err = path + ": cannot open for writing";
+    throw err.c_str();
+  }
+  out << text;
+}
+
+// App<K,LDF> (common/framework.h:100-353) over the compat types
+template <class K>
+class App {
+ public:
+  typedef skc::MData Data;
+  typedef std::pair<std::string, Data> Example;
+  typedef std::vector<Example> ExampleSet;
+  typedef skc::DataLoaderFactory<skc::DataLoader<skc::MData>> LDF;
+
+  App(const K& kernel, const LDF& ldf, const Options& opts) : kernel_(kernel), ldf_(ldf), opts_(opts) {}
+  bool execute() const { return opts_.predict_mode ? predict() : train(); }
+
+ private:
+  bool train() const {
+    ExampleSet ex;
+    load_examples(ex, opts_.labels, opts_.files);
+    skc::KernelMatrix<double> matrix;
+    const double elapsed = matrix.calculate(ex, kernel_, opts_.normalize, opts_.n_th);
+    std::cout << "elapsed time: " << elapsed << "s" << std::endl;
+    std::ostringstream os;
+    matrix.print(os);
+    write_text(opts_.output, os.str());
+    return true;
+  }
+
+  bool predict() const {
+    ExampleSet ex;
+    load_examples(ex, opts_.labels, opts_.files);
+    std::vector<double> diag(ex.size()), vec(ex.size());
+    if (opts_.normalize) {
+      const double e = skc::KernelMatrix<double>::diagonal(diag, ex, opts_.sv_index, kernel_, opts_.n_th);
+      std::cout << "elapsed time for diagonals: " << e << "s" << std::endl;
+    }
+    const bool norm = opts_.normalize || !opts_.norm_output.empty();
+    std::ostringstream kout, tout;
+    unsigned cnt = 0;
+    for (size_t i = 0; i != opts_.ts_files.size(); ++i) {
+      double elapsed = 0.0;
+      std::cout << "predicting " << opts_.ts_files[i] << std::flush;
+      std::unique_ptr<typename LDF::Loader> loader(ldf_.get_loader(opts_.ts_files[i].c_str()));
+      for (;;) {
+        const double t0 = now_s();
+        std::unique_ptr<Data> data(loader->get());
+        elapsed += now_s() - t0;
+        if (!data) break;
+        double self = 0.0;
+        elapsed += skc::KernelMatrix<double>::calculate(vec, Example(opts_.ts_labels[i], *data), ex,
+                                                        opts_.sv_index, kernel_, opts_.n_th,
+                                                        norm ? &self : NULL);
+        if (opts_.normalize)
+          for (size_t j = 0; j != vec.size(); ++j) vec[j] /= std::sqrt(diag[j] * self);
+        ++cnt;
+        // Output::kernel_output / norm_output (common/framework.cpp:193-234)
+        if (!opts_.predict_only) {
+          kout << opts_.ts_labels[i] << " 0:" << cnt << " ";
+          for (size_t j = 0; j != vec.size(); ++j) kout << (j + 1) << ":" << vec[j] << " ";
+          kout << std::endl;
+        }
+        if (!opts_.norm_output.empty()) tout << self << std::endl;
+      }
+      std::cout << " (" << elapsed << "s) done." << std::endl;
+    }
+    if (!opts_.predict_only) write_text(opts_.output, kout.str());
+    if (!opts_.norm_output.empty()) write_text(opts_.norm_output, tout.str());
+    return true;
+  }
+
+  // App::load_examples (common/framework.h:308-353); no globbing: a file
+  // name is taken as given
+  void load_examples(ExampleSet& ex, const std::vector<std::string>& labels,
+                     const std::vector<std::string>& files) const {
+    for (size_t i = 0; i != files.size(); ++i) {
+      double elapsed = 0.0;
+      std::unique_ptr<typename LDF::Loader> loader(ldf_.get_loader(files[i].c_str()));
+      std::cout << "loading " << files[i] << " as label " << labels[i] << std::flush;
+      for (;;) {
+        const double t0 = now_s();
+        std::unique_ptr<Data> d(loader->get());
+        elapsed += now_s() - t0;
+        if (!d) break;
+        ex.push_back(std::make_pair(labels[i], *d));
+      }
+      std::cout << " (" << elapsed << "s) done." << std::endl;
+    }
+  }
+
+  K kernel_;
+  LDF ldf_;
+  const Options& opts_;
+};
+
+template <class K>
+bool run(const K& kernel, const Options& o) {
+  skc::DataLoaderFactory<skc::DataLoader<skc::MData>> ldf(o.th, o.bp);
+  App<K> app(kernel, ldf, o);
+  return app.execute();
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Options o;
+  std::vector<std::string> extra;
+  bool help = false;
+  if (!parse(argc, argv, o, extra, help)) return 1;
+  if (help || extra.size() < 3) {
+    std::cout << "Kernel Matrix Calculator for Stem Kernels" << std::endl
+              << "Usage:" << std::endl
+              << " " << argv[0]
+              << " [options] output [label1 training-data1] ... [--test] [label1] [test-data1] ...\n\n"
+              << kUsage << std::endl;
+    return 1;
+  }
+  parse_extra_args(o, extra);
+  bool res = false;
+  try {
+    if (!o.predict_output.empty())
+      throw "--predict: SVM prediction (libsvm) is outside the engine; run svm-predict on the kernel rows";
+    if (o.bp.no_LonelyPairs) throw "--noLonelyPairs is not supported by the engine's fold";
+    if (o.bp.alifold) throw "--use-alifold is not supported by the engine's fold";
+    if (o.predict_mode && !o.trained_model_file.empty()) load_sv_index(o.sv_index, o.trained_model_file);
+    // kernel choice: main.cpp:166-214
+    if (!o.no_string && !o.no_ribosum) {
+      if (!o.use_log)
+        res = run(skc::SuStemStrKernel<double, skc::MData>(o.alpha, o.beta, o.loop_gap, o.gap, o.len_band), o);
+      else
+        res = run(skc::LSuStemStrKernel<double, skc::MData>(o.alpha, o.beta, o.loop_gap, o.gap, o.len_band), o);
+    } else if (o.no_string && !o.no_ribosum) {
+      if (!o.use_log)
+        res = run(skc::SuStemKernel<double, skc::MData>(o.loop_gap, o.beta, o.len_band), o);
+      else
+        res = run(skc::LSuStemKernel<double, skc::MData>(o.loop_gap, o.beta, o.len_band), o);
+    } else if (!o.no_string && o.no_ribosum) {
+      res = run(skc::SiStemStrKernel<double, skc::MData>(o.loop_gap, o.stack, o.covar, o.gap, o.str_match,
+                                                         o.str_mismatch, o.len_band),
+                o);
+    } else {
+      res = run(skc::SiStemKernel<double, skc::MData>(o.loop_gap, o.stack, o.covar, o.len_band), o);
+    }
+  } catch (const char* str) {
+    std::cout << str << std::endl;
+  }
+  return res ? 0 : 1;
+}

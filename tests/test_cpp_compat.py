@@ -49,8 +49,9 @@ def test_compat_app_matches_engine(gpu_ctx, tmp_path, normalize):
     gram = np.array([[float(v) for v in out[i].split()] for i in range(n)])
     rows = np.array([[float(v) for v in out[n + t].split()] for t in range(len(test))])
     kern = ska.SuStemStrKernel()
-    ds = ska.Dataset.from_sequences(train, bpp=[ska.fold(s.lower()) for s in train])
-    dt = ska.Dataset.from_sequences(test, bpp=[ska.fold(s.lower()) for s in test])
+    # MData folds with the engine's GPU McCaskill (BPMatrix FOLD without ViennaRNA)
+    ds = ska.Dataset.from_sequences(train, bpp=gpu_ctx.fold([s.lower() for s in train]))
+    dt = ska.Dataset.from_sequences(test, bpp=gpu_ctx.fold([s.lower() for s in test]))
     assert np.array_equal(gram, gpu_ctx.gram(ds, kern, normalize=bool(normalize)))
     diag = gpu_ctx.diagonal(ds, kern)
     for t in range(len(test)):
