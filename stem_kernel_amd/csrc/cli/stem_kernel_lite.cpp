@@ -265,6 +265,46 @@ void write_text(const std::string& path, const std::string& text) {
   out << text;
 }
 
+// streaming text output (plain, or gzip by suffix) for predict mode
+class TextSink {
+ public:
+  explicit TextSink(const std::string& path) : path_(path) {
+    static std::string err;
+    if (path.size() >= 4 && path.compare(path.size() - 4, 4, ".bz2") == 0) {
+      err = path + ": bzip2 output is not available in this build";
+      throw err.c_str();
+    }
+    if (path.size() >= 3 && path.compare(path.size() - 3, 3, ".gz") == 0) gz_ = gzopen(path.c_str(), "wb");
+    else out_.open(path);
+    if (gz_ ? false : !out_.is_open()) {
+      err = path + ": cannot open for writing";
+      throw err.c_str();
+    }
+  }
+  ~TextSink() {
+    if (gz_) gzclose(gz_);
+  }
+  void write(const std::string& s) {
+    if (gz_) gzwrite(gz_, s.data(), (unsigned)s.size());
+    else out_ << s;
+  }
+
+ private:
+  std::string path_;
+  gzFile gz_ = nullptr;
+  std::ofstream out_;
+};
+
+void flush_if_large(std::ostringstream& buf, std::unique_ptr<TextSink>& sink, const std::string& path,
+                    bool final_flush = false) {
+  if (path.empty()) return;
+  if (!sink) sink.reset(new TextSink(path));
+  if (final_flush || buf.str().size() > (size_t)10 * 1024 * 1024) {
+    sink->write(buf.str());
+    buf.str("");
+  }
+}
+
 // App<K,LDF> (common/framework.h:100-353) over the compat types
 template <class K>
 class App {
@@ -300,6 +340,7 @@ class App {
     }
     const bool norm = opts_.normalize || !opts_.norm_output.empty();
     std::ostringstream kout, tout;
+    std::unique_ptr<TextSink> kfile, tfile;
     unsigned cnt = 0;
     for (size_t i = 0; i != opts_.ts_files.size(); ++i) {
       double elapsed = 0.0;
@@ -324,11 +365,14 @@ class App {
           kout << std::endl;
         }
         if (!opts_.norm_output.empty()) tout << self << std::endl;
+        // Output flushes its buffers past MAX = 10 MB (framework.cpp:193-234)
+        flush_if_large(kout, kfile, opts_.predict_only ? std::string() : opts_.output);
+        flush_if_large(tout, tfile, opts_.norm_output);
       }
       std::cout << " (" << elapsed << "s) done." << std::endl;
     }
-    if (!opts_.predict_only) write_text(opts_.output, kout.str());
-    if (!opts_.norm_output.empty()) write_text(opts_.norm_output, tout.str());
+    flush_if_large(kout, kfile, opts_.predict_only ? std::string() : opts_.output, true);
+    flush_if_large(tout, tfile, opts_.norm_output, true);
     return true;
   }
 

@@ -1567,10 +1567,18 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
   double* d_tb = static_cast<double*>(ctx->work);
   hipStream_t S = ctx->stream;
   SK_HIP(ctx, hipMemcpyAsync(d_tb, kp->score_table, 16 * 8, hipMemcpyHostToDevice, S));
-  int32_t* d_xy = nullptr;
-  double* d_out = nullptr;
-  SK_HIP(ctx, hipMalloc(&d_xy, (size_t)2 * n * sizeof(int32_t)));
-  SK_HIP(ctx, hipMalloc(&d_out, (size_t)5 * n * sizeof(double)));
+  // freed on every return path (an early SK_HIP return inside an optimizer
+  // loop would otherwise leak both on each failing call)
+  struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+      if (p) (void)hipFree(p);
+    }
+  } xy_buf, out_buf;
+  SK_HIP(ctx, hipMalloc(&xy_buf.p, (size_t)2 * n * sizeof(int32_t)));
+  SK_HIP(ctx, hipMalloc(&out_buf.p, (size_t)5 * n * sizeof(double)));
+  int32_t* d_xy = static_cast<int32_t*>(xy_buf.p);
+  double* d_out = static_cast<double*>(out_buf.p);
   SK_HIP(ctx, hipMemcpyAsync(d_xy, x, (size_t)n * 4, hipMemcpyHostToDevice, S));
   SK_HIP(ctx, hipMemcpyAsync(d_xy + n, y, (size_t)n * 4, hipMemcpyHostToDevice, S));
   double total_ms = 0.0;
@@ -1617,8 +1625,6 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
     if (e == hipSuccess) e = hipMemcpy(grad, d_out + n, (size_t)4 * n * 8, hipMemcpyDeviceToHost);
     if (e != hipSuccess) rc = fail(ctx, SK_ERR_HIP, hipGetErrorString(e));
   }
-  (void)hipFree(d_xy);
-  (void)hipFree(d_out);
   ctx->last_stem_ms = total_ms;
   return rc;
 }
