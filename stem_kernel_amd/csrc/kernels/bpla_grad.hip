@@ -15,6 +15,7 @@
 // (float products of the scores as the reference rounds them).
 #include <hip/hip_runtime.h>
 
+#include "bpla_fast.h"
 #include "device_set.h"
 #include "launch.h"
 
@@ -253,6 +254,252 @@ __global__ void __launch_bounds__(64) sk_bpla_grad_kernel(BplaGradLaunch P) {
 }
 
 }  // namespace
+
+// ===========================================================================
+// Wave-per-pair gradients for dyadic profiles (the operand tables and exp of
+// bpla.hip's fast path; every profile entry a multiple of 1/256).
+//
+// The gradient sums (BPLA_ForwardBackword, :325-383) read the forward states
+// around a cell and the backward states M, IX, IY at the cell, so:
+//   1. the BACKWARD pass runs first, on the forward kernel's streamed-strip
+//      systolic schedule played in reverse time (lane l owns rows 64s+l+1;
+//      row a+1 lives one lane up: wave_shl; the strip boundary row goes
+//      through LDS, written by lane 0, read by lane 63), and stores B_M, B_IX,
+//      B_IY in a per-wave HBM table laid out by (state, step, lane) -- 512
+//      contiguous bytes per state per step;
+//   2. the FORWARD pass recomputes F step by step and adds the gradient terms
+//      with the stored B of the same (step, lane).
+// The reference's scatter backward (:245-305) is gathered:
+//   B_M(a,b)  = [a<n,b<m] bs(a+1,b+1) B_M(a+1,b+1) + [a<n] (e^{bg} B_IX(a+1,b) + B_RX(a+1,b))
+//             + [b<m] (e^{bg} B_IY(a,b+1) + B_RY(a,b+1))
+//   B_IX(a,b) = [a<n,b<m] bs B_M(a+1,b+1) + [a<n] e^{be} B_IX(a+1,b) + [b<m] e^{bg} B_IY(a,b+1)
+//   B_IY(a,b) = [a<n,b<m] bs B_M(a+1,b+1) + [b<m] e^{be} B_IY(a,b+1)
+// with B_RX(a,b) = [b >= 1 or a = n] and B_RY(a,b) = [a = n] in closed form
+// (they only ever add 1s), and B_LX, B_LY never feeding M, IX, IY.  Forward,
+// F_LX = 1 and F_LY = j on rows i >= 1 (row 0: F_M = F_LX = 1 at (0,0),
+// F_LY = 1), and 1 + F_M + F_RX + F_RY at (n,m) = 1 + sum of F_M over cells
+// i, j >= 1.  Per pair: two exps per cell, 24 B per cell written and read
+// back.  Sums run in another order than the reference's (~1e-15 relative).
+__device__ void bpla_grad_wave_pair(const BplaGradLaunch& P, int x, int y, const BplaPos* ycol,
+                                    double* bnd, const double* etab, double* __restrict__ Bt,
+                                    int lane, double& value, double (&g)[4]) {
+  const double alpha = P.alpha, beta = P.beta, gap = P.gap, ext = P.ext;
+  const double bg = P.beta_gap, be = P.beta_ext;
+  const int Lx = __builtin_amdgcn_readfirstlane(P.xset.ex_len[x]);
+  const int Ly = __builtin_amdgcn_readfirstlane(P.yset.ex_len[y]);
+  const int xpb = __builtin_amdgcn_readfirstlane(P.xset.ex_pos_base[x]);
+  const int Lys = max(Ly, 64);
+  const int T = bpla_steps(Lx, Ly);
+  const int64_t TS = (int64_t)T * 64;
+  double* __restrict__ BM = Bt;
+  double* __restrict__ BX = Bt + TS;
+  double* __restrict__ BY = Bt + 2 * TS;
+  auto wave_sync = []() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // BPLAScore (bpla_kernel.cpp:45-62): the pair weight in float as written,
+  // the LAScore from the tabulated factors
+  auto score = [&](const BplaPos& xr, const BplaPos& yc, double& wp) {
+    double la = xr.v[0] * yc.v[0];
+    la = __builtin_fma(xr.v[1], yc.v[1], la);
+    la = __builtin_fma(xr.v[2], yc.v[2], la);
+    la = __builtin_fma(xr.v[3], yc.v[3], la);
+    const float pp = __fadd_rn(__fmul_rn(xr.pr, yc.pr), __fmul_rn(xr.pl, yc.pl));
+    const float uu = __fmul_rn(xr.pu, yc.pu);
+    wp = (double)pp;
+    return alpha * (double)pp + (double)uu * la;
+  };
+
+  // ---------------------------------------------------------------- backward
+  double* bndX = bnd;              // B_IX of row 64s+1 (lane 0), column b
+  double* bndP = bnd + (Lys + 2);  // bs * B_M of the same cells
+  for (int j = lane; j < 2 * (Lys + 2); j += 64) bnd[j] = 0.0;
+  wave_sync();
+  {
+    double oX = 0.0, oP = 0.0, oY = 0.0;  // my outputs of the previous (reverse) step
+    double dP = 0.0;                      // P(a+1, b+1): received a step earlier
+    int xs_cur = -1;
+    BplaPos xr;
+    for (int t = T - 1; t >= 0; --t) {
+      const int u = t - lane;
+      const int s = u >= 0 ? u / Lys : -1;
+      const int b = u - s * Lys + 1;
+      const int a = 64 * s + lane + 1;
+      // lane 63's row a+1 is lane 0 of the next strip (boundary row)
+      const int b63 = __builtin_amdgcn_readlane(b, 63);
+      const int bi = (b63 >= 1 && b63 <= Ly) ? b63 : 0;
+      const double rX = wave_shl1_to(oX, bndX[bi]);
+      const double rP = wave_shl1_to(oP, bndP[bi]);
+      double M = 0.0, X = 0.0, Y = 0.0, Pn = 0.0;
+      if (u >= 0 && b <= Ly && a <= Lx) {
+        if (s != xs_cur) {
+          xr = P.xtab[xpb + a - 1];
+          xs_cur = s;
+        }
+        const bool an = a < Lx, bm = b < Ly;
+        const double diag = (an && bm) ? dP : 0.0;
+        const double iyr = bm ? oY : 0.0;
+        const double ixd = an ? rX : 0.0;
+        M = diag + (an ? __builtin_fma(bg, ixd, 1.0) : 0.0) +
+            (bm ? __builtin_fma(bg, iyr, a == Lx ? 1.0 : 0.0) : 0.0);
+        X = diag + (an ? be * ixd : 0.0) + (bm ? bg * iyr : 0.0);
+        Y = diag + (bm ? be * iyr : 0.0);
+        if (!an && !bm) {  // (n, m): B_M = B_RX = B_RY = 1
+          M = 1.0;
+          X = Y = 0.0;
+        }
+        const BplaPos yc = ycol[b - 1];
+        double wp;
+        const double sc = score(xr, yc, wp);
+        Pn = fast_exp(beta * sc, etab, P.ec) * M;
+        BM[(int64_t)t * 64 + lane] = M;
+        BX[(int64_t)t * 64 + lane] = X;
+        BY[(int64_t)t * 64 + lane] = Y;
+        if (lane == 0) {
+          bndX[b] = X;
+          bndP[b] = Pn;
+        }
+      }
+      oX = X;
+      oP = Pn;
+      oY = Y;
+      dP = rP;
+    }
+  }
+  wave_sync();
+
+  // ---------------------------------------------------------------- forward + gradients
+  for (int j = lane; j < 3 * (Lys + 1); j += 64) bnd[j] = 0.0;  // row 0 (M, IX, IY)
+  wave_sync();
+  int j = 1 - lane, i = lane + 1;
+  bool row_ok = i <= Lx;
+  BplaPos xr = P.xtab[xpb + (row_ok ? i - 1 : 0)];
+  BplaPos xnext = P.xtab[xpb + (i + 64 <= Lx ? i + 63 : 0)];
+  double lM = 0.0, lX = 0.0, lY = 0.0;  // (i, j-1)
+  double dM = 0.0, dX = 0.0, dY = 0.0;  // (i-1, j-1): received a step earlier
+  double acc = 0.0, ga = 0.0, gb = 0.0, gg = 0.0, ge = 0.0;
+  // B at (step t, lane), prefetched a step ahead
+  double nbm = T > 0 ? BM[lane] : 0.0, nbx = T > 0 ? BX[lane] : 0.0, nby = T > 0 ? BY[lane] : 0.0;
+  for (int t = 0; t < T; ++t) {
+    const double bm = nbm, bx = nbx, by = nby;
+    if (t + 1 < T) {
+      nbm = BM[(int64_t)(t + 1) * 64 + lane];
+      nbx = BX[(int64_t)(t + 1) * 64 + lane];
+      nby = BY[(int64_t)(t + 1) * 64 + lane];
+    }
+    const int jb = __builtin_amdgcn_readfirstlane(j);
+    const double* bj = bnd + 3 * (jb >= 1 && jb <= Ly ? jb : 0);
+    const double uM = wave_shr1(lM, bj[0]);
+    const double uX = wave_shr1(lX, bj[1]);
+    const double uY = wave_shr1(lY, bj[2]);
+    if (j >= 1 && j <= Ly) {
+      const BplaPos yc = ycol[j - 1];
+      double wp;
+      const double sc = score(xr, yc, wp);
+      const double bs = fast_exp(beta * sc, etab, P.ec);
+      const bool c1 = j == 1;
+      // diagonal F_M + F_IX + F_IY + F_LX + F_LY at (i-1, j-1)
+      const double extra = i == 1 ? (c1 ? 3.0 : 1.0) : (double)j;
+      const double nM = bs * (dM + dX + dY + extra);
+      const double nX = bg * uM + be * uX;
+      const double lMX = c1 ? 0.0 : lM + lX, lYc = c1 ? 0.0 : lY;
+      const double nY = bg * lMX + be * lYc;
+      if (row_ok) {
+        acc += nM;
+        const double vd = nM * bm;
+        const double vgx = uM * bg * bx, vex = uX * be * bx;
+        const double vgy = lMX * bg * by, vey = lYc * be * by;
+        ga += beta * wp * vd;
+        gb += sc * vd + gap * (vgx + vgy) + ext * (vex + vey);
+        gg += beta * (vgx + vgy);
+        ge += beta * (vex + vey);
+      }
+      lM = nM;
+      lX = nX;
+      lY = nY;
+      if (lane == 63) {
+        double* bw = bnd + 3 * j;
+        bw[0] = nM;
+        bw[1] = nX;
+        bw[2] = nY;
+      }
+    }
+    dM = uM;
+    dX = uX;
+    dY = uY;
+    if (++j > Lys) {  // next strip: row i + 64, column 1
+      j = 1;
+      i += 64;
+      row_ok = i <= Lx;
+      xr = xnext;
+      if (i + 64 <= Lx) xnext = P.xtab[xpb + i + 63];
+      dM = dX = dY = 0.0;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    acc += __shfl_xor(acc, off, 64);
+    ga += __shfl_xor(ga, off, 64);
+    gb += __shfl_xor(gb, off, 64);
+    gg += __shfl_xor(gg, off, 64);
+    ge += __shfl_xor(ge, off, 64);
+  }
+  value = 1.0 + acc;
+  g[0] = ga;
+  g[1] = gb;
+  g[2] = gg;
+  g[3] = ge;
+  wave_sync();
+}
+
+__global__ void __launch_bounds__(256) sk_bpla_grad_wave_kernel(BplaGradLaunch P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int maxlen = P.lds_max_len;
+  double* etab = reinterpret_cast<double*>(smem);
+  unsigned char* wbase = smem + kBplaExpLds + (size_t)wave * bpla_grad_wave_lds_bytes(maxlen);
+  BplaPos* ycol = reinterpret_cast<BplaPos*>(wbase);
+  double* bnd = reinterpret_cast<double*>(ycol + maxlen);
+  double* Bt = P.scratch + (int64_t)(blockIdx.x * (blockDim.x >> 6) + wave) * P.bt_doubles;
+  fill_exp_table(etab);
+  auto next_pair = [&]() {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(P.pair_counter, 1ull);
+    return (int64_t)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+                     (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v));
+  };
+  for (int64_t pr = next_pair(); pr < P.n_pairs; pr = next_pair()) {
+    const int x = __builtin_amdgcn_readfirstlane(P.xs[pr]);
+    const int y = __builtin_amdgcn_readfirstlane(P.ys[pr]);
+    const int Ly = P.yset.ex_len[y], ypb = P.yset.ex_pos_base[y];
+    for (int j = lane; j < Ly; j += 64) ycol[j] = P.ytab[ypb + j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double v, g[4];
+    bpla_grad_wave_pair(P, x, y, ycol, bnd, etab, Bt, lane, v, g);
+    if (lane == 0) {
+      const int64_t o = P.oidx ? P.oidx[pr] : pr;
+      P.value[o] = v;
+      P.grad[4 * o + 0] = g[0];
+      P.grad[4 * o + 1] = g[1];
+      P.grad[4 * o + 2] = g[2];
+      P.grad[4 * o + 3] = g[3];
+    }
+  }
+}
+
+hipError_t launch_bpla_grad_wave(const BplaGradLaunch& P, int grid, int nwaves, hipStream_t st) {
+  if (P.n_pairs == 0 || grid <= 0) return hipSuccess;
+  const size_t lds = kBplaExpLds + (size_t)nwaves * bpla_grad_wave_lds_bytes(P.lds_max_len);
+  hipError_t e = hipFuncSetAttribute((const void*)sk_bpla_grad_wave_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sk_bpla_grad_wave_kernel, dim3(grid), dim3(64 * nwaves), lds, st, P);
+  return hipGetLastError();
+}
 
 size_t bpla_grad_pair_bytes(int n1, int m1) { return (size_t)(2 * 7 + 1) * n1 * m1 * sizeof(double); }
 

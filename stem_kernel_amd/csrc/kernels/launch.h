@@ -119,9 +119,29 @@ struct BplaGradLaunch {
   double* scratch = nullptr;
   double* value = nullptr;  // n_pairs
   double* grad = nullptr;   // 4 * n_pairs: d/d(alpha, beta, gap, ext)
+  // wave-per-pair kernel (dyadic profiles, bpla_grad.hip): operand tables of
+  // sk_bpla_tab_kernel, pairs pulled by waves, result of pair k at oidx[k]
+  const BplaPos* xtab = nullptr;
+  const BplaPos* ytab = nullptr;
+  double ec[4] = {8.3333333333333332e-03, 4.1666666666666664e-02, 1.6666666666666666e-01, 0.5};
+  unsigned long long* pair_counter = nullptr;
+  const int64_t* oidx = nullptr;
+  int32_t lds_max_len = 0;  // even, >= 64
+  int64_t bt_doubles = 0;   // per-wave backward table: 3 states x steps x 64 lanes
 };
 size_t bpla_grad_pair_bytes(int n1, int m1);
 hipError_t launch_bpla_grad(const BplaGradLaunch& P, hipStream_t st);
+// steps of the streamed-strip systolic schedule of one (|x|, |y|) pair
+__host__ __device__ inline int bpla_steps(int lx, int ly) {
+  const int lys = ly > 64 ? ly : 64;
+  return lx <= 0 || ly <= 0 ? 0 : ((lx + 63) / 64 - 1) * lys + ((lx - 1) & 63) + ly;
+}
+// per-wave LDS of the wave gradient kernel: y columns | boundary row
+__host__ __device__ inline size_t bpla_grad_wave_lds_bytes(int maxlen) {
+  const size_t b = (size_t)maxlen * sizeof(BplaPos) + (size_t)3 * (maxlen + 2) * 8;
+  return (b + 15) & ~(size_t)15;
+}
+hipError_t launch_bpla_grad_wave(const BplaGradLaunch& P, int grid, int nwaves, hipStream_t st);
 
 // per-wave LDS of the BPLA kernel: 4 boundary rows + y columns (16-B aligned)
 __host__ __device__ inline size_t bpla_wave_lds_bytes(int maxlen) {

@@ -1576,17 +1576,118 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
     }
   } xy_buf, out_buf;
   SK_HIP(ctx, hipMalloc(&xy_buf.p, (size_t)2 * n * sizeof(int32_t)));
-  SK_HIP(ctx, hipMalloc(&out_buf.p, (size_t)5 * n * sizeof(double)));
+  SK_HIP(ctx, hipMalloc(&out_buf.p, (size_t)10 * n * sizeof(double)));
   int32_t* d_xy = static_cast<int32_t*>(xy_buf.p);
   double* d_out = static_cast<double*>(out_buf.p);
   SK_HIP(ctx, hipMemcpyAsync(d_xy, x, (size_t)n * 4, hipMemcpyHostToDevice, S));
   SK_HIP(ctx, hipMemcpyAsync(d_xy + n, y, (size_t)n * 4, hipMemcpyHostToDevice, S));
   double total_ms = 0.0;
-  for (int64_t b0 = 0; b0 < n && rc == SK_OK;) {
+  // pairs whose profiles are all dyadic take the wave-per-pair kernel (the
+  // BPLA fast path's operand tables); the rest the thread-per-pair one
+  const HostPack& PX = xs_->pack;
+  const HostPack& PY = ys_->pack;
+  std::vector<int32_t> wx, wy, gx, gy;
+  std::vector<int64_t> wo, go;
+  const bool general_only = std::getenv("SK_BPLA_GENERAL") != nullptr;  // A/B switch
+  for (int64_t k = 0; k < n; ++k) {
+    if (!general_only && PX.ex_dyadic[x[k]] && PY.ex_dyadic[y[k]]) {
+      wx.push_back(x[k]);
+      wy.push_back(y[k]);
+      wo.push_back(k);
+    } else {
+      gx.push_back(x[k]);
+      gy.push_back(y[k]);
+      go.push_back(k);
+    }
+  }
+  if (!wx.empty()) {
+    const size_t nw = wx.size();
+    const size_t npx = PX.pos_prof.size(), npy = ys_ == xs_ ? 0 : PY.pos_prof.size();
+    const size_t ntab = 2 * (npx + npy);
+    int tmax = 1, maxlen = 64;
+    for (size_t k = 0; k < nw; ++k) {
+      tmax = std::max(tmax, sk::bpla_steps(xs_->ex[wx[k]].len, ys_->ex[wy[k]].len));
+      maxlen = std::max(maxlen, ys_->ex[wy[k]].len);
+    }
+    maxlen = (maxlen + 1) & ~1;
+    const size_t wl = sk::bpla_grad_wave_lds_bytes(maxlen);
+    if (wl + sk::kBplaExpLds > 163840)
+      return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for the BPLA gradient kernel LDS");
+    const int per_cu_w = (int)std::max<size_t>(1, std::min<size_t>(16, (163840 - 2 * sk::kBplaExpLds) / wl));
+    const int wpb = std::min(4, per_cu_w);
+    const int64_t bt = (int64_t)3 * 64 * tmax;
+    int64_t grid = (int64_t)ctx->n_cu * std::max(1, per_cu_w / wpb);
+    grid = std::min<int64_t>(grid, std::max<int64_t>(1, ((int64_t)nw + wpb - 1) / wpb));
+    grid = std::min<int64_t>(grid, std::max<int64_t>(1, (int64_t)(budget / (8.0 * bt * wpb))));
+    DevBuf tab_buf, idx_buf;
+    SK_HIP(ctx, hipMalloc(&tab_buf.p, ntab * sizeof(sk::BplaPos) + 64));
+    SK_HIP(ctx, hipMalloc(&idx_buf.p, nw * (4 + 4 + 8) + 64));
+    int32_t* d_wx = static_cast<int32_t*>(idx_buf.p);
+    int32_t* d_wy = d_wx + nw;
+    int64_t* d_wo = reinterpret_cast<int64_t*>(static_cast<char*>(idx_buf.p) + ((nw * 8 + 15) & ~size_t(15)));
+    unsigned long long* d_cnt = reinterpret_cast<unsigned long long*>(d_tb + 16);  // after the table (work arena)
+    SK_HIP(ctx, hipMemcpyAsync(d_wx, wx.data(), nw * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_wy, wy.data(), nw * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_wo, wo.data(), nw * 8, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemsetAsync(d_cnt, 0, 8, S));
+    sk::BplaPos* tabs = static_cast<sk::BplaPos*>(tab_buf.p);
+    sk::BplaPos* tx = tabs;  // [npx] x role | [npx] y role (| [npy] x role | [npy] y role)
+    sk::BplaPos* ty = tabs + npx;
+    SK_HIP(ctx, sk::launch_bpla_tab(xs_->dev.pos_prof, xs_->dev.pos_lru, (int64_t)npx, d_tb, tx,
+                                    tabs + npx, S));
+    if (npy) {
+      ty = tabs + 2 * npx + npy;
+      SK_HIP(ctx, sk::launch_bpla_tab(ys_->dev.pos_prof, ys_->dev.pos_lru, (int64_t)npy, d_tb,
+                                      tabs + 2 * npx, ty, S));
+    }
+    rc = ensure_scratch(ctx, (size_t)grid * wpb * (size_t)bt * 8 + 64);
+    if (rc) return rc;
+    sk::BplaGradLaunch W;
+    W.xset = xs_->dev;
+    W.yset = ys_->dev;
+    W.table = d_tb;
+    W.alpha = kp->alpha;
+    W.beta = kp->beta;
+    W.gap = kp->gap;
+    W.ext = kp->ext;
+    W.beta_gap = std::exp(kp->beta * kp->gap);  // bpla_kernel.cpp:188-189
+    W.beta_ext = std::exp(kp->beta * kp->ext);
+    W.xs = d_wx;
+    W.ys = d_wy;
+    W.n_pairs = (int64_t)nw;
+    W.scratch = ctx->scratch;
+    W.value = d_out;
+    W.grad = d_out + n;
+    W.xtab = tx;
+    W.ytab = ty;
+    W.pair_counter = d_cnt;
+    W.oidx = d_wo;
+    W.lds_max_len = maxlen;
+    W.bt_doubles = bt;
+    SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
+    SK_HIP(ctx, sk::launch_bpla_grad_wave(W, (int)grid, wpb, S));
+    SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
+    SK_HIP(ctx, hipStreamSynchronize(S));
+    float ms = 0.f;
+    SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    total_ms += ms;
+  }
+  // the thread-per-pair kernel over the remaining pairs, in place of (x, y)
+  if (!wx.empty() && !gx.empty()) {
+    SK_HIP(ctx, hipMemcpyAsync(d_xy, gx.data(), gx.size() * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_xy + n, gy.data(), gy.size() * 4, hipMemcpyHostToDevice, S));
+  }
+  const int64_t ng = wx.empty() ? n : (int64_t)gx.size();
+  const int32_t* hx = wx.empty() ? x : gx.data();
+  const int32_t* hy = wx.empty() ? y : gy.data();
+  // general results: in place when every pair is general, else in their own
+  // region (values | grads of the general list), scattered on the host
+  double* g_out = wx.empty() ? d_out : d_out + 5 * n;
+  for (int64_t b0 = 0; b0 < ng && rc == SK_OK;) {
     int n1 = 1, m1 = 1;
     int64_t b1 = b0;
-    while (b1 < n) {
-      const int a1 = std::max(n1, xs_->ex[x[b1]].len + 1), c1 = std::max(m1, ys_->ex[y[b1]].len + 1);
+    while (b1 < ng) {
+      const int a1 = std::max(n1, xs_->ex[hx[b1]].len + 1), c1 = std::max(m1, ys_->ex[hy[b1]].len + 1);
       if (b1 > b0 && (double)(b1 - b0 + 1) * sk::bpla_grad_pair_bytes(a1, c1) > budget) break;
       n1 = a1, m1 = c1, ++b1;
     }
@@ -1609,8 +1710,8 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
     G.n1 = n1;
     G.m1 = m1;
     G.scratch = ctx->scratch;
-    G.value = d_out + b0;
-    G.grad = d_out + n + 4 * b0;
+    G.value = g_out + b0;
+    G.grad = g_out + ng + 4 * b0;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     SK_HIP(ctx, sk::launch_bpla_grad(G, S));
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
@@ -1621,8 +1722,26 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
     b0 = b1;
   }
   if (rc == SK_OK) {
-    hipError_t e = hipMemcpy(value, d_out, (size_t)n * 8, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(grad, d_out + n, (size_t)4 * n * 8, hipMemcpyDeviceToHost);
+    hipError_t e = hipSuccess;
+    if (!wx.empty()) {  // wave kernel: by original index
+      std::vector<double> v(n), g(4 * (size_t)n);
+      e = hipMemcpy(v.data(), d_out, (size_t)n * 8, hipMemcpyDeviceToHost);
+      if (e == hipSuccess) e = hipMemcpy(g.data(), d_out + n, (size_t)4 * n * 8, hipMemcpyDeviceToHost);
+      for (int64_t k : wo) {
+        value[k] = v[k];
+        for (int q = 0; q < 4; ++q) grad[4 * k + q] = g[4 * k + q];
+      }
+    }
+    if (e == hipSuccess && ng) {
+      std::vector<double> v(ng), g(4 * (size_t)ng);
+      e = hipMemcpy(v.data(), g_out, (size_t)ng * 8, hipMemcpyDeviceToHost);
+      if (e == hipSuccess) e = hipMemcpy(g.data(), g_out + ng, (size_t)4 * ng * 8, hipMemcpyDeviceToHost);
+      for (int64_t t = 0; t < ng; ++t) {
+        const int64_t k = wx.empty() ? t : go[t];
+        value[k] = v[t];
+        for (int q = 0; q < 4; ++q) grad[4 * k + q] = g[4 * t + q];
+      }
+    }
     if (e != hipSuccess) rc = fail(ctx, SK_ERR_HIP, hipGetErrorString(e));
   }
   ctx->last_stem_ms = total_ms;
