@@ -714,11 +714,17 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
       px.reserve(n);
       py.reserve(n);
       oidx.reserve(n);
-      std::vector<int64_t> fast;
-      fast.reserve(n_fast);
-      for (int64_t k = 0; k < n; ++k)
-        if (is_fast(k)) fast.push_back(k);
-      if (group) std::stable_sort(fast.begin(), fast.end(), [&](int64_t a, int64_t b) { return y[a] < y[b]; });
+      std::vector<int64_t> fast(n_fast);
+      if (group) {  // stable counting sort by y (ycnt holds the per-y counts)
+        std::vector<int64_t> pos(ys_->ex.size() + 1, 0);
+        for (size_t j = 0; j < ys_->ex.size(); ++j) pos[j + 1] = pos[j] + ycnt[j];
+        for (int64_t k = 0; k < n; ++k)
+          if (is_fast(k)) fast[pos[y[k]]++] = k;
+      } else {
+        int64_t f = 0;
+        for (int64_t k = 0; k < n; ++k)
+          if (is_fast(k)) fast[f++] = k;
+      }
       for (int64_t k : fast) {
         px.push_back(x[k]);
         py.push_back(y[k]);
