@@ -123,6 +123,9 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_SEGSUM  // MATCH: same-parent runs summed per quad before the atomic (0 = off)
 #define SK_SEGSUM 1
 #endif
+#ifndef SK_SKIP_LOOPS  // cost experiment only (wrong results): loop rows skip MATCH and the sweep
+#define SK_SKIP_LOOPS 0
+#endif
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
 #define SK_MU 3
 #endif
@@ -385,7 +388,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #ifdef SK_STAMPS
     cnt[3] += qb > qa ? qb - qa : 0;
 #endif
-    if (qa < qb) {
+    if (qa < qb && !(SK_SKIP_LOOPS && xloop)) {
       // node records and path counts come from HBM (L2-resident per y),
       // the first pass's issued before A, each later pass's during the
       // pass before.  A pass covers NW = 64*SK_PW nodes [q0, top], lane l
@@ -606,7 +609,9 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #ifdef SK_STAMPS
     cnt[1] += Y.nch - c0;
 #endif
-    if (c0 < Y.nch) {
+    // a row nobody reads (a root: pslot 0xffff) needs only its MATCH terms
+    // (K is the path sum of M), so it skips the sweep and the store
+    if (c0 < Y.nch && pslot != 0xffffu && !(SK_SKIP_LOOPS && xloop)) {
       const lds_u32* rp = Y.sc + c0 * 64 + lane;
       const lds_f64* wp = Y.ew + c0 * 64 + lane;
       // three chunk slots in rotation (the loop is unrolled by three, so no
@@ -645,15 +650,15 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     }
     STAMP(5);
 
-    // ---- D: G0 row p = G1 + v_s*S, to p's slot (roots are never read).
-    // Every later read of element q of this row is by the same lane (q =
-    // lane + 64k), so per-thread program order makes it visible: no fence.
-    // Rows never read (pslot 0xffff) go to the slab's last (junk) row, so
-    // the store is unconditional and the R reads of all slots issue back to
-    // back.
-    {
-      const uint32_t oslot = pslot == 0xffffu ? (uint32_t)(P.slab_doubles / stride - 1) : pslot;
-      double* __restrict__ orow = slab + (size_t)oslot * stride + lane;
+    // ---- D: G0 row p = G1 + v_s*S, to p's slot.  Every later read of
+    // element q of this row is by the same lane (q = lane + 64k), so
+    // per-thread program order makes it visible: no fence.  A row nobody
+    // reads (a root) is not stored; it is no child of the next row either.
+    if (pslot == 0xffffu) {
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k) S[k] = egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
+    } else {
+      double* __restrict__ orow = slab + (size_t)pslot * stride + lane;
       // all R reads issued before the first store (one LDS round trip)
       double g1[MAXK];
 #pragma unroll
