@@ -59,6 +59,34 @@ __global__ void sk_prep_kernel(DevSet s, DevParamNodes pn, const double* __restr
     pn.nd_SL[nb + k] = SL;
   }
   for (int r = 0; r < nl; ++r) pn.xr_SL[nb + r] = pn.nd_SL[nb + s.xr_node[nb + r]];
+  // child-edge weights of both x schedules
+  {
+    int k = s.ex_xch_base[e];
+    for (int r = 0; r < nl; ++r) {
+      const int ne = s.xrow[nb + r].a & 0xff;
+      for (int t = 0; t < ne; ++t, ++k) pn.xr_chw[k] = gpow[s.xr_ch[k] >> 16];
+    }
+  }
+  if (s.n_gam > 0) {
+    const int gb = s.ex_xg_base[e], nlg = s.ex_nlxg[e];
+    int k = s.ex_xgch_base[e];
+    for (int r = 0; r < nlg; ++r) {
+      pn.xg_SL[gb + r] = pn.nd_SL[nb + s.xg_node[gb + r]];
+      const int ne = s.xgrow[gb + r].a & 0xff;
+      for (int t = 0; t < ne; ++t, ++k) {
+        const uint32_t c = s.xg_ch[k];
+        double w = gpow[c >> 16];
+        if (c & 0x8000u) w *= gpow[s.xg_clg[k]] * (double)s.xg_cpf[k];  // gamma child
+        pn.xg_chw[k] = w;
+      }
+    }
+    double* h = pn.gam_h + (int64_t)e * s.n_gam;
+    for (int g = 0; g < s.n_gam; ++g) h[g] = 0.0;
+    for (int i = s.ex_gr_base[e]; i < s.ex_gr_base[e + 1]; ++i) {
+      const uint32_t inf = s.gr_info[i];
+      h[inf & 0xffff] += s.gr_P[i] * (gpow[inf >> 16] * (double)s.gr_pf[i]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -221,26 +249,92 @@ __device__ __forceinline__ void add_rows2(double (&S)[MAXK], __amdgpu_buffer_rsr
 //   C. IY sweep over the y levels, edge-parallel: G1[q] += G1[cy]*w(q,cy)
 //      with w = gap^2*w_y(q)*g^gaps (LDS f64 atomics);
 //   D. G0[p][q] = G1[q] + v_s(p)*S[k] -> slot of p.
+// ---- C of a row (and the Gamma rows of an item): the IY recurrence
+// G1[q] += w(q,cy) G1[cy], w = gap^2 w_y(q) g^gaps, over the y example's
+// sweep schedule from chunk c0: chunks of 64 edges, each placed after every
+// edge of its children (host list schedule).  A chunk's R reads are issued
+// after the previous chunk's atomics and a wave's LDS ops execute in issue
+// order, so nothing drains between chunks: only the data a lane consumes is
+// waited for.  Records are read two chunks ahead, weights one; dummy records
+// (weight 0) pad the chunks.  Ends with a wave barrier.
+__device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int lane) {
+  const lds_u32* rp = Y.sc + c0 * 64 + lane;
+  const lds_f64* wp = Y.ew + c0 * 64 + lane;
+  // three chunk slots in rotation (the loop is unrolled by three, so no
+  // loaded register is ever copied, which would force a wait for it)
+  struct Ck {
+    uint32_t rec;
+    double w, rv;
+  };
+  Ck A, B, C;
+  A.rec = rp[0];
+  A.w = wp[0];
+  B.rec = rp[64];
+  B.w = 0.0;
+  C.rec = 0u;
+  C.w = C.rv = B.rv = 0.0;
+  A.rv = R[A.rec & 0x7ff];
+  int c = c0;
+  const int nch = Y.nch;
+  // chunk X now, Y next, Z after: false after the last chunk
+  auto step = [&](Ck& X, Ck& Yc, Ck& Z) __attribute__((always_inline)) -> bool {
+    Z.rec = rp[128];
+    Yc.w = wp[64];
+    __hip_atomic_fetch_add(&R[(X.rec >> 11) & 0x7ff], X.rv * X.w, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+    Yc.rv = R[Yc.rec & 0x7ff];
+    rp += 64;
+    wp += 64;
+    return ++c < nch;
+  };
+  for (;;) {
+    if (!step(A, B, C)) break;
+    if (!step(B, C, A)) break;
+    if (!step(C, A, B)) break;
+  }
+  wave_sync();
+}
+
+// base of child row c of an x schedule: a slab slot, or (bit 15) the y's
+// Gamma row of a gamma child
+__device__ __forceinline__ const double* child_row(uint32_t c, const double* slab,
+                                                   const double* gamtab, int stride) {
+  return (c & 0x8000u) ? gamtab + (size_t)(c & 0x7fffu) * stride : slab + (size_t)(c & 0xffffu) * stride;
+}
+
 template <int MAXK>
 __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds_f64* hb,
                             const lds_f64* co, const lds_f64* gp, double* __restrict__ slab, int x,
-                            int lane) {
+                            int lane, bool gam, const double* __restrict__ gamtab,
+                            const lds_f64* kap) {
   constexpr int stride = 64 * MAXK;
   const DevSet& s = P.xset;
   const DevSet& ys = P.yset;
   const double* __restrict__ yPg = ys.yn_P + Y.nb;  // path counts of y (HBM, L2-resident)
-  const int nlx = s.ex_nl[x];
   const int NLy = Y.nl;
-  if (nlx == 0 || NLy == 0) return 0.0;
+  if (s.ex_nl[x] == 0 || NLy == 0) return 0.0;
   const int xnb = s.ex_node_base[x], xbb = s.ex_bpf_base[x];
-  int chp = s.ex_xch_base[x];
+  // the x schedule: every non-leaf row, or (gamma) all but the gamma rows,
+  // whose K terms come from the y's Gamma sums: sum_g h_x[g] kappa_y[g]
+  const int xgb = gam ? s.ex_xg_base[x] : 0;
+  const int nlx = gam ? s.ex_nlxg[x] : s.ex_nl[x];
+  int chp = gam ? s.ex_xgch_base[x] : s.ex_xch_base[x];
   const double x_nseq = (double)s.ex_nseqs[x];
   const double gap2 = P.gap2;
   const int band = (int)P.band;
-  const XRow* __restrict__ xrows = s.xrow + xnb;
-  const double* __restrict__ xsl = P.pn.xr_SL + xnb;
-  const uint32_t* __restrict__ xch = s.xr_ch;
+  const XRow* __restrict__ xrows = gam ? s.xgrow + xgb : s.xrow + xnb;
+  const double* __restrict__ xsl = gam ? P.pn.xg_SL + xgb : P.pn.xr_SL + xnb;
+  const uint32_t* __restrict__ xch = gam ? s.xg_ch : s.xr_ch;
+  const double* __restrict__ xchw = gam ? P.pn.xg_chw : P.pn.xr_chw;
   double kacc = 0.0;
+  if (gam) {
+    const double* __restrict__ h = P.pn.gam_h + (int64_t)x * s.n_gam;
+    for (int g = lane; g < s.n_gam; g += 64) kacc += h[g] * kap[g];
+  }
+  if (nlx == 0) {
+    for (int off = 32; off > 0; off >>= 1) kacc += __shfl_xor(kacc, off, 64);
+    return kacc;
+  }
 #ifdef SK_STAMPS
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long cnt[4] = {0, 0, 0, 0};  // A-loaded rows, levels, passes, band nodes
@@ -256,11 +350,16 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
   const cst_ptr<XRow> xrows_c = (cst_ptr<XRow>)xrows;
   const cst_ptr<double> xsl_c = (cst_ptr<double>)xsl;
   const cst_ptr<uint32_t> xch_c = (cst_ptr<uint32_t>)xch;
+  const cst_ptr<double> xchw_c = (cst_ptr<double>)xchw;
   XRow nx = xrows_c[0];
   double nSL = xsl_c[0];
   uint32_t nch[4];
+  double ncw[4];  // their weights (g^gaps, times g^lg pf for a gamma child)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) nch[j] = xch_c[chp + j];
+  for (int j = 0; j < 4; ++j) {
+    nch[j] = xch_c[chp + j];
+    ncw[j] = xchw_c[chp + j];
+  }
 
   double S[MAXK];  // this row's weighted child sum (carried over rows)
 #pragma unroll
@@ -273,8 +372,12 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     const double x_nbp = (double)nx.nbp;
     const double xP = nx.P, xSL = nSL, xpf = (double)nx.bp0;
     uint32_t ch[4];
+    double cw[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ch[j] = nch[j];
+    for (int j = 0; j < 4; ++j) {
+      ch[j] = nch[j];
+      cw[j] = ncw[j];
+    }
     const int xne = xa & 0xff, xnbf = (xa >> 8) & 0xff;
     const int chp_r = chp;
     chp += xne;
@@ -320,7 +423,10 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       nx = xrows_c[r + 1];
       nSL = xsl_c[r + 1];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) nch[j] = xch_c[chp + j];
+      for (int j = 0; j < 4; ++j) {
+        nch[j] = xch_c[chp + j];
+        ncw[j] = xchw_c[chp + j];
+      }
     }
     SCHED_FENCE();
 
@@ -330,6 +436,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      registers; `done` marks those among the first four children.
     {
       uint32_t c[4] = {0u, 0u, 0u, 0u};
+      double w[4] = {0.0, 0.0, 0.0, 0.0};
       int na = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -338,15 +445,19 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
         c[1] = (take && na == 1) ? ch[j] : c[1];
         c[2] = (take && na == 2) ? ch[j] : c[2];
         c[3] = (take && na == 3) ? ch[j] : c[3];
+        w[0] = (take && na == 0) ? cw[j] : w[0];
+        w[1] = (take && na == 1) ? cw[j] : w[1];
+        w[2] = (take && na == 2) ? cw[j] : w[2];
+        w[3] = (take && na == 3) ? cw[j] : w[3];
         na += take ? 1 : 0;
       }
       for (int h = 0; h < 4; h += 2) {
         if (na > h) {
           const bool two = na > h + 1;
           const uint32_t c0 = c[h], c1 = two ? c[h + 1] : c[h];
-          const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
-          add_rows2<MAXK>(S, row_rsrc(slab + (size_t)(c0 & 0xffff) * stride, NLy),
-                          row_rsrc(slab + (size_t)(c1 & 0xffff) * stride, NLy), eg0, eg1, lane);
+          const double eg0 = w[h], eg1 = two ? w[h + 1] : 0.0;
+          add_rows2<MAXK>(S, row_rsrc(child_row(c0, slab, gamtab, stride), NLy),
+                          row_rsrc(child_row(c1, slab, gamtab, stride), NLy), eg0, eg1, lane);
         }
       }
     }
@@ -361,9 +472,9 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       const uint32_t c0 = xch[chp_r + t];
       const bool two = t + 1 < xne;
       const uint32_t c1 = two ? xch[chp_r + t + 1] : c0;
-      const double eg0 = gp[c0 >> 16], eg1 = two ? gp[c1 >> 16] : 0.0;
-      add_rows2<MAXK>(S, row_rsrc(slab + (size_t)(c0 & 0xffff) * stride, NLy),
-                      row_rsrc(slab + (size_t)(c1 & 0xffff) * stride, NLy), eg0, eg1, lane);
+      const double eg0 = xchw[chp_r + t], eg1 = two ? xchw[chp_r + t + 1] : 0.0;
+      add_rows2<MAXK>(S, row_rsrc(child_row(c0, slab, gamtab, stride), NLy),
+                      row_rsrc(child_row(c1, slab, gamtab, stride), NLy), eg0, eg1, lane);
     }
     STAMP(1);
 
@@ -561,7 +672,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       for (int j = 0; j < 4; ++j) {
         if (j < nne) {
           const uint32_t c = nch[j];
-          const double g = gp[c >> 16];
+          const double g = ncw[j];
           if ((c & 0xffff) == pslot) {
             egd += g;
             nxt_done |= 1u << j;
@@ -579,12 +690,12 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
         }
       }
       if (npf >= 1) {
-        const __amdgpu_buffer_rsrc_t r0 = row_rsrc(slab + (size_t)(pf0 & 0xffff) * stride, NLy);
+        const __amdgpu_buffer_rsrc_t r0 = row_rsrc(child_row(pf0, slab, gamtab, stride), NLy);
 #pragma unroll
         for (int k = 0; k < MAXK; ++k) T0[k] = row_ld(r0, lane, k);
       }
       if (NPF >= 2 && npf >= 2) {
-        const __amdgpu_buffer_rsrc_t r1 = row_rsrc(slab + (size_t)(pf1 & 0xffff) * stride, NLy);
+        const __amdgpu_buffer_rsrc_t r1 = row_rsrc(child_row(pf1, slab, gamtab, stride), NLy);
 #pragma unroll
         for (int k = 0; k < MAXK; ++k) T1[k] = row_ld(r1, lane, k);
       }
@@ -612,40 +723,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // a row nobody reads (a root: pslot 0xffff) needs only its MATCH terms
     // (K is the path sum of M), so it skips the sweep and the store
     if (c0 < Y.nch && pslot != 0xffffu && !(SK_SKIP_LOOPS && xloop)) {
-      const lds_u32* rp = Y.sc + c0 * 64 + lane;
-      const lds_f64* wp = Y.ew + c0 * 64 + lane;
-      // three chunk slots in rotation (the loop is unrolled by three, so no
-      // loaded register is ever copied, which would force a wait for it)
-      struct Ck {
-        uint32_t rec;
-        double w, rv;
-      };
-      Ck A, B, C;
-      A.rec = rp[0];
-      A.w = wp[0];
-      B.rec = rp[64];
-      B.w = 0.0;
-      C.rec = 0u;
-      C.w = C.rv = B.rv = 0.0;
-      A.rv = R[A.rec & 0x7ff];
-      int c = c0;
-      const int nch = Y.nch;
-      // chunk X now, Y next, Z after: false after the last chunk
-      auto step = [&](Ck& X, Ck& Yc, Ck& Z) __attribute__((always_inline)) -> bool {
-        Z.rec = rp[128];
-        Yc.w = wp[64];
-        __hip_atomic_fetch_add(&R[(X.rec >> 11) & 0x7ff], X.rv * X.w, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WAVEFRONT);
-        Yc.rv = R[Yc.rec & 0x7ff];
-        rp += 64;
-        wp += 64;
-        return ++c < nch;
-      };
-      for (;;) {
-        if (!step(A, B, C)) break;
-        if (!step(B, C, A)) break;
-        if (!step(C, A, B)) break;
-      }
+      iy_sweep(Y, R, c0, lane);
       wave_sync();
     }
     STAMP(5);
@@ -715,6 +793,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   lds_i32* ylf = (lds_i32*)(yed2 + P.lds_max_edges);          // lds_max_len_pad
   lds_i32* ycs = ylf + P.lds_max_len_pad;                     // lds_max_len_pad
   lds_i32* ctl = ycs + P.lds_max_len_pad;                     // 4 ints
+  lds_f64* kap = (lds_f64*)(ctl + 4);                         // xset.n_gam (gam_on)
 
   for (int k = threadIdx.x; k < 256; k += blockDim.x) co[k] = P.co_subst[k];
   for (int k = threadIdx.x; k < P.n_gpow; k += blockDim.x) gp[k] = P.gpow[k];
@@ -723,7 +802,9 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   lds_f64* hb = hball + (size_t)wave * 64 * SK_PW;
   for (int j = 0; j < SK_PW; ++j) hb[64 * j + lane] = 0.0;  // kept zero between MATCH passes
   double* slab = P.scratch + (size_t)(blockIdx.x * nwaves + wave) * P.slab_doubles;
+  double* gamtab = P.gam_on ? P.gam + (size_t)blockIdx.x * P.gam_doubles : nullptr;
   const double gap2 = P.gap2;
+  const int band = (int)P.band;
 
   // wave index as an SGPR value: every branch below on it is wave-uniform
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -773,6 +854,54 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     }
     __syncthreads();
 
+    // Gamma rows of this y (gapless y only): for every gamma key g = (code,
+    // len) of the x set, Gamma_g = the IY sweep of M_g[q] = co[code][bp(q)]
+    // p(q) g^{leaf gaps(q)} over the y loop nodes q in len's length band (an
+    // x gamma row's G0 row is g^lg pf Gamma_g; its MATCH row is that times
+    // M_g), into this workgroup's table; kappa_g = sum_q M_g[q] P_y[q].
+    const bool gam = P.gam_on && s.ex_gapless[y];
+    if (gam) {
+      const DevSet& xset = P.xset;
+      for (int g = wave_u; g < xset.n_gam; g += nwaves) {
+        const uint32_t key = xset.gam_key[g];
+        const int gcode = (int)(key >> 16) * 16, glen = (int)(key & 0xffff);
+        double kp = 0.0;
+        for (int k = 0; k < MAXK; ++k) {
+          const int q = lane + 64 * k;
+          double M = 0.0;
+          if (q < Y.nl) {
+            const uint4 nd = Y.nrg[q];
+            const int ylen = (int)(s.yn_b[nb + q] & 0xffff);
+            if (((nd.x >> 16) & 0xff) == 0 && (band == 0 || abs(glen - ylen) <= band)) {
+              double vs;
+              if ((nd.y >> 24) != 0u) {
+                vs = co[gcode + ((nd.y >> 16) & 0xf)] * (double)__uint_as_float(nd.w);
+              } else {
+                vs = 0.0;
+                const int yb0 = (int)(s.yn_b[nb + q] >> 16), ynb = (int)(nd.x >> 24);
+                for (int b = 0; b < ynb; ++b)
+                  vs += co[gcode + s.bpf_code[bb + yb0 + b]] * (double)s.bpf_p[bb + yb0 + b];
+              }
+              M = vs * gp[nd.y & 0xffff];
+              kp += M * s.yn_P[nb + q];
+            }
+          }
+          R[q] = M;
+        }
+        for (int off = 32; off > 0; off >>= 1) kp += __shfl_xor(kp, off, 64);
+        if (lane == 0) kap[g] = kp;
+        wave_sync();
+        int c0 = 0;
+        if (band > 0) c0 = Y.ycs[min(max(glen - band, 0), Y.lmax + 1)];
+        c0 = __builtin_amdgcn_readfirstlane(c0);
+        if (c0 < Y.nch) iy_sweep(Y, R, c0, lane);
+        double* grow = gamtab + (size_t)g * (64 * MAXK);
+        for (int k = 0; k < MAXK; ++k) grow[lane + 64 * k] = R[lane + 64 * k];
+        wave_sync();
+      }
+      __syncthreads();  // the table and kappa, for every wave's pairs
+    }
+
     // the item's pairs (costliest first) go to whichever wave is free next
     // (the first nwaves dealt statically; ctl[1] counts the pairs taken), so
     // the workgroup waits at the item boundary for one pair, not a round
@@ -780,7 +909,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     __syncthreads();
     for (int t = wave_u; t < item.z;) {
       const int x = P.xs[item.y + t];
-      const double k = stem_pair<MAXK>(P, Y, R, hb, co, gp, slab, x, lane);
+      const double k = stem_pair<MAXK>(P, Y, R, hb, co, gp, slab, x, lane, gam, gamtab, kap);
       if (lane == 0) P.out[P.oidx[item.y + t]] = k;
       int nt = 0;
       // generic-pointer atomic on the LDS counter
@@ -809,6 +938,7 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += (size_t)P.lds_max_nch * 64 * 12;            // sweep schedule: weights + records
   b += (size_t)P.lds_max_edges * 4;                // node-major edges
   b += (size_t)P.lds_max_len_pad * 4 * 2 + 16;     // length tables, control
+  if (P.gam_on) b += (size_t)P.xset.n_gam * 8;     // Gamma sums kappa
   return b;
 }
 

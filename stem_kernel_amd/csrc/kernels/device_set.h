@@ -85,6 +85,27 @@ struct DevSet {
   const int32_t* ex_nch = nullptr;
   const int32_t* ycs = nullptr;
   const int32_t* ex_ycs_base = nullptr;
+  // Gamma schedule (dag_stem.hip): the x rows in post-order without the gamma
+  // rows (x loop rows with one bp-frequency entry and no gap column, whose G0
+  // row is g^lg pf Gamma_{code,len}(y)); a child record with bit 15 set is a
+  // gamma child (low bits: gamma index), its weight factors in xg_clg
+  // (loop leaf gaps) and xg_cpf (pf); gr_* lists the gamma rows for their K
+  // terms.  gam_key[g] = code:16 | len:16, n_gam keys over the set.
+  const XRow* xgrow = nullptr;
+  const uint32_t* xg_node = nullptr;
+  const uint32_t* xg_ch = nullptr;
+  const uint32_t* xg_clg = nullptr;
+  const float* xg_cpf = nullptr;
+  const int32_t* ex_xg_base = nullptr;
+  const int32_t* ex_nlxg = nullptr;
+  const int32_t* ex_xgch_base = nullptr;
+  const uint32_t* gr_info = nullptr;  // gamma index:16 | loop leaf gaps:16
+  const float* gr_pf = nullptr;
+  const double* gr_P = nullptr;
+  const int32_t* ex_gr_base = nullptr;  // n_examples + 1 entries
+  const int32_t* ex_gapless = nullptr;  // y role: no gap column in any non-leaf node
+  const uint32_t* gam_key = nullptr;
+  int32_t n_gam = 0;
   // maxima over the set
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
   int32_t max_nch = 0;
@@ -96,6 +117,13 @@ struct DevParamNodes {
   double* nd_L = nullptr;   // G0 at (node, any y-leaf column), level order
   double* nd_SL = nullptr;  // sum_e g^gaps(e) * L[child(e)], level order
   double* xr_SL = nullptr;  // nd_SL in x-row (post-)order
+  // gamma schedule: nd_SL per row, child weights g^gaps (x g^lg pf for a
+  // gamma child), and per example sum over its gamma rows of P g^lg pf by
+  // gamma index (n_examples x n_gam)
+  double* xg_SL = nullptr;
+  double* xg_chw = nullptr;
+  double* gam_h = nullptr;
+  double* xr_chw = nullptr;  // x schedule child weights g^gaps
 };
 
 }  // namespace sk

@@ -31,6 +31,11 @@ struct StemLaunch {
   int* item_counter = nullptr;
   double* scratch = nullptr;   // per-wave G0 slabs
   int64_t slab_doubles = 0;
+  // Gamma rows (gam_on: the x set has gamma keys): per-workgroup table of
+  // xset.n_gam rows of 64*MAXK doubles, Gamma_g(y) of the current item's y
+  double* gam = nullptr;
+  int64_t gam_doubles = 0;  // per workgroup
+  int32_t gam_on = 0;
   unsigned long long* stamps = nullptr;  // diagnostic builds (SK_STAMPS) only
 };
 

@@ -96,6 +96,13 @@ struct HostPack {
   std::vector<double> yn_P;
   std::vector<int32_t> ycs, ex_ysc_base, ex_nch, ex_ycs_base;
   std::vector<uint32_t> xr_node, xr_ch;
+  // gamma schedule (device_set.h): the x rows without the gamma rows, the
+  // gamma rows' K inputs, the dataset's gamma keys and the y gapless flags
+  std::vector<sk::XRow> xgrow;
+  std::vector<uint32_t> xg_node, xg_ch, xg_clg, gr_info, gam_key;
+  std::vector<float> xg_cpf, gr_pf;
+  std::vector<double> gr_P;
+  std::vector<int32_t> ex_xg_base, ex_nlxg, ex_xgch_base, ex_gr_base, ex_gapless;
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
   int32_t max_nch = 0;
 };
@@ -262,6 +269,32 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
   const bool sweep_lanes_greedy = !lanes_env || std::atoi(lanes_env) != 0;
   P = HostPack();
   const int n = (int)ds->ex.size();
+  // Gamma rows: x loop rows (one leaf child) with one bp-frequency entry and
+  // no gap column.  Their G0 row is (g^gaps pf) x Gamma_{code,len}(y), the
+  // IY sweep of a y-only vector (dag_stem.hip), so the gamma schedule skips
+  // them; the dataset's (code, len) keys index the per-y Gamma rows.
+  auto is_gamma = [&](const Example& X, int v) {
+    const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
+    if (e1 - e0 != 1) return false;
+    const uint32_t c = X.edge_to[e0];
+    if (X.edge_off[c + 1] != X.edge_off[c]) return false;  // the child is not a leaf: a stem
+    return X.bpf_off[v + 1] - X.bpf_off[v] == 1 && X.prof5[(size_t)X.first[v] * 5 + 4] == 0.0f;
+  };
+  auto gamma_key = [&](const Example& X, int v) {
+    return ((uint32_t)X.bpf_code[X.bpf_off[v]] << 16) | (uint32_t)(X.last[v] - X.first[v]);
+  };
+  for (int e = 0; e < n; ++e) {
+    const Example& X = ds->ex[e];
+    for (int v = 0; v < X.n_nodes(); ++v)
+      if (is_gamma(X, v)) P.gam_key.push_back(gamma_key(X, v));
+  }
+  std::sort(P.gam_key.begin(), P.gam_key.end());
+  P.gam_key.erase(std::unique(P.gam_key.begin(), P.gam_key.end()), P.gam_key.end());
+  const bool gam_on = !P.gam_key.empty() && P.gam_key.size() <= 512 && !std::getenv("SK_NO_GAMMA");
+  if (!gam_on) P.gam_key.clear();
+  auto gamma_idx = [&](uint32_t key) {
+    return (uint32_t)(std::lower_bound(P.gam_key.begin(), P.gam_key.end(), key) - P.gam_key.begin());
+  };
   P.ex_node_base.push_back(0);
   P.ex_edge_base.push_back(0);
   P.ex_bpf_base.push_back(0);
@@ -548,6 +581,81 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       }
       P.ex_nslots.push_back(nslots);
       P.max_slots = std::max(P.max_slots, nslots);
+
+      // the gamma schedule: the same post-order without the gamma rows
+      // (slots only among the remaining rows; a gamma child is a record
+      // 0x8000 | gamma index, its weight factors g^lg pf in xg_clg / xg_cpf)
+      P.ex_xg_base.push_back((int32_t)P.xgrow.size());
+      P.ex_xgch_base.push_back((int32_t)P.xg_ch.size());
+      P.ex_gr_base.push_back((int32_t)P.gr_info.size());
+      std::vector<uint32_t> gslot(nn, 0xffff);
+      std::vector<int> gfree;
+      int gslots = 0, nlxg = 0;
+      for (int v = 0; v < nn; ++v) {
+        if (level[v] < 0) continue;
+        const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
+        const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
+        if (gam_on && is_gamma(X, v)) {
+          P.gr_info.push_back(gamma_idx(gamma_key(X, v)) | (X.edge_gaps[e0] << 16));
+          P.gr_pf.push_back(X.bpf_p[b0]);
+          P.gr_P.push_back(Pw[v]);
+          continue;
+        }
+        const bool loop = level[v] == 0;
+        uint32_t nch = 0;
+        if (!loop) {
+          for (uint32_t k = e0; k < e1; ++k) {
+            const int c = X.edge_to[k];
+            if (gam_on && is_gamma(X, c)) {
+              P.xg_ch.push_back((0x8000u | gamma_idx(gamma_key(X, c))) | (X.edge_gaps[k] << 16));
+              P.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
+              P.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
+            } else {
+              P.xg_ch.push_back(gslot[c] | (X.edge_gaps[k] << 16));
+              P.xg_clg.push_back(0u);
+              P.xg_cpf.push_back(1.0f);
+            }
+            ++nch;
+          }
+        }
+        for (uint32_t k = e0; k < e1; ++k) {
+          const int c = X.edge_to[k];
+          if (level[c] >= 0 && last_parent[c] == v && gslot[c] != 0xffff) gfree.push_back(gslot[c]);
+        }
+        if (last_parent[v] >= 0) {
+          int sl;
+          if (!gfree.empty()) {
+            sl = gfree.back();
+            gfree.pop_back();
+          } else {
+            sl = gslots++;
+          }
+          gslot[v] = (uint32_t)sl;
+        }
+        sk::XRow xr;
+        xr.a = nch | ((b1 - b0) << 8) | ((loop ? X.edge_gaps[e0] : 0u) << 16);
+        xr.b = (X.last[v] - X.first[v]) | (gslot[v] << 16);
+        xr.w = X.weight[v];
+        xr.nbp = X.prof5[(size_t)X.first[v] * 5 + 4];
+        xr.bp0 = b1 > b0 ? X.bpf_p[b0] : 0.0f;
+        xr.P = Pw[v];
+        xr.c = (P.nd_b[P.ex_node_base.back() + nid[v]] >> 16) |
+               ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16);
+        P.xgrow.push_back(xr);
+        P.xg_node.push_back((uint32_t)nid[v]);
+        ++nlxg;
+      }
+      if (gslots >= 0x8000) {  // slot ids share the record with the gamma flag
+        err = "too many live DAG rows";
+        return SK_ERR_UNSUPPORTED;
+      }
+      P.ex_nlxg.push_back(nlxg);
+      P.max_slots = std::max(P.max_slots, gslots);
+    }
+    {  // y role: no gap column in any non-leaf node (the Gamma rows need it)
+      bool gl = true;
+      for (int k = 0; k < nl; ++k) gl &= P.nd_nbp[P.ex_node_base.back() + k] == 0.0f;
+      P.ex_gapless.push_back(gl ? 1 : 0);
     }
     P.ex_nl.push_back(nl);
     P.ex_nlev.push_back(nlev);
@@ -1232,6 +1340,8 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       L.lds_max_len_pad = (max_len + 2 + 3) & ~3;
       L.n_gpow = max_len + 2;
       L.n_gpow_pad = (L.n_gpow + 1) & ~1;
+      L.xset.n_gam = (int32_t)PX.gam_key.size();
+      L.gam_on = L.xset.n_gam > 0;
       int max_dyn = 0, vgprs = 0, max_w = 8;
       SK_HIP(ctx, sk::stem_kernel_attr(L.lds_max_nl, &max_dyn, &vgprs, &max_w));
       const int valloc = ((std::max(vgprs, 1) + 7) / 8) * 8;
@@ -1376,14 +1486,24 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     SK_HIP(ctx, hipMemcpyAsync(d_oidx, ioidx.data(), nb * 8, hipMemcpyHostToDevice, S));
     const double gap2 = kp->loop_gap * kp->loop_gap;
     const size_t nnd = std::max<size_t>(PX.nd_a.size(), 1);
+    const size_t nxc = std::max<size_t>(PX.xr_ch.size(), 1), nxg = std::max<size_t>(PX.xgrow.size(), 1),
+                 nxgc = std::max<size_t>(PX.xg_ch.size(), 1),
+                 ngh = std::max<size_t>(PX.ex_nl.size() * PX.gam_key.size(), 1);
     if (!xs_->prep) {
       void* p = nullptr;
-      SK_HIP(ctx, hipMalloc(&p, 3 * nnd * sizeof(double)));
+      SK_HIP(ctx, hipMalloc(&p, (3 * nnd + nxc + nxg + nxgc + ngh) * sizeof(double)));
       xs_->prep = static_cast<double*>(p);
       xs_->buf.ptrs.push_back(p);
       xs_->prep_loop_gap = -1.0;
     }
-    sk::DevParamNodes pn{xs_->prep, xs_->prep + nnd, xs_->prep + 2 * nnd};
+    sk::DevParamNodes pn;
+    pn.nd_L = xs_->prep;
+    pn.nd_SL = xs_->prep + nnd;
+    pn.xr_SL = xs_->prep + 2 * nnd;
+    pn.xr_chw = xs_->prep + 3 * nnd;
+    pn.xg_SL = pn.xr_chw + nxc;
+    pn.xg_chw = pn.xg_SL + nxg;
+    pn.gam_h = pn.xg_chw + nxgc;
     if (!(xs_->prep_loop_gap == kp->loop_gap)) {  // once per dataset and loop_gap
       SK_HIP(ctx, sk::launch_prep(xs_->dev, pn, d_gp_loop, gap2, S));
       xs_->prep_loop_gap = kp->loop_gap;
@@ -1393,7 +1513,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     for (const StemClass& C : classes) {
       // + one junk row: root rows are stored there (never read)
       const int64_t slab = (int64_t)(PX.max_slots + 1) * 64 * C.maxk;
-      scratch_need = std::max(scratch_need, (size_t)C.grid * C.nwaves * slab * sizeof(double));
+      // + the workgroups' Gamma tables
+      const int64_t gtab = (int64_t)PX.gam_key.size() * 64 * C.maxk;
+      scratch_need = std::max(scratch_need, (size_t)C.grid * (C.nwaves * slab + gtab) * sizeof(double));
     }
     // big-y kernel: per wave S, G1 and the G0 slots, rows of `big_stride`
     // doubles; as many waves as pairs, the grid, and a scratch budget allow
@@ -1444,6 +1566,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.item_counter = d_ctr + 16 + (int)c;
       SL.slab_doubles = (int64_t)(PX.max_slots + 1) * SL.lds_max_nl;
       SL.scratch = ctx->scratch;
+      SL.gam_on = !PX.gam_key.empty();
+      SL.gam_doubles = (int64_t)PX.gam_key.size() * SL.lds_max_nl;
+      SL.gam = ctx->scratch + (size_t)C.grid * C.nwaves * SL.slab_doubles;
 #ifdef SK_STAMPS
       SL.stamps = d_stamps;
 #endif
@@ -2091,6 +2216,25 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.ex_ycs_base, &D.ex_ycs_base));
   SK_HIP(ctx, upload(B, P.xr_node, &D.xr_node));
   SK_HIP(ctx, upload(B, P.xr_ch, &D.xr_ch));
+  SK_HIP(ctx, upload(B, P.xgrow, &D.xgrow));
+  SK_HIP(ctx, upload(B, P.xg_node, &D.xg_node));
+  SK_HIP(ctx, upload(B, P.xg_ch, &D.xg_ch));
+  SK_HIP(ctx, upload(B, P.xg_clg, &D.xg_clg));
+  SK_HIP(ctx, upload(B, P.xg_cpf, &D.xg_cpf));
+  SK_HIP(ctx, upload(B, P.ex_xg_base, &D.ex_xg_base));
+  SK_HIP(ctx, upload(B, P.ex_nlxg, &D.ex_nlxg));
+  SK_HIP(ctx, upload(B, P.ex_xgch_base, &D.ex_xgch_base));
+  {
+    std::vector<int32_t> grb = P.ex_gr_base;
+    grb.push_back((int32_t)P.gr_info.size());
+    SK_HIP(ctx, upload(B, grb, &D.ex_gr_base));
+  }
+  SK_HIP(ctx, upload(B, P.gr_info, &D.gr_info));
+  SK_HIP(ctx, upload(B, P.gr_pf, &D.gr_pf));
+  SK_HIP(ctx, upload(B, P.gr_P, &D.gr_P));
+  SK_HIP(ctx, upload(B, P.ex_gapless, &D.ex_gapless));
+  SK_HIP(ctx, upload(B, P.gam_key, &D.gam_key));
+  D.n_gam = (int32_t)P.gam_key.size();
   D.max_nl = P.max_nl;
   D.max_edges = P.max_edges;
   D.max_bpf = P.max_bpf;
