@@ -149,6 +149,11 @@ struct sk_context {
   // persistent stem launches and fills the CUs their tails free
   hipStream_t side = nullptr;
   hipEvent_t evf = nullptr, evj = nullptr;
+  // second class stream: DAG stem register classes alternate between the
+  // main stream and this one, so a class's fill overlaps the previous one's
+  // tail
+  hipStream_t cls = nullptr;
+  hipEvent_t evk = nullptr, evx = nullptr;
   double last_stem_ms = 0.0, last_str_ms = 0.0, last_cells = 0.0;
   int32_t last_launches = 0;
   // kernel instantiations the last compute call launched (sk_last_classes):
@@ -1508,14 +1513,19 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SK_HIP(ctx, sk::launch_prep(xs_->dev, pn, d_gp_loop, gap2, S));
       xs_->prep_loop_gap = kp->loop_gap;
     }
-    // one scratch buffer serves the class launches in turn (same stream)
-    size_t scratch_need = 0;
-    for (const StemClass& C : classes) {
+    // class c runs on the main stream (c even) or the class stream (c odd):
+    // one scratch region per stream, serving its classes in turn
+    const bool two_streams = classes.size() > 1 && !std::getenv("SK_SERIAL_CLASSES");
+    size_t scratch_need = 0, scratch_x = 0;
+    for (size_t c = 0; c < classes.size(); ++c) {
+      const StemClass& C = classes[c];
       // + one junk row: root rows are stored there (never read)
       const int64_t slab = (int64_t)(PX.max_slots + 1) * 64 * C.maxk;
       // + the workgroups' Gamma tables
       const int64_t gtab = (int64_t)PX.gam_key.size() * 64 * C.maxk;
-      scratch_need = std::max(scratch_need, (size_t)C.grid * (C.nwaves * slab + gtab) * sizeof(double));
+      const size_t b = (size_t)C.grid * (C.nwaves * slab + gtab) * sizeof(double);
+      size_t& r = (two_streams && (c & 1)) ? scratch_x : scratch_need;
+      r = std::max(r, b);
     }
     // big-y kernel: per wave S, G1 and the G0 slots, rows of `big_stride`
     // doubles; as many waves as pairs, the grid, and a scratch budget allow
@@ -1533,16 +1543,23 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       scratch_need = std::max(scratch_need,
                               (size_t)big_grid * sk::kStemBigWaves * (size_t)big_wave * sizeof(double));
     }
-    rc = ensure_scratch(ctx, std::max<size_t>(scratch_need, 64));
+    scratch_need = (scratch_need + 255) / 256 * 256;
+    rc = ensure_scratch(ctx, std::max<size_t>(scratch_need + scratch_x, 64));
     if (rc) return rc;
+    double* scratch_cls = ctx->scratch + scratch_need / sizeof(double);
 #ifdef SK_STAMPS
     unsigned long long* d_stamps = nullptr;
     SK_HIP(ctx, hipMalloc(&d_stamps, 16 * sizeof(unsigned long long)));
     SK_HIP(ctx, hipMemsetAsync(d_stamps, 0, 16 * sizeof(unsigned long long), S));
 #endif
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
+    if (two_streams) {
+      SK_HIP(ctx, hipEventRecord(ctx->evk, S));
+      SK_HIP(ctx, hipStreamWaitEvent(ctx->cls, ctx->evk, 0));
+    }
     for (size_t c = 0; c < classes.size(); ++c) {
       const StemClass& C = classes[c];
+      const bool on_cls = two_streams && (c & 1);
       sk::StemLaunch SL;
       SL.xset = xs_->dev;
       SL.yset = ys_->dev;
@@ -1565,15 +1582,19 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.out = stem_out;
       SL.item_counter = d_ctr + 16 + (int)c;
       SL.slab_doubles = (int64_t)(PX.max_slots + 1) * SL.lds_max_nl;
-      SL.scratch = ctx->scratch;
+      SL.scratch = on_cls ? scratch_cls : ctx->scratch;
       SL.gam_on = !PX.gam_key.empty();
       SL.gam_doubles = (int64_t)PX.gam_key.size() * SL.lds_max_nl;
-      SL.gam = ctx->scratch + (size_t)C.grid * C.nwaves * SL.slab_doubles;
+      SL.gam = SL.scratch + (size_t)C.grid * C.nwaves * SL.slab_doubles;
 #ifdef SK_STAMPS
       SL.stamps = d_stamps;
 #endif
-      SK_HIP(ctx, sk::launch_stem(SL, C.grid, C.nwaves, S));
+      SK_HIP(ctx, sk::launch_stem(SL, C.grid, C.nwaves, on_cls ? ctx->cls : S));
       ctx->last_stem_classes |= 1u << (C.maxk / 4);
+    }
+    if (two_streams) {
+      SK_HIP(ctx, hipEventRecord(ctx->evx, ctx->cls));
+      SK_HIP(ctx, hipStreamWaitEvent(S, ctx->evx, 0));
     }
     if (!big_x.empty()) {
       const size_t nbig = big_x.size();
@@ -1976,8 +1997,11 @@ int sk_open(int device, void* hip_stream, sk_context** out) {
     c->own_stream = true;
   }
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->cls, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->evf, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evk, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evx, hipEventDisableTiming) != hipSuccess)
     return SK_ERR_HIP;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess)
@@ -1998,7 +2022,8 @@ int sk_close(sk_context* ctx) {
   if (ctx->s4d.items) (void)hipFree(ctx->s4d.items);
   if (ctx->s4d.band) (void)hipFree(ctx->s4d.band);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
-  for (hipEvent_t e : {ctx->evf, ctx->evj})
+  if (ctx->cls) (void)hipStreamDestroy(ctx->cls);
+  for (hipEvent_t e : {ctx->evf, ctx->evj, ctx->evk, ctx->evx})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3})
     if (e) (void)hipEventDestroy(e);

@@ -1,10 +1,4 @@
-# One GPU round trip (run through gpurun from the repo root): the HIP parity
-# suite, the driver's smoke check and the default (north-star) bench line.
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -1 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
-tail -1 gpurun_out/smoke.log
-timeout -k 10 600 python3 -u bench.py > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
-tail -1 gpurun_out/bench.log | cut -c1-160
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_large_configs.py tests/test_gamma.py tests/test_gpu_parity.py > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+tail -2 gpurun_out/t.log
+bash tools/gpu_quick.sh c2 ns c5 && SK_SERIAL_CLASSES=1 bash tools/gpu_quick.sh c2 ns
