@@ -49,7 +49,7 @@ __device__ __forceinline__ double la_score_f(const double (&u)[4], float4 xc, fl
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int l = 0; l < 4; ++l) n = __fadd_rn(n, __fmul_rn(xa[k], yb[l]));
+      for (int l = 0; l < 4; ++l) n = f32_madd(n, xa[k], yb[l]);
   }
   const double v = u[0] * (double)yb[0] + u[1] * (double)yb[1] + u[2] * (double)yb[2] +
                    u[3] * (double)yb[3];
@@ -158,8 +158,8 @@ __global__ void __launch_bounds__(256) sk_bpla_kernel(BplaLaunch P) {
         double s = la_score_f(u, xc, yc, xsum, yw.w);
         if (bp) {
           // BPLAScore (bpla_kernel.cpp:55-60): float products as written
-          const float pp = __fadd_rn(__fmul_rn(xw.y, yw.y), __fmul_rn(xw.x, yw.x));
-          const float uu = __fmul_rn(xw.z, yw.z);
+          const float pp = f32_dot2(xw.y, yw.y, xw.x, yw.x);
+          const float uu = xw.z * yw.z;
           s = alpha * (double)pp + (double)uu * s;
         }
         // the left cell (i, j-1); column 0 is zero.  (lM.. keep the last
@@ -304,109 +304,208 @@ hipError_t launch_bpla_tab(const float4* prof, const float4* lru, int64_t n, con
   return hipGetLastError();
 }
 
-// One pair on one wavefront: ycol holds y's operand columns (LDS), bnd is the
-// wave's boundary row; returns K in every lane.
+// A chunk of np pairs sharing y on one wavefront: their x rows are streamed
+// back to back as one sequence of rows (chunk row G = first row of pair p +
+// local row i), so a strip may end one pair's rows and start the next's and
+// the drain of a partly filled last strip is paid once per chunk, not per
+// pair.  ci[p] = {xtab base, Lx, first chunk row, -} (LDS), ksum[p] receives
+// the pair's sum of M cells (exp) or its max (SW: np == 1).  ycol holds y's
+// operand columns (LDS), bnd is the wave's boundary row.
+//
+// Lane l computes chunk row 64s + l + 1 of strip s, one column per step, a
+// step behind lane l-1 (DPP wave_shr); a lane moves on to its row of the
+// next strip right after its last column.  The steps fall in wave-uniform
+// phases: the 64-step WINDOW of strip s (step w: lane w starts its new row
+// at column 1, lanes above it finish strip s-1's row), then the INTERIOR
+// (every lane inside strip s, columns 2..Ly: no per-lane control flow at
+// all).  The next strip's row operands are loaded for all lanes at the end
+// of a window, a strip ahead of their use.  The first row of a pair sees row
+// 0 (zero) above it: its "up" and "diagonal" inputs are scaled by fb = 0
+// (folded into the coefficients, no extra instruction per cell).
 template <bool SW, bool BP>
-__device__ __forceinline__ double bpla_fast_pair(const BplaLaunch& P, int x, int y,
-                                                 const BplaPos* ycol, double* bnd,
-                                                 const double* etab, int lane) {
+__device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, const int4* ci,
+                                                double* ksum, int Ly, const BplaPos* ycol,
+                                                double* bnd, const double* etab, int lane) {
   const double alpha = P.alpha, beta = P.beta, gap = P.gap, ext = P.ext;
   const double bg = P.beta_gap, be = P.beta_ext;
-  const int Lx = __builtin_amdgcn_readfirstlane(P.xset.ex_len[x]);
-  const int Ly = __builtin_amdgcn_readfirstlane(P.yset.ex_len[y]);
-  const int xpb = __builtin_amdgcn_readfirstlane(P.xset.ex_pos_base[x]);
+  const int4 last = ci[np - 1];
+  const int Rt = __builtin_amdgcn_readfirstlane(last.z + last.y);  // rows of the chunk
   const int Lys = max(Ly, 64);
   for (int j = lane; j < 3 * (Lys + 1); j += 64) bnd[j] = 0.0;  // row 0
+  if (lane < np) ksum[lane] = 0.0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int nstrips = (Lx + 63) / 64;
-  int j = 1 - lane, i = lane + 1;
-  // byte offset of y column j-1 in ycol (advances with j)
-  unsigned yofs = (unsigned)(j - 1) * (unsigned)sizeof(BplaPos);
+  if (Rt == 0 || Ly == 0) return;  // no cells: K = 1 (exp) / 0 (SW)
+  const int nstrips = (Rt + 63) / 64;
+  const int T = (nstrips - 1) * Lys + ((Rt - 1) & 63) + Ly;  // steps
   const char* ybase = reinterpret_cast<const char*>(ycol);
-  bool row_ok = i <= Lx;
-  // my row's operands and the next strip's (prefetched from the table)
-  BplaPos xr = P.xtab[xpb + (row_ok ? i - 1 : 0)];
-  BplaPos xnext = P.xtab[xpb + (i + 64 <= Lx ? i + 63 : 0)];
+
+  // chunk row G (1-based) -> its pair, whether it exists, fb, xtab index
+  auto map_row = [&](int G, int& pp, bool& ok, double& fbv, int& xi) __attribute__((always_inline)) {
+    int q = 0;
+    for (int k = 1; k < np; ++k) q += G - 1 >= ci[k].z ? 1 : 0;
+    const int4 c = ci[q];
+    const int i = G - c.z;
+    ok = G <= Rt;
+    pp = q;
+    fbv = i == 1 ? 0.0 : 1.0;
+    xi = ok ? c.x + i - 1 : ci[0].x;
+  };
+  int pn, xi;
+  bool okn;
+  double fbn;
+  map_row(lane + 1, pn, okn, fbn, xi);
+  BplaPos xn = P.xtab[xi];  // the next strip's row operands (strip 0 first)
+  BplaPos xr = xn;
+  int p = 0;                // my row's pair
+  bool row_ok = false;      // my row exists (and has started)
+  double fb = 1.0, cbg = bg, cbe = be;  // 0 / 0 / 0 on a pair's first row
+  unsigned yofs = 0;        // byte offset of my column j-1 in ycol
   double lM = 0.0, lX = 0.0, lY = 0.0;  // (i, j-1): my previous output
-  double acc = 0.0;                      // sum of my M cells (exp) / max (SW)
-  // one step: d* = (i-1, j-1) received a step earlier; u* receives (i-1, j)
-  auto step = [&](double& dM, double& dX, double& dY, double& uM, double& uX, double& uY) {
-    // lane 0 takes row i-1 from the boundary row; row 0 is zero, and a
-    // strip's boundary column is written 63 steps before lane 0 reads it
-    const int jb = __builtin_amdgcn_readfirstlane(j);
-    const double* bj = bnd + 3 * (jb >= 1 && jb <= Ly ? jb : 0);
+  double acc = 0.0;                      // sum of my row's M cells (exp) / max (SW)
+
+  // cell (i, j) from d = (i-1, j-1), u = (i-1, j) and l = (i, j-1); c1: j == 1
+  auto cell = [&](double dM, double dX, double dY, double uM, double uX, double uY, bool c1,
+                  double& nM, double& nX, double& nY) __attribute__((always_inline)) {
+    const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+    double s = xr.v[0] * yc.v[0];
+    s = __builtin_fma(xr.v[1], yc.v[1], s);
+    s = __builtin_fma(xr.v[2], yc.v[2], s);
+    s = __builtin_fma(xr.v[3], yc.v[3], s);
+    if (BP) {
+      // BPLAScore (bpla_kernel.cpp:55-60): float products as written
+      const float pp = f32_dot2(xr.pr, yc.pr, xr.pl, yc.pl);
+      const float uu = xr.pu * yc.pu;
+      s = alpha * (double)pp + (double)uu * s;
+    }
+    if (!SW) {
+      nM = fast_exp(beta * s, etab, P.ec) * __builtin_fma(fb, dX + dY + dM, 1.0);
+      nX = cbg * uM + cbe * uX;
+      nY = c1 ? 0.0 : bg * (lM + lX) + be * lY;  // column 0 is zero
+      acc += row_ok ? nM : 0.0;
+    } else {
+      nM = fmax(fmax(fmax(0.0, fb * dM), fb * dX), fb * dY) + s;
+      nX = fmax(fb * uM + gap, fb * uX + ext);
+      // column 0 is zero: max(0 + gap, 0 + gap, 0 + ext)
+      nY = c1 ? fmax(gap, ext) : fmax(fmax(lM + gap, lX + gap), lY + ext);
+      if (row_ok) acc = fmax(acc, nM);
+    }
+  };
+
+  // step of an interior: lane 0's column jb (uniform); every lane active
+  auto interior = [&](int jb, double& dM, double& dX, double& dY, double& uM, double& uX,
+                      double& uY) __attribute__((always_inline)) {
+    const double* bj = bnd + 3 * jb;
     uM = wave_shr1(lM, bj[0]);
     uX = wave_shr1(lX, bj[1]);
     uY = wave_shr1(lY, bj[2]);
-    if (j >= 1 && j <= Ly) {
-      const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
-      double s = xr.v[0] * yc.v[0];
-      s = __builtin_fma(xr.v[1], yc.v[1], s);
-      s = __builtin_fma(xr.v[2], yc.v[2], s);
-      s = __builtin_fma(xr.v[3], yc.v[3], s);
-      if (BP) {
-        // BPLAScore (bpla_kernel.cpp:55-60): float products as written
-        const float pp = __fadd_rn(__fmul_rn(xr.pr, yc.pr), __fmul_rn(xr.pl, yc.pl));
-        const float uu = __fmul_rn(xr.pu, yc.pu);
-        s = alpha * (double)pp + (double)uu * s;
+    double nM, nX, nY;
+    cell(dM, dX, dY, uM, uX, uY, false, nM, nX, nY);
+    lM = nM;
+    lX = nX;
+    lY = nY;
+    if (lane == 63) {  // lane 63's column is jb - 63
+      double* bw = bnd + 3 * (jb - 63);
+      bw[0] = nM;
+      bw[1] = nX;
+      bw[2] = nY;
+    }
+    yofs += (unsigned)sizeof(BplaPos);
+  };
+
+  // step w of strip s's window: lane w starts its row of strip s at column 1
+  // (diagonal and left are column 0: zero), handing its finished row's sum
+  // to the pair; lanes below it are at column w - lane + 1 of strip s, lanes
+  // above at column Lys + w - lane + 1 of strip s-1 (none for s = 0).  The
+  // window of s = nstrips is the drain: only the last strip's lanes above w
+  // are still working.
+  auto window = [&](int s, int w, double& dM, double& dX, double& dY, double& uM, double& uX,
+                    double& uY) __attribute__((always_inline)) {
+    const bool wrap = lane == w;
+    if (wrap) {
+      if (row_ok) {
+        if (SW) ksum[p] = fmax(ksum[p], acc);
+        else ksum[p] += acc;
       }
-      const bool c1 = j == 1;  // column 0 is zero
+      acc = 0.0;
+      xr = xn;
+      p = pn;
+      row_ok = okn;
+      fb = fbn;
+      cbg = bg * fbn;
+      cbe = be * fbn;
+      yofs = 0;
+      dM = dX = dY = 0.0;
+    }
+    const int jl = lane <= w ? w - lane + 1 : Lys + w - lane + 1;
+    const bool on = jl <= Ly && (lane <= w ? s < nstrips : s > 0);
+    const int jb = w + 1;  // lane 0's column (strip s)
+    const double* bj = bnd + 3 * (jb <= Ly ? jb : 0);
+    uM = wave_shr1(lM, bj[0]);
+    uX = wave_shr1(lX, bj[1]);
+    uY = wave_shr1(lY, bj[2]);
+    if (on) {
       double nM, nX, nY;
-      if (!SW) {
-        nM = fast_exp(beta * s, etab, P.ec) * (1.0 + dX + dY + dM);
-        nX = bg * uM + be * uX;
-        nY = c1 ? 0.0 : bg * (lM + lX) + be * lY;
-        if (row_ok) acc += nM;
-      } else {
-        nM = fmax(fmax(fmax(0.0, dM), dX), dY) + s;
-        nX = fmax(uM + gap, uX + ext);
-        // column 0 is zero: max(0 + gap, 0 + gap, 0 + ext)
-        nY = c1 ? fmax(gap, ext) : fmax(fmax(lM + gap, lX + gap), lY + ext);
-        if (row_ok) acc = fmax(acc, nM);
-      }
+      cell(dM, dX, dY, uM, uX, uY, wrap, nM, nX, nY);
       lM = nM;
       lX = nX;
       lY = nY;
       if (lane == 63) {
-        double* bw = bnd + 3 * j;
+        double* bw = bnd + 3 * jl;
         bw[0] = nM;
         bw[1] = nX;
         bw[2] = nY;
       }
     }
     yofs += (unsigned)sizeof(BplaPos);
-    if (++j > Lys) {  // next strip: row i + 64, column 1
-      j = 1;
-      yofs = 0;
-      i += 64;
-      row_ok = i <= Lx;
-      xr = xnext;
-      if (i + 64 <= Lx) xnext = P.xtab[xpb + i + 63];
-      uM = uX = uY = 0.0;
-    }
   };
-  double aM = 0.0, aX = 0.0, aY = 0.0, bM_ = 0.0, bX_ = 0.0, bY_ = 0.0;
-  const int T = (nstrips - 1) * Lys + ((Lx - 1) & 63) + Ly;
-  int t = 0;
-  for (; t + 1 < T; t += 2) {  // two steps, the d/u roles alternate
-    step(aM, aX, aY, bM_, bX_, bY_);
-    step(bM_, bX_, bY_, aM, aX, aY);
+
+  // d* = values received a step earlier, u* = this step's; the unrolled
+  // pairs of steps swap their roles (no register copies)
+  double aM = 0.0, aX = 0.0, aY = 0.0, bM = 0.0, bX = 0.0, bY = 0.0;
+  for (int s = 0; s <= nstrips; ++s) {
+    const int Ws = s * Lys;
+    const int wend = min(64, T - Ws);
+    if (wend <= 0) break;
+    int w = 0;
+    for (; w + 1 < wend; w += 2) {
+      window(s, w, aM, aX, aY, bM, bX, bY);
+      window(s, w + 1, bM, bX, bY, aM, aX, aY);
+    }
+    if (w < wend) {
+      window(s, w, aM, aX, aY, bM, bX, bY);
+      aM = bM;
+      aX = bX;
+      aY = bY;
+    }
+    if (s + 1 < nstrips) {
+      map_row(64 * (s + 1) + lane + 1, pn, okn, fbn, xi);
+      xn = P.xtab[xi];
+    }
+    const int tend = s < nstrips ? min(Ws + Lys, T) : 0;
+    int t = Ws + 64;
+    for (; t + 1 < tend; t += 2) {
+      interior(t - Ws + 1, aM, aX, aY, bM, bX, bY);
+      interior(t - Ws + 2, bM, bX, bY, aM, aX, aY);
+    }
+    if (t < tend) {
+      interior(t - Ws + 1, aM, aX, aY, bM, bX, bY);
+      aM = bM;
+      aX = bX;
+      aY = bY;
+    }
   }
-  if (t < T) step(aM, aX, aY, bM_, bX_, bY_);
-  double r;
-  if (SW) {
+  // the rows still held
+  if (SW) {  // (acc >= 0: it starts at 0)
     for (int off = 32; off > 0; off >>= 1) acc = fmax(acc, __shfl_xor(acc, off, 64));
-    r = acc;
-  } else {
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    r = 1.0 + acc;
+    if (lane == 0) ksum[0] = fmax(ksum[0], acc);
+  } else if (row_ok) {
+    __hip_atomic_fetch_add(&ksum[p], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return r;
 }
 
 // Pairs dealt one per wave: each wave stages its own y columns.
@@ -420,6 +519,8 @@ __global__ void __launch_bounds__(256) sk_bpla_fast_kernel(BplaLaunch P) {
   unsigned char* wbase = smem + kBplaExpLds + (size_t)wave * bpla_fast_wave_lds_bytes(maxlen);
   BplaPos* ycol = reinterpret_cast<BplaPos*>(wbase);
   double* bnd = reinterpret_cast<double*>(ycol + maxlen);
+  int4* ci = reinterpret_cast<int4*>(bnd + 3 * (maxlen + 2));
+  double* ksum = reinterpret_cast<double*>(ci + kBplaChunkMax);
   fill_exp_table(etab);
   // the wave's next pair: lane 0 draws, the value goes through SGPRs
   auto next_pair = [&]() {
@@ -431,28 +532,38 @@ __global__ void __launch_bounds__(256) sk_bpla_fast_kernel(BplaLaunch P) {
   for (int64_t pr = next_pair(); pr < P.n_pairs; pr = next_pair()) {
     const int x = __builtin_amdgcn_readfirstlane(P.xs[pr]);
     const int y = __builtin_amdgcn_readfirstlane(P.ys[pr]);
-    const int Ly = P.yset.ex_len[y], ypb = P.yset.ex_pos_base[y];
+    const int Ly = __builtin_amdgcn_readfirstlane(P.yset.ex_len[y]);
+    const int ypb = P.yset.ex_pos_base[y];
     for (int j = lane; j < Ly; j += 64) ycol[j] = P.ytab[ypb + j];
-    const double r = bpla_fast_pair<SW, BP>(P, x, y, ycol, bnd, etab, lane);
-    if (lane == 0) P.out[P.oidx ? P.oidx[pr] : (int64_t)pr] = r;
+    if (lane == 0) ci[0] = make_int4(P.xset.ex_pos_base[x], P.xset.ex_len[x], 0, 0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bpla_fast_chunk<SW, BP>(P, 1, ci, ksum, Ly, ycol, bnd, etab, lane);
+    if (lane == 0) P.out[P.oidx ? P.oidx[pr] : (int64_t)pr] = SW ? ksum[0] : 1.0 + ksum[0];
   }
 }
 
 // Pairs grouped by y into items {first, count} of one y: a workgroup stages
-// the y columns once in LDS for all its waves, and its waves take the item's
-// pairs from an LDS counter.  Per wave only the boundary row (24 B per
-// column), so 16 waves fit a CU.
+// the y columns once in LDS for all its waves, and its waves take chunks of
+// the item's pairs (P.chunk at a time) from an LDS counter.  Per wave only
+// the boundary row (24 B per column) and the chunk table, so 16 waves fit a
+// CU.
 template <bool SW, bool BP>
 __global__ void __launch_bounds__(512) sk_bpla_fast_items_kernel(BplaLaunch P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwaves = blockDim.x >> 6;
   const int maxlen = P.lds_max_len;
   double* etab = reinterpret_cast<double*>(smem);
   int* sh = reinterpret_cast<int*>(smem + kBplaExpLds);  // [0] item, [1] in-item counter
   BplaPos* ycol = reinterpret_cast<BplaPos*>(smem + kBplaExpLds + 16);
-  double* bnd = reinterpret_cast<double*>(ycol + maxlen) + (size_t)wave * 3 * (maxlen + 2);
+  unsigned char* wb = reinterpret_cast<unsigned char*>(ycol + maxlen) +
+                      (size_t)wave * (3 * (maxlen + 2) * 8 + kBplaChunkLds);
+  double* bnd = reinterpret_cast<double*>(wb);
+  int4* ci = reinterpret_cast<int4*>(bnd + 3 * (maxlen + 2));
+  double* ksum = reinterpret_cast<double*>(ci + kBplaChunkMax);
+  const int chunk = SW ? 1 : __builtin_amdgcn_readfirstlane(min(max(P.chunk, 1), kBplaChunkMax));
   fill_exp_table(etab);
   for (;;) {
     if (threadIdx.x == 0) {
@@ -466,22 +577,40 @@ __global__ void __launch_bounds__(512) sk_bpla_fast_items_kernel(BplaLaunch P) {
     const int2 item = make_int2(__builtin_amdgcn_readfirstlane(item0.x),
                                 __builtin_amdgcn_readfirstlane(item0.y));
     const int y = __builtin_amdgcn_readfirstlane(P.ys[item.x]);
-    const int Ly = P.yset.ex_len[y], ypb = P.yset.ex_pos_base[y];
+    const int Ly = __builtin_amdgcn_readfirstlane(P.yset.ex_len[y]);
+    const int ypb = P.yset.ex_pos_base[y];
     for (int j = threadIdx.x; j < Ly; j += blockDim.x) ycol[j] = P.ytab[ypb + j];
     __syncthreads();
-    // the wave's next pair of the item: lane 0 draws, through an SGPR
+    // the wave's next chunk of the item: lane 0 draws, through an SGPR
     auto next_k = [&]() {
       int v = 0;
-      if (lane == 0) v = atomicAdd(&sh[1], 1);
+      if (lane == 0) v = atomicAdd(&sh[1], chunk);
       return __builtin_amdgcn_readfirstlane(v);
     };
     for (int k = next_k(); k < item.y; k = next_k()) {
-      const int64_t pr = (int64_t)item.x + k;
-      const int x = __builtin_amdgcn_readfirstlane(P.xs[pr]);
-      const double r = bpla_fast_pair<SW, BP>(P, x, y, ycol, bnd, etab, lane);
-      if (lane == 0) P.out[P.oidx ? P.oidx[pr] : pr] = r;
+      const int np = min(chunk, item.y - k);
+      // chunk table: first rows by an exclusive prefix sum over the pairs
+      int len = 0, pb = 0;
+      if (lane < np) {
+        const int x = P.xs[item.x + k + lane];
+        len = P.xset.ex_len[x];
+        pb = P.xset.ex_pos_base[x];
+      }
+      int start = 0;
+      for (int q = 0; q < np - 1; ++q) {
+        const int lq = __shfl(len, q, 64);
+        start += lane > q ? lq : 0;
+      }
+      if (lane < np) ci[lane] = make_int4(pb, len, start, 0);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      bpla_fast_chunk<SW, BP>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
+      if (lane < np) {
+        const int64_t pr = (int64_t)item.x + k + lane;
+        P.out[P.oidx ? P.oidx[pr] : pr] = SW ? ksum[lane] : 1.0 + ksum[lane];
+      }
     }
-    (void)nwaves;
     __syncthreads();
   }
 }

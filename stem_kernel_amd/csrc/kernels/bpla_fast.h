@@ -26,6 +26,18 @@ __device__ __forceinline__ double wave_shl1_to(double v, double high) {
   return __hiloint2double(rhi, rlo);
 }
 
+// The reference's float expressions a*b + c*d and n + a*b, every operation
+// rounded on its own: no fused multiply-add (a contracted one differs by an
+// ulp of float, ~1e-8 relative in K after the exponentials).
+__device__ __forceinline__ float f32_dot2(float a, float b, float c, float d) {
+#pragma clang fp contract(off)
+  return a * b + c * d;
+}
+__device__ __forceinline__ float f32_madd(float n, float a, float b) {
+#pragma clang fp contract(off)
+  return n + a * b;
+}
+
 // exp(x), |x| << 700: x = (64m + j) ln2/64 + r, |r| <= ln2/128, e^r by its
 // Taylor series to degree 5 (truncation < 4e-17 relative), times 2^(j/64)
 // from an LDS table, times 2^m.

@@ -306,8 +306,8 @@ __device__ void bpla_grad_wave_pair(const BplaGradLaunch& P, int x, int y, const
     la = __builtin_fma(xr.v[1], yc.v[1], la);
     la = __builtin_fma(xr.v[2], yc.v[2], la);
     la = __builtin_fma(xr.v[3], yc.v[3], la);
-    const float pp = __fadd_rn(__fmul_rn(xr.pr, yc.pr), __fmul_rn(xr.pl, yc.pl));
-    const float uu = __fmul_rn(xr.pu, yc.pu);
+    const float pp = f32_dot2(xr.pr, yc.pr, xr.pl, yc.pl);
+    const float uu = xr.pu * yc.pu;
     wp = (double)pp;
     return alpha * (double)pp + (double)uu * la;
   };

@@ -108,6 +108,7 @@ struct BplaLaunch {
   double* out = nullptr;
   unsigned long long* pair_counter = nullptr;
   int32_t lds_max_len = 0;  // even, >= 64 (streamed strips)
+  int32_t chunk = 1;        // grouped fast kernel: pairs a wave streams back to back (<= kBplaChunkMax)
 };
 
 // BPLA gradients (bpla_kernel.cpp:178-401): one thread per pair, forward and
@@ -246,9 +247,15 @@ hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st);
 
 // fast kernels: a workgroup's LDS starts with the exp table 2^(j/64), j < 64
 constexpr size_t kBplaExpLds = 64 * 8;
+// a wave's chunk of pairs streamed back to back: per pair {xtab base,
+// length, first row, -} and its K sum
+constexpr int kBplaChunkMax = 8;
+constexpr size_t kBplaChunkLds = kBplaChunkMax * (16 + 8);
 // grouped fast kernel: exp table | shared y columns | per wave boundary row
+// and chunk
 __host__ __device__ inline size_t bpla_items_lds_bytes(int maxlen, int nwaves) {
-  return kBplaExpLds + 16 + (size_t)maxlen * sizeof(BplaPos) + (size_t)nwaves * 3 * (maxlen + 2) * 8;
+  return kBplaExpLds + 16 + (size_t)maxlen * sizeof(BplaPos) +
+         (size_t)nwaves * (3 * (maxlen + 2) * 8 + kBplaChunkLds);
 }
 size_t bpla_lds_bytes(const BplaLaunch& P, int nwaves);
 hipError_t launch_bpla(const BplaLaunch& P, int grid, int nwaves, hipStream_t st);
@@ -256,9 +263,9 @@ hipError_t launch_bpla(const BplaLaunch& P, int grid, int nwaves, hipStream_t st
 hipError_t launch_bpla_tab(const float4* prof, const float4* lru, int64_t n, const double* table,
                            BplaPos* xrole, BplaPos* yrole, hipStream_t st);
 // per-wave LDS of the fast kernel: y columns (BplaPos, maxlen) | boundary
-// row {M, X, Y} [maxlen + 2]
+// row {M, X, Y} [maxlen + 2] | chunk
 __host__ __device__ inline size_t bpla_fast_wave_lds_bytes(int maxlen) {
-  const size_t b = (size_t)maxlen * sizeof(BplaPos) + (size_t)3 * (maxlen + 2) * 8;
+  const size_t b = (size_t)maxlen * sizeof(BplaPos) + (size_t)3 * (maxlen + 2) * 8 + kBplaChunkLds;
   return (b + 15) & ~(size_t)15;
 }
 hipError_t launch_bpla_fast(const BplaLaunch& P, int grid, int nwaves, hipStream_t st);

@@ -923,6 +923,10 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
     if (d_items) {  // y-grouped: 8-wave workgroups sharing the y columns
       F.items = d_items;
       F.n_items = (int32_t)items.size();
+      // pairs a wave streams back to back (SK_BPLA_CHUNK: 1..kBplaChunkMax)
+      F.chunk = 4;
+      if (const char* e = std::getenv("SK_BPLA_CHUNK")) F.chunk = std::atoi(e);
+      F.chunk = std::min(std::max(F.chunk, 1), sk::kBplaChunkMax);
       w = kItemWaves;
       const size_t l = sk::bpla_items_lds_bytes(F.lds_max_len, w);
       if (l > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");

@@ -113,9 +113,11 @@ def test_bpla_normalized_and_predict(gpu_ctx, bpla_set):
 @pytest.mark.parametrize("noBP,SW", MODES)
 def test_bpla_y_grouped_items(gpu_ctx, bpla_set, noBP, SW, monkeypatch):
     """Many pairs per y: the fast pairs go to the y-grouped kernel (a
-    workgroup stages one y for its waves); the non-dyadic ones (the 3-row
-    alignment) stay on the general kernel.  Same values as one pair per wave,
-    bit for bit, and as the oracle."""
+    workgroup stages one y for its waves, each wave streams a chunk of
+    pairs back to back); the non-dyadic ones (the 3-row alignment) stay on
+    the general kernel.  The oracle's values for every chunk size, and the
+    same as one pair per wave (bit for bit for the max-plus SW modes; the
+    exp sums only change order)."""
     ds, om = bpla_set
     n = len(om)
     kern = ska.BPLAKernel(noBP=noBP, SW=SW)
@@ -124,6 +126,32 @@ def test_bpla_y_grouped_items(gpu_ctx, bpla_set, noBP, SW, monkeypatch):
     got = gpu_ctx.pairs(ds, kern, x, y)
     uniq = sorted(set(zip(x.tolist(), y.tolist())))
     ref = {p: po.kernel_value(kern.params.kind, om[p[0]], om[p[1]], kern.params) for p in uniq}
-    assert rel_err(got, [ref[p] for p in zip(x.tolist(), y.tolist())]) < TOL
+    want = [ref[p] for p in zip(x.tolist(), y.tolist())]
+    assert rel_err(got, want) < TOL
+    for chunk in ("1", "3", "8"):
+        monkeypatch.setenv("SK_BPLA_CHUNK", chunk)
+        assert rel_err(gpu_ctx.pairs(ds, kern, x, y), want) < TOL
+    monkeypatch.delenv("SK_BPLA_CHUNK")
     monkeypatch.setenv("SK_BPLA_NO_ITEMS", "1")
-    assert np.array_equal(gpu_ctx.pairs(ds, kern, x, y), got)
+    single = gpu_ctx.pairs(ds, kern, x, y)
+    if SW:
+        assert np.array_equal(single, got)
+    else:
+        assert rel_err(single, got) < 1e-13
+
+
+@pytest.mark.gpu
+def test_bpla_chunks_of_long_rows(gpu_ctx):
+    """Chunks whose pairs end and start inside a strip, rows of 1 to 3
+    strips, a pair of one row after a long one."""
+    seqs = ska.random_sequences(2, 150, 0x5EED0033) + ska.random_sequences(2, 64, 9) + \
+        ska.random_sequences(2, 100, 11) + ["G", "ACGUACGUAC"]
+    ds, om = make_examples(seqs)
+    n = len(seqs)
+    kern = ska.BPLAKernel()
+    x = np.tile(np.array([0, 7, 2, 1, 6, 3, 4, 5], np.int32), 40)
+    y = np.repeat(np.array([0, 4], np.int32), x.size // 2)
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    ref = {(a, b): po.kernel_value(kern.params.kind, om[a], om[b], kern.params)
+           for a in range(n) for b in (0, 4)}
+    assert rel_err(got, [ref[p] for p in zip(x.tolist(), y.tolist())]) < TOL
