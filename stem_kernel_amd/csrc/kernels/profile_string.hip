@@ -25,8 +25,11 @@ __device__ __forceinline__ int onehot_code(float4 c) {
   return -1;
 }
 
-// subst_score(st, Column x, Column y): string_kernel.cpp:81-100
+// subst_score(st, Column x, Column y): string_kernel.cpp:81-100.  Every
+// operation rounded as the reference's (no fused multiply-add: a contracted
+// float weight n is off by an ulp of float)
 __device__ __forceinline__ double prof_subst(const double* __restrict__ st, float4 xc, float4 yc) {
+#pragma clang fp contract(off)
   const float xa[4] = {xc.x, xc.y, xc.z, xc.w};
   const float yb[4] = {yc.x, yc.y, yc.z, yc.w};
   double v_c = 0.0;
