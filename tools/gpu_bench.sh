@@ -11,7 +11,7 @@ case $CFG in
   c2) KIND=ss; LEN=150; KSUB=sk_dag_stem_kernel;;
   c5) KIND=stem; LEN=300; KSUB=sk_dag_stem_kernel;;
   c3) KIND=stem4d; LEN=200; KSUB=sk_stem4d_kernel;;
-  c4) KIND=bpla; LEN=210; KSUB=sk_bpla_kernel;;
+  c4) KIND=bpla; LEN=210; KSUB=sk_bpla;;
 esac
 mkdir -p $OUT; export TMPDIR=/tmp
 if [ "$NOTESTS" != "--no-tests" ]; then
