@@ -151,7 +151,7 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_SEGSUM  // MATCH: same-parent runs summed per quad before the atomic (0 = off)
 #define SK_SEGSUM 1
 #endif
-#ifndef SK_SKIP_LOOPS  // cost experiment only (wrong results): loop rows skip MATCH and the sweep
+#ifndef SK_SKIP_LOOPS  // cost experiment only (wrong results): loop rows (1) / rows with only gamma children (2) skip MATCH and the sweep
 #define SK_SKIP_LOOPS 0
 #endif
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
@@ -389,6 +389,13 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // single bp-frequency entry of x (the common single-sequence case)
     const bool x_one = xnbf == 1 && x_nbp == 0.0;
     const uint32_t xcode = (xc >> 16) * 16u;
+#if SK_SKIP_LOOPS == 2  // cost experiment: rows whose children are all gamma rows
+    bool skipr = gam && xne > 0 && xne <= 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) skipr = skipr && (j >= xne || (ch[j] & 0x8000u));
+#else
+    const bool skipr = xloop;
+#endif
     // MATCH node range [qa, qb): y nodes are numbered by length, so the
     // length band [xlen-band, xlen+band] is one index range; its first
     // pass's node records are requested now, ahead of the child rows
@@ -499,7 +506,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #ifdef SK_STAMPS
     cnt[3] += qb > qa ? qb - qa : 0;
 #endif
-    if (qa < qb && !(SK_SKIP_LOOPS && xloop)) {
+    if (qa < qb && !(SK_SKIP_LOOPS && skipr)) {
       // node records and path counts come from HBM (L2-resident per y),
       // the first pass's issued before A, each later pass's during the
       // pass before.  A pass covers NW = 64*SK_PW nodes [q0, top], lane l
@@ -722,7 +729,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #endif
     // a row nobody reads (a root: pslot 0xffff) needs only its MATCH terms
     // (K is the path sum of M), so it skips the sweep and the store
-    if (c0 < Y.nch && pslot != 0xffffu && !(SK_SKIP_LOOPS && xloop)) {
+    if (c0 < Y.nch && pslot != 0xffffu && !(SK_SKIP_LOOPS && skipr)) {
       iy_sweep(Y, R, c0, lane);
       wave_sync();
     }
