@@ -12,7 +12,8 @@ BUILD := $(ROOT)build
 LIB := $(ROOT)stem_kernel_amd/libstem_kernel_amd.so
 
 HOST_SRC := $(ROOT)stem_kernel_amd/csrc/host/synth.cpp $(ROOT)stem_kernel_amd/csrc/host/example_build.cpp \
-            $(ROOT)stem_kernel_amd/csrc/host/readers.cpp $(ROOT)stem_kernel_amd/csrc/host/shard.cpp
+            $(ROOT)stem_kernel_amd/csrc/host/readers.cpp $(ROOT)stem_kernel_amd/csrc/host/shard.cpp \
+            $(ROOT)stem_kernel_amd/csrc/host/svm_predict.cpp
 API_SRC := $(ROOT)stem_kernel_amd/csrc/sk_api.cpp
 HIP_SRC := $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip $(ROOT)stem_kernel_amd/csrc/kernels/profile_string.hip \
            $(ROOT)stem_kernel_amd/csrc/kernels/bpla.hip $(ROOT)stem_kernel_amd/csrc/kernels/stem4d.hip \
@@ -65,7 +66,7 @@ stamps:
 	@mkdir -p $(BUILD)/stamps
 	$(HIPCC) $(HIPFLAGS) -DSK_STAMPS -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip -o $(BUILD)/stamps/dag_stem.o
 	$(HIPCC) $(CXXFLAGS) -DSK_STAMPS -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/stamps/sk_api.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/kernels/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(STAMPS_LIB) $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/host/svm_predict.o $(BUILD)/stamps/sk_api.o $(BUILD)/stamps/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/kernels/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 .PHONY: stamps
 
 # experiment build: make variant NAME=x DEFS="-DSK_PW=3 [-DSK_STAMPS]" -> build/libsk_x.so
@@ -73,12 +74,12 @@ variant:
 	@mkdir -p $(BUILD)/var/$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/dag_stem.hip -o $(BUILD)/var/$(NAME)/dag_stem.o
 	$(HIPCC) $(CXXFLAGS) $(DEFS) -D__HIP_PLATFORM_AMD__ -c $(API_SRC) -o $(BUILD)/var/$(NAME)/sk_api.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/var/$(NAME)/sk_api.o $(BUILD)/var/$(NAME)/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/kernels/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/host/svm_predict.o $(BUILD)/var/$(NAME)/sk_api.o $(BUILD)/var/$(NAME)/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/kernels/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 .PHONY: variant
 
 # 4-D kernel experiment build: make variant4 NAME=x DEFS="-DSK4_MINB=4" -> build/libsk_x.so
 variant4:
 	@mkdir -p $(BUILD)/var/$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/stem4d.hip -o $(BUILD)/var/$(NAME)/stem4d.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/sk_api.o $(BUILD)/kernels/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/var/$(NAME)/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/kernels/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/host/svm_predict.o $(BUILD)/sk_api.o $(BUILD)/kernels/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/var/$(NAME)/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/kernels/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 .PHONY: variant4

@@ -339,6 +339,38 @@ const char *sk_seqfile_last_error(void);
  * out (n_seqs*(len+1) bytes, NUL separated); *state advances. */
 int sk_random_sequences(uint64_t *state, int32_t n_seqs, int32_t len, char *out);
 
+/* ---------------------------------------------------------------- SVM prediction
+ * Predict mode's Output (f3) feeds every test row through the libsvm models
+ * of --model / --predict: SVMPredict (libsvm/svm_util.cpp:11-95) over the
+ * reference's vendored libsvm 2.8x, restated in csrc/host/svm_predict.cpp.
+ *   sk_svm_model_load   svm_load_model (libsvm/svm.cpp:1288-1475): text
+ *                       model, any svm_type / kernel_type (precomputed:
+ *                       an SV's value is its 1-based training index);
+ *                       SK_ERR_INVALID with sk_svm_last_error() on failure.
+ *   sk_svm_model_info   svm_get_svm_type / svm_get_nr_class / svm_get_labels
+ *                       (svm.cpp:1024-1039; labels untouched when the model
+ *                       has none), and whether probA/probB are present.
+ *   sk_svm_predict      SVMPredict::do_svm_predict's arithmetic
+ *                       (svm_util.cpp:41-80) on the test vector
+ *                       make_svm_node(cnt, row) builds (x[0] = cnt,
+ *                       x[i+1] = row[i], row = the test row over the training
+ *                       examples): with probability != 0 and a C-SVC / nu-SVC
+ *                       model, *label = svm_predict_probability
+ *                       (svm.cpp:1152-1189) and values[0..nr_class) = the
+ *                       class probabilities (zeros if the model has no
+ *                       probA/probB: svm_predict's label); otherwise *label =
+ *                       svm_predict (svm.cpp:1108-1150) and
+ *                       values[0..max(nr_class(nr_class-1)/2, 1)) = the
+ *                       decision values (svm_predict_values, svm.cpp:1053-1106). */
+typedef struct sk_svm_model sk_svm_model;
+int sk_svm_model_load(const char *path, sk_svm_model **out);
+void sk_svm_model_free(sk_svm_model *m);
+int sk_svm_model_info(const sk_svm_model *m, int32_t *svm_type, int32_t *nr_class, int32_t *labels,
+                      int32_t *has_probability);
+int sk_svm_predict(const sk_svm_model *m, int32_t cnt, const double *row, int32_t n, int32_t probability,
+                   double *label, double *values);
+const char *sk_svm_last_error(void);
+
 /* ---------------------------------------------------------------- diagnostics */
 /* Milliseconds spent in the last compute call's dominant kernel (DAG stem
  * DP), measured with HIP events on the context's stream, and its launch

@@ -4,7 +4,7 @@ See include/stem_kernel.h for the ABI and DESIGN.md for the design.
 """
 from ._lib import StemKernelError, lib, default_params  # noqa: F401
 from .kernel_matrix import (  # noqa: F401
-    BPLAKernel, Context, Dataset, KernelMatrix, LSuStemKernel, LSuStemStrKernel, NaiveStringKernel, SiStemKernel,
+    BPLAKernel, Context, Dataset, KernelMatrix, SVMModel, LSuStemKernel, LSuStemStrKernel, NaiveStringKernel, SiStemKernel,
     SiStemStrKernel, StemKernel4D, StemStrKernel, StringKernel, SuStemKernel, SuStemStrKernel, fold,
     format_libsvm, parse_examples, random_sequences, read_examples,
 )

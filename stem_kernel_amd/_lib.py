@@ -107,6 +107,13 @@ SIGNATURES = {
     "sk_seqfile_rows": (C.c_int32, [_P, C.c_int64]),
     "sk_seqfile_row": (C.c_char_p, [_P, C.c_int64, C.c_int32]),
     "sk_seqfile_last_error": (C.c_char_p, []),
+    "sk_svm_model_load": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
+    "sk_svm_model_free": (None, [_P]),
+    "sk_svm_model_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_int32)]),
+    "sk_svm_predict": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_double), C.c_int32, C.c_int32,
+                                 C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "sk_svm_last_error": (C.c_char_p, []),
 }
 
 _lock = threading.Lock()

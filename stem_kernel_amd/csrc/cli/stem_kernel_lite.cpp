@@ -11,12 +11,14 @@
 // zlib); predict mode (--test) writes one kernel row per test example
 // (Output::kernel_output, common/framework.cpp:193-209), optionally only the
 // support vectors of --model files (load_sv_index, libsvm/model.cpp:56-99),
-// and their self values to --norm (Output::norm_output).
+// their self values to --norm (Output::norm_output), and each --model's
+// predictions to the matching --predict file (Output::prob_output through
+// SVMPredict, libsvm/svm_util.cpp:11-95: sk_svm_model_load / sk_svm_predict).
 //
 // Differences, by necessity: base-pairing probabilities come from the
 // engine's GPU McCaskill (sk_fold_mccaskill) instead of ViennaRNA;
-// --noLonelyPairs, --use-alifold and --predict (libsvm's SVM, outside the
-// engine) are refused; .bz2 output is refused (no libbz2 headers here).  The
+// --noLonelyPairs and --use-alifold are refused; .bz2 output is refused (no
+// libbz2 headers here).  The
 // reference's default kernel (SuStemStr without --log) only estimates memory
 // and never runs App::execute (main.cpp:176-183, `//res = app.execute();`);
 // here every kernel choice computes its matrix.
@@ -305,6 +307,62 @@ void flush_if_large(std::ostringstream& buf, std::unique_ptr<TextSink>& sink, co
   }
 }
 
+// SVMPredict (libsvm/svm_util.cpp:11-80): one model, one prediction file;
+// probability estimates requested (Output constructs it with true), so the
+// file starts with the model's labels and each row is "label p1 p2 ..." for
+// C-SVC / nu-SVC, else "target dec1 dec2 ..."; buffered like Output (10 MB).
+class SvmPredictOut {
+ public:
+  SvmPredictOut(const std::string& out_file, const std::string& model_file) : out_(out_file) {
+    static std::string err;
+    if (!out_.is_open()) {
+      err = out_file + ": cannot open for writing";
+      throw err.c_str();
+    }
+    if (sk_svm_model_load(model_file.c_str(), &model_) != SK_OK) {
+      err = model_file + ": " + sk_svm_last_error();
+      throw err.c_str();
+    }
+    sk_svm_model_info(model_, &svm_type_, &nr_class_, nullptr, nullptr);
+    std::vector<int32_t> labels(std::max(nr_class_, 1), 0);  // zeros when the model has none
+    sk_svm_model_info(model_, nullptr, nullptr, labels.data(), nullptr);
+    out_ << "labels ";
+    for (int k = 0; k < nr_class_; ++k) out_ << labels[k] << " ";
+    out_ << std::endl;
+  }
+  ~SvmPredictOut() {
+    out_ << buf_.str();
+    sk_svm_model_free(model_);
+  }
+  void predict(double target, unsigned cnt, const std::vector<double>& row) {
+    static std::string err;
+    std::vector<double> vals(std::max(nr_class_ * (nr_class_ - 1) / 2, std::max(nr_class_, 1)));
+    double v = 0.0;
+    if (sk_svm_predict(model_, (int32_t)cnt, row.data(), (int32_t)row.size(), 1, &v, vals.data()) != SK_OK) {
+      err = sk_svm_last_error();
+      throw err.c_str();
+    }
+    if (svm_type_ == 0 || svm_type_ == 1) {
+      buf_ << v << " ";
+      for (int k = 0; k < nr_class_; ++k) buf_ << vals[k] << " ";
+    } else {
+      buf_ << target << " ";
+      for (int k = 0; k < nr_class_ * (nr_class_ - 1) / 2; ++k) buf_ << vals[k] << " ";
+    }
+    buf_ << std::endl;
+    if (buf_.str().size() > (size_t)10 * 1024 * 1024) {
+      out_ << buf_.str();
+      buf_.str("");
+    }
+  }
+
+ private:
+  std::ofstream out_;
+  std::ostringstream buf_;
+  sk_svm_model* model_ = nullptr;
+  int32_t svm_type_ = 0, nr_class_ = 0;
+};
+
 // App<K,LDF> (common/framework.h:100-353) over the compat types
 template <class K>
 class App {
@@ -341,6 +399,12 @@ class App {
     const bool norm = opts_.normalize || !opts_.norm_output.empty();
     std::ostringstream kout, tout;
     std::unique_ptr<TextSink> kfile, tfile;
+    // Output's SVMPredict per --predict file with the --model of the same
+    // position (framework.cpp:142-154)
+    std::vector<std::unique_ptr<SvmPredictOut>> pout;
+    for (size_t k = 0; k != opts_.predict_output.size(); ++k) {
+      pout.emplace_back(new SvmPredictOut(opts_.predict_output[k], opts_.trained_model_file[k]));
+    }
     unsigned cnt = 0;
     for (size_t i = 0; i != opts_.ts_files.size(); ++i) {
       double elapsed = 0.0;
@@ -365,6 +429,8 @@ class App {
           kout << std::endl;
         }
         if (!opts_.norm_output.empty()) tout << self << std::endl;
+        // Output::prob_output (framework.cpp:211-221)
+        for (auto& p : pout) p->predict(std::atof(opts_.ts_labels[i].c_str()), cnt, vec);
         // Output flushes its buffers past MAX = 10 MB (framework.cpp:193-234)
         flush_if_large(kout, kfile, opts_.predict_only ? std::string() : opts_.output);
         flush_if_large(tout, tfile, opts_.norm_output);
@@ -425,8 +491,8 @@ int main(int argc, char** argv) {
   parse_extra_args(o, extra);
   bool res = false;
   try {
-    if (!o.predict_output.empty())
-      throw "--predict: SVM prediction (libsvm) is outside the engine; run svm-predict on the kernel rows";
+    if (o.predict_output.size() > o.trained_model_file.size())
+      throw "--predict: every prediction file needs the --model of the same position";
     if (o.bp.no_LonelyPairs) throw "--noLonelyPairs is not supported by the engine's fold";
     if (o.bp.alifold) throw "--use-alifold is not supported by the engine's fold";
     if (o.predict_mode && !o.trained_model_file.empty()) load_sv_index(o.sv_index, o.trained_model_file);

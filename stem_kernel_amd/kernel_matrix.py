@@ -31,7 +31,7 @@ __all__ = [
     "fold", "random_sequences", "Dataset", "Context", "KernelMatrix",
     "SuStemKernel", "SiStemKernel", "StringKernel", "SuStemStrKernel", "StemStrKernel",
     "SiStemStrKernel", "LSuStemKernel", "LSuStemStrKernel", "NaiveStringKernel",
-    "StemKernelError",
+    "StemKernelError", "SVMModel",
 ]
 
 
@@ -606,6 +606,48 @@ def format_libsvm(matrix: np.ndarray, labels: Sequence[str]) -> str:
     check(lib().sk_format_libsvm(m.ctypes.data_as(C.POINTER(C.c_double)), rows, cols, larr, buf,
                                  need.value, C.byref(need)))
     return buf.value.decode()
+
+
+class SVMModel:
+    """A libsvm model for predict mode's Output (f3): SVMPredict
+    (libsvm/svm_util.cpp:11-95) over the reference's libsvm 2.8x
+    (sk_svm_model_load / sk_svm_predict, csrc/host/svm_predict.cpp)."""
+
+    def __init__(self, path: str):
+        h = C.c_void_p()
+        rc = lib().sk_svm_model_load(str(path).encode(), C.byref(h))
+        if rc != SK_OK:
+            raise StemKernelError(rc, lib().sk_svm_last_error().decode())
+        self._h = h
+        t, k, p = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib().sk_svm_model_info(self._h, C.byref(t), C.byref(k), None, C.byref(p)))
+        self.svm_type, self.nr_class, self.has_probability = t.value, k.value, bool(p.value)
+        labels = (C.c_int32 * max(k.value, 1))()
+        check(lib().sk_svm_model_info(self._h, None, None, labels, None))
+        self.labels = [labels[i] for i in range(k.value)]
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().sk_svm_model_free(h)
+            self._h = None
+
+    def predict(self, row, cnt: int = 1, probability: bool = True):
+        """(label, values) of SVMPredict::do_svm_predict for the test row
+        (kernel values against the training examples, in training order):
+        class probabilities for C-SVC / nu-SVC with probability, else the
+        one-vs-one decision values."""
+        r = np.ascontiguousarray(row, dtype=np.float64)
+        nv = max(self.nr_class * (self.nr_class - 1) // 2, self.nr_class, 1)
+        vals = np.zeros(nv, dtype=np.float64)
+        label = C.c_double()
+        rc = lib().sk_svm_predict(self._h, int(cnt), r.ctypes.data_as(C.POINTER(C.c_double)), r.size,
+                                  int(probability), C.byref(label), vals.ctypes.data_as(C.POINTER(C.c_double)))
+        if rc != SK_OK:
+            raise StemKernelError(rc, lib().sk_svm_last_error().decode())
+        if probability and self.svm_type in (0, 1):
+            return label.value, vals[: self.nr_class]
+        return label.value, vals[: max(self.nr_class * (self.nr_class - 1) // 2, 1)]
 
 
 class KernelMatrix:

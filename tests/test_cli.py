@@ -61,11 +61,11 @@ def test_refused_folding_options(tmp_path, flag, msg):
     assert r.returncode == 1 and msg in r.stdout
 
 
-def test_predict_output_refused(tmp_path):
+def test_predict_needs_model(tmp_path):
     _write_fa(tmp_path / "a.fa", ["GGGGAAACCCC"])
     r = _run([tmp_path / "o.txt", "+1", tmp_path / "a.fa", "--test", "+1", tmp_path / "a.fa",
-              "--model", tmp_path / "m", "--predict", tmp_path / "p"])
-    assert r.returncode == 1 and "libsvm" in r.stdout
+              "--predict", tmp_path / "p"])
+    assert r.returncode == 1 and "--model" in r.stdout
 
 
 def test_missing_file_message(tmp_path):
@@ -159,3 +159,50 @@ def test_cli_predict_rows_and_norms(gpu_ctx, fa_files, tmp_path):
         assert np.max(np.abs(got[t][nz] - ref[nz]) / np.abs(ref[nz])) < 1e-5
     nrm = np.array([float(v) for v in norms.read_text().split()])
     assert np.max(np.abs(nrm - np.array(self_vals)) / np.array(self_vals)) < 1e-5
+
+
+@pytest.mark.gpu
+def test_cli_predict_with_svm_models(gpu_ctx, fa_files, tmp_path):
+    """--model/--predict pairs: Output::prob_output through SVMPredict
+    (framework.cpp:211-221, libsvm/svm_util.cpp:11-80) on the normalised
+    test rows; a C-SVC model with probabilities and an epsilon-SVR model,
+    both trained by scikit-learn's libsvm on the engine's Gram."""
+    svm = pytest.importorskip("sklearn.svm")
+    from oracle import svm_oracle as so
+    d, pos, neg, test = fa_files
+    train = ska.Dataset.folded(gpu_ctx, pos + neg)
+    tst = ska.Dataset.folded(gpu_ctx, test)
+    kern = ska.SuStemStrKernel()
+    K = gpu_ctx.gram(train, kern, normalize=True)
+    y = np.array([1] * len(pos) + [-1] * len(neg))
+    clf = svm.SVC(kernel="precomputed", C=4.0, probability=True, random_state=0).fit(K, y)
+    reg = svm.SVR(kernel="precomputed", C=2.0, epsilon=0.01).fit(K, np.linspace(0, 1, len(y)))
+    mc = dict(svm_type="c_svc", nr_class=2, label=[int(c) for c in clf.classes_],
+              nSV=clf.n_support_.tolist(), sv_index=(clf.support_ + 1).tolist(),
+              sv_coef=np.atleast_2d(clf._dual_coef_).tolist(), rho=(-clf._intercept_).tolist(),
+              probA=clf.probA_.tolist(), probB=clf.probB_.tolist())
+    mr = dict(svm_type="epsilon_svr", nr_class=2, sv_index=(reg.support_ + 1).tolist(),
+              sv_coef=np.atleast_2d(reg._dual_coef_).tolist(), rho=(-reg._intercept_).tolist())
+    so.write_model(tmp_path / "mc", mc)
+    so.write_model(tmp_path / "mr", mr)
+    r = _run(["-n", "--no-matrix", "--model", tmp_path / "mc", "--predict", tmp_path / "pc",
+              "--model", tmp_path / "mr", "--predict", tmp_path / "pr", tmp_path / "rows.txt",
+              "+1", d / "pos.fa", "-1", d / "neg.fa", "--test", "-1", d / "test.fa"])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert not (tmp_path / "rows.txt").exists()  # --no-matrix
+    pc = (tmp_path / "pc").read_text().splitlines()
+    pr = (tmp_path / "pr").read_text().splitlines()
+    assert pc[0].split() == ["labels"] + [str(c) for c in clf.classes_]
+    assert pr[0].split() == ["labels", "0", "0"]  # an SVR model has no labels
+    sv = np.union1d(clf.support_, reg.support_).astype(np.int32)
+    diag = gpu_ctx.diagonal(train, kern, sv_index=sv)
+    for t in range(len(test)):
+        row, slf = gpu_ctx.test_row(tst, t, train, kern, sv_index=sv, self_value=True)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            row = row / np.sqrt(diag * slf)
+        lab, prob = so.predict_probability(mc, row)
+        got = [float(v) for v in pc[t + 1].split()]
+        assert got[0] == lab and np.allclose(got[1:], prob, rtol=1e-5, atol=1e-6)
+        dec = so.decision_values(mr, row)
+        got = [float(v) for v in pr[t + 1].split()]
+        assert got[0] == -1.0 and np.allclose(got[1:], dec, rtol=1e-5, atol=1e-6)
