@@ -70,14 +70,26 @@ __global__ void sk_prep_kernel(DevSet s, DevParamNodes pn, const double* __restr
   if (s.n_gam > 0) {
     const int gb = s.ex_xg_base[e], nlg = s.ex_nlxg[e];
     int k = s.ex_xgch_base[e];
+    int pk = s.n_phi > 0 ? s.ex_phk_base[e] : 0;
     for (int r = 0; r < nlg; ++r) {
-      pn.xg_SL[gb + r] = pn.nd_SL[nb + s.xg_node[gb + r]];
-      const int ne = s.xgrow[gb + r].a & 0xff;
+      const double SLr = pn.nd_SL[nb + s.xg_node[gb + r]];
+      pn.xg_SL[gb + r] = SLr;
+      const XRow xr = s.xgrow[gb + r];
+      const int ne = xr.a & 0xff;
       for (int t = 0; t < ne; ++t, ++k) {
+        // the record's weight recipe (device_set.h)
         const uint32_t c = s.xg_ch[k];
-        double w = gpow[c >> 16];
-        if (c & 0x8000u) w *= gpow[s.xg_clg[k]] * (double)s.xg_cpf[k];  // gamma child
+        const double wc = gpow[c >> 16] * gpow[s.xg_clg[k]] * (double)s.xg_cpf[k];
+        double w;
+        switch (s.xg_cty[k]) {
+          case 0: w = gpow[c >> 16]; break;
+          case 1: w = wc; break;
+          case 2: w = (double)xr.bp0 * wc; break;
+          case 3: w = (double)xr.bp0 * SLr; break;
+          default: w = gap2 * (double)xr.w * wc; break;
+        }
         pn.xg_chw[k] = w;
+        if (s.xg_cty[k] == 2) pn.phk_w[pk++] = xr.P * w;
       }
     }
     double* h = pn.gam_h + (int64_t)e * s.n_gam;
@@ -86,6 +98,11 @@ __global__ void sk_prep_kernel(DevSet s, DevParamNodes pn, const double* __restr
       const uint32_t inf = s.gr_info[i];
       h[inf & 0xffff] += s.gr_P[i] * (gpow[inf >> 16] * (double)s.gr_pf[i]);
     }
+    if (s.n_phi > 0)  // phi rows' Gamma_{code,len} terms: P pf xSL
+      for (int i = s.ex_gra_base[e]; i < s.ex_gra_base[e + 1]; ++i) {
+        const uint32_t r = s.gra_row[i];
+        h[s.gra_gidx[i]] += s.xgrow[r].P * ((double)s.xgrow[r].bp0 * pn.xg_SL[r]);
+      }
   }
 }
 
@@ -153,6 +170,9 @@ __device__ __forceinline__ void wave_sync() {
 #endif
 #ifndef SK_SKIP_LOOPS  // cost experiment only (wrong results): loop rows (1) / rows with only gamma children (2) skip MATCH and the sweep
 #define SK_SKIP_LOOPS 0
+#endif
+#ifndef SK_PHI_EXP  // cost experiments only (wrong values): 1 phi rows load nothing, 2 no Phi tables
+#define SK_PHI_EXP 0
 #endif
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
 #define SK_MU 3
@@ -295,18 +315,21 @@ __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int
   wave_sync();
 }
 
-// base of child row c of an x schedule: a slab slot, or (bit 15) the y's
-// Gamma row of a gamma child
-__device__ __forceinline__ const double* child_row(uint32_t c, const double* slab,
-                                                   const double* gamtab, int stride) {
-  return (c & 0x8000u) ? gamtab + (size_t)(c & 0x7fffu) * stride : slab + (size_t)(c & 0xffffu) * stride;
+// base of child row c of an x schedule: a slab slot, (bit 15) the y's Gamma
+// row of a gamma child or component, or (bit 14) the y's Phi row of a phi
+// component
+__device__ __forceinline__ const double* child_row(uint32_t c, const double* slab, const double* gamtab,
+                                                   const double* phitab, int stride) {
+  const double* base = (c & 0x8000u) ? gamtab : (c & 0x4000u) ? phitab : slab;
+  return base + (size_t)(c & 0x3fffu) * stride;
 }
 
 template <int MAXK>
 __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds_f64* hb,
                             const lds_f64* co, const lds_f64* gp, double* __restrict__ slab, int x,
                             int lane, bool gam, const double* __restrict__ gamtab,
-                            const lds_f64* kap) {
+                            const lds_f64* kap, const double* __restrict__ phitab,
+                            const double* __restrict__ phikap) {
   constexpr int stride = 64 * MAXK;
   const DevSet& s = P.xset;
   const DevSet& ys = P.yset;
@@ -330,6 +353,9 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
   if (gam) {
     const double* __restrict__ h = P.pn.gam_h + (int64_t)x * s.n_gam;
     for (int g = lane; g < s.n_gam; g += 64) kacc += h[g] * kap[g];
+    if (P.phi_on)  // phi rows' Phi components: sum P_p w kappa_Phi
+      for (int j = s.ex_phk_base[x] + lane; j < s.ex_phk_base[x + 1]; j += 64)
+        kacc += P.pn.phk_w[j] * phikap[s.phk_idx[j]];
   }
   if (nlx == 0) {
     for (int off = 32; off > 0; off >>= 1) kacc += __shfl_xor(kacc, off, 64);
@@ -388,7 +414,10 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     const double xeg0 = gp[xa >> 16];
     // single bp-frequency entry of x (the common single-sequence case)
     const bool x_one = xnbf == 1 && x_nbp == 0.0;
-    const uint32_t xcode = (xc >> 16) * 16u;
+    const uint32_t xcode = ((xc >> 16) & 0xffu) * 16u;
+    // a phi (combination) row: G0 = S, the weighted sum of its component
+    // rows; no MATCH, no sweep (its K terms come with the y's Phi sums)
+    const bool combo = (xc >> 31) != 0u;
 #if SK_SKIP_LOOPS == 2  // cost experiment: rows whose children are all gamma rows
     bool skipr = gam && xne > 0 && xne <= 4;
 #pragma unroll
@@ -459,12 +488,12 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
         na += take ? 1 : 0;
       }
       for (int h = 0; h < 4; h += 2) {
-        if (na > h) {
+        if (na > h && !(SK_PHI_EXP == 1 && combo)) {
           const bool two = na > h + 1;
           const uint32_t c0 = c[h], c1 = two ? c[h + 1] : c[h];
           const double eg0 = w[h], eg1 = two ? w[h + 1] : 0.0;
-          add_rows2<MAXK>(S, row_rsrc(child_row(c0, slab, gamtab, stride), NLy),
-                          row_rsrc(child_row(c1, slab, gamtab, stride), NLy), eg0, eg1, lane);
+          add_rows2<MAXK>(S, row_rsrc(child_row(c0, slab, gamtab, phitab, stride), NLy),
+                          row_rsrc(child_row(c1, slab, gamtab, phitab, stride), NLy), eg0, eg1, lane);
         }
       }
     }
@@ -475,13 +504,13 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       cnt[0] += nl_ + (xne > 4 ? xne - 4 : 0);
     }
 #endif
-    for (int t = 4; t < xne; t += 2) {  // children past the fourth
+    for (int t = 4; t < xne && !(SK_PHI_EXP == 1 && combo); t += 2) {  // children past the fourth
       const uint32_t c0 = xch[chp_r + t];
       const bool two = t + 1 < xne;
       const uint32_t c1 = two ? xch[chp_r + t + 1] : c0;
       const double eg0 = xchw[chp_r + t], eg1 = two ? xchw[chp_r + t + 1] : 0.0;
-      add_rows2<MAXK>(S, row_rsrc(child_row(c0, slab, gamtab, stride), NLy),
-                      row_rsrc(child_row(c1, slab, gamtab, stride), NLy), eg0, eg1, lane);
+      add_rows2<MAXK>(S, row_rsrc(child_row(c0, slab, gamtab, phitab, stride), NLy),
+                      row_rsrc(child_row(c1, slab, gamtab, phitab, stride), NLy), eg0, eg1, lane);
     }
     STAMP(1);
 
@@ -499,14 +528,16 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      the pass's edge count, not its largest node degree.
     //      (LDS ops of a wave complete in issue order.)
     // (nodes from qb up have M = 0 and are never read as children here)
+    if (!combo) {
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = lane + 64 * k < qb ? S[k] : 0.0;
+      for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = lane + 64 * k < qb ? S[k] : 0.0;
+    }
     double rowk = 0.0;
     STAMP(2);
 #ifdef SK_STAMPS
     cnt[3] += qb > qa ? qb - qa : 0;
 #endif
-    if (qa < qb && !(SK_SKIP_LOOPS && skipr)) {
+    if (!combo && qa < qb && !(SK_SKIP_LOOPS && skipr)) {
       // node records and path counts come from HBM (L2-resident per y),
       // the first pass's issued before A, each later pass's during the
       // pass before.  A pass covers NW = 64*SK_PW nodes [q0, top], lane l
@@ -654,7 +685,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) {
       const int q = lane + 64 * k;
-      if (64 * k < qa && q < qa) R[q] = 0.0;
+      if (!combo && 64 * k < qa && q < qa) R[q] = 0.0;
     }
     kacc += xP * rowk;
     wave_sync();
@@ -697,12 +728,12 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
         }
       }
       if (npf >= 1) {
-        const __amdgpu_buffer_rsrc_t r0 = row_rsrc(child_row(pf0, slab, gamtab, stride), NLy);
+        const __amdgpu_buffer_rsrc_t r0 = row_rsrc(child_row(pf0, slab, gamtab, phitab, stride), NLy);
 #pragma unroll
         for (int k = 0; k < MAXK; ++k) T0[k] = row_ld(r0, lane, k);
       }
       if (NPF >= 2 && npf >= 2) {
-        const __amdgpu_buffer_rsrc_t r1 = row_rsrc(child_row(pf1, slab, gamtab, stride), NLy);
+        const __amdgpu_buffer_rsrc_t r1 = row_rsrc(child_row(pf1, slab, gamtab, phitab, stride), NLy);
 #pragma unroll
         for (int k = 0; k < MAXK; ++k) T1[k] = row_ld(r1, lane, k);
       }
@@ -729,7 +760,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #endif
     // a row nobody reads (a root: pslot 0xffff) needs only its MATCH terms
     // (K is the path sum of M), so it skips the sweep and the store
-    if (c0 < Y.nch && pslot != 0xffffu && !(SK_SKIP_LOOPS && skipr)) {
+    if (!combo && c0 < Y.nch && pslot != 0xffffu && !(SK_SKIP_LOOPS && skipr)) {
       iy_sweep(Y, R, c0, lane);
       wave_sync();
     }
@@ -746,12 +777,18 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       double* __restrict__ orow = slab + (size_t)pslot * stride + lane;
       // all R reads issued before the first store (one LDS round trip)
       double g1[MAXK];
+      const double cw = combo ? 1.0 : xwg;
+      if (combo) {
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k) g1[k] = R[lane + 64 * k];
+        for (int k = 0; k < MAXK; ++k) g1[k] = 0.0;
+      } else {
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k) g1[k] = R[lane + 64 * k];
+      }
       SCHED_FENCE();
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) {
-        const double o = g1[k] + xwg * S[k];
+        const double o = g1[k] + cw * S[k];
 #ifndef SK_XNOSTORE
         orow[64 * k] = o;
 #endif
@@ -810,6 +847,9 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   for (int j = 0; j < SK_PW; ++j) hb[64 * j + lane] = 0.0;  // kept zero between MATCH passes
   double* slab = P.scratch + (size_t)(blockIdx.x * nwaves + wave) * P.slab_doubles;
   double* gamtab = P.gam_on ? P.gam + (size_t)blockIdx.x * P.gam_doubles : nullptr;
+  // the workgroup's Phi table: n_phi rows of 64*MAXK, then their sums kappa
+  double* phitab = P.phi_on ? P.phi + (size_t)blockIdx.x * P.phi_doubles : nullptr;
+  double* phikap = P.phi_on ? phitab + (size_t)P.xset.n_phi * (64 * MAXK) : nullptr;
   const double gap2 = P.gap2;
   const int band = (int)P.band;
 
@@ -907,6 +947,89 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
         wave_sync();
       }
       __syncthreads();  // the table and kappa, for every wave's pairs
+
+      // Phi rows of the item's phi keys t = (code a, len, gamma key g):
+      // M_t[q] = co[a][bp(q)] p(q) sum_{cy in ch(q)} g^gy Gamma_g[cy] over
+      // the y stems q in len's band; Phi_t = its IY sweep; kappa_t = sum_q
+      // M_t[q] P_y[q] (a phi row's MATCH row is pf_p sum_c w_c M_{t(c)} plus
+      // its Gamma_{a,len} part)
+      if (P.phi_on && SK_PHI_EXP != 2) {
+        // the item's keys come sorted by gamma key: wave w takes the w-th
+        // contiguous share, and H_g[q] = sum_{cy in ch(q)} g^gy Gamma_g[cy]
+        // (independent of the key's code and length) is formed once per
+        // gamma key from the Gamma row staged in the wave's LDS row
+        const DevSet& xset = P.xset;
+        const int pb = P.item_phi_off[it], pe = P.item_phi_off[it + 1];
+        const int share = (pe - pb + nwaves - 1) / nwaves;
+        const int t0 = pb + wave_u * share, t1 = min(pe, t0 + share);
+        int gcur = -1;
+        double Hr[MAXK];
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k) Hr[k] = 0.0;
+        for (int t = t0; t < t1; ++t) {
+          const int idx = __builtin_amdgcn_readfirstlane(P.item_phi[t]);
+          const int g = __builtin_amdgcn_readfirstlane((int)xset.phi_g[idx]);
+          if (g != gcur) {
+            gcur = g;
+            const double* __restrict__ grow = gamtab + (size_t)g * (64 * MAXK);
+#pragma unroll
+            for (int k = 0; k < MAXK; ++k) R[lane + 64 * k] = grow[lane + 64 * k];
+            wave_sync();
+            for (int k = 0; k < MAXK; ++k) {
+              const int q = lane + 64 * k;
+              double H = 0.0;
+              if (q < Y.nl) {
+                const uint32_t na = Y.nrg[q].x;
+                const int ne = (int)((na >> 16) & 0xff), e0 = (int)(na & 0xffff);
+                for (int e = 0; e < ne; ++e) {
+                  const uint32_t rec = Y.ed2[e0 + e];
+                  H += gp[rec >> 22] * R[rec & 0x7ff];
+                }
+              }
+              Hr[k] = H;
+            }
+            wave_sync();
+          }
+          const uint32_t al = xset.phi_al[idx];
+          const int acode = (int)(al >> 16) * 16, alen = (int)(al & 0xffff);
+          double kp = 0.0;
+#pragma unroll
+          for (int k = 0; k < MAXK; ++k) {
+            const int q = lane + 64 * k;
+            double M = 0.0;
+            if (q < Y.nl) {
+              const uint4 nd = Y.nrg[q];
+              const int ylen = (int)(s.yn_b[nb + q] & 0xffff);
+              if (Hr[k] != 0.0 && (band == 0 || abs(alen - ylen) <= band)) {
+                double vs;
+                if ((nd.y >> 24) != 0u) {
+                  vs = co[acode + ((nd.y >> 16) & 0xf)] * (double)__uint_as_float(nd.w);
+                } else {
+                  vs = 0.0;
+                  const int yb0 = (int)(s.yn_b[nb + q] >> 16), ynb = (int)(nd.x >> 24);
+                  for (int b = 0; b < ynb; ++b)
+                    vs += co[acode + s.bpf_code[bb + yb0 + b]] * (double)s.bpf_p[bb + yb0 + b];
+                }
+                M = vs * Hr[k];
+                kp += M * s.yn_P[nb + q];
+              }
+            }
+            R[q] = M;
+          }
+          for (int off = 32; off > 0; off >>= 1) kp += __shfl_xor(kp, off, 64);
+          if (lane == 0) phikap[idx] = kp;
+          wave_sync();
+          int c0 = 0;
+          if (band > 0) c0 = Y.ycs[min(max(alen - band, 0), Y.lmax + 1)];
+          c0 = __builtin_amdgcn_readfirstlane(c0);
+          if (c0 < Y.nch) iy_sweep(Y, R, c0, lane);
+          double* prow = phitab + (size_t)idx * (64 * MAXK);
+#pragma unroll
+          for (int k = 0; k < MAXK; ++k) prow[lane + 64 * k] = R[lane + 64 * k];
+          wave_sync();
+        }
+        __syncthreads();
+      }
     }
 
     // the item's pairs (costliest first) go to whichever wave is free next
@@ -916,7 +1039,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     __syncthreads();
     for (int t = wave_u; t < item.z;) {
       const int x = P.xs[item.y + t];
-      const double k = stem_pair<MAXK>(P, Y, R, hb, co, gp, slab, x, lane, gam, gamtab, kap);
+      const double k = stem_pair<MAXK>(P, Y, R, hb, co, gp, slab, x, lane, gam, gamtab, kap, phitab, phikap);
       if (lane == 0) P.out[P.oidx[item.y + t]] = k;
       int nt = 0;
       // generic-pointer atomic on the LDS counter

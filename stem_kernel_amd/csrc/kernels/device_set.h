@@ -106,6 +106,23 @@ struct DevSet {
   const int32_t* ex_gapless = nullptr;  // y role: no gap column in any non-leaf node
   const uint32_t* gam_key = nullptr;
   int32_t n_gam = 0;
+  // phi rows (combination rows, flag bit 31 of XRow.c): child record bit 14
+  // = a Phi table row (low bits: phi index); xg_cty per record its weight
+  // recipe (0 g^gaps; 1 gamma child g^gaps g^lg pf; 2 Phi component
+  // pf_p g^gaps g^lg pf_c; 3 Gamma_{code,len} component pf_p xSL_p; 4 Gamma
+  // component of a child gap2 w_p g^gaps g^lg pf_c); gra_* the rows'
+  // Gamma_{code,len} K terms (gamma index, gamma-schedule row); phk_idx per
+  // example the phi index of each type-2 record, in record order; phi key t =
+  // (phi_al[t] = code:16 | len:16, phi_g[t] = gamma index of the child key)
+  const uint8_t* xg_cty = nullptr;
+  const uint32_t* gra_gidx = nullptr;
+  const uint32_t* gra_row = nullptr;
+  const int32_t* ex_gra_base = nullptr;  // n_examples + 1
+  const uint32_t* phk_idx = nullptr;
+  const int32_t* ex_phk_base = nullptr;  // n_examples + 1
+  const uint32_t* phi_al = nullptr;
+  const uint32_t* phi_g = nullptr;
+  int32_t n_phi = 0;
   // maxima over the set
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
   int32_t max_nch = 0;
@@ -124,6 +141,7 @@ struct DevParamNodes {
   double* xg_chw = nullptr;
   double* gam_h = nullptr;
   double* xr_chw = nullptr;  // x schedule child weights g^gaps
+  double* phk_w = nullptr;   // per phi component: P_p times its record weight (K terms)
 };
 
 }  // namespace sk

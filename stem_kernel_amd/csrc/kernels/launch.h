@@ -36,6 +36,14 @@ struct StemLaunch {
   double* gam = nullptr;
   int64_t gam_doubles = 0;  // per workgroup
   int32_t gam_on = 0;
+  // Phi rows (phi_on: the x set has phi keys): per-workgroup table of
+  // xset.n_phi rows of 64*MAXK doubles and their n_phi sums; the item's phi
+  // keys item_phi[item_phi_off[it] .. item_phi_off[it + 1])
+  double* phi = nullptr;
+  int64_t phi_doubles = 0;  // per workgroup
+  const int32_t* item_phi_off = nullptr;
+  const int32_t* item_phi = nullptr;
+  int32_t phi_on = 0;
   unsigned long long* stamps = nullptr;  // diagnostic builds (SK_STAMPS) only
 };
 

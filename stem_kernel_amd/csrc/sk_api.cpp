@@ -103,6 +103,13 @@ struct HostPack {
   std::vector<float> xg_cpf, gr_pf;
   std::vector<double> gr_P;
   std::vector<int32_t> ex_xg_base, ex_nlxg, ex_xgch_base, ex_gr_base, ex_gapless;
+  // phi rows (combination rows of the gamma schedule): per child record its
+  // weight recipe, the rows' Gamma_{code,len} K inputs, each example's phi
+  // components (phi key per type-2 record, in record order), the phi keys
+  std::vector<uint8_t> xg_cty;
+  std::vector<uint32_t> gra_gidx, gra_row, phk_idx, phi_al, phi_g;
+  std::vector<int32_t> ex_gra_base, ex_phk_base;
+  std::vector<uint64_t> ex_phi_bits;  // per example, the phi keys it uses (bitset)
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
   int32_t max_nch = 0;
 };
@@ -288,10 +295,30 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
   auto gamma_key = [&](const Example& X, int v) {
     return ((uint32_t)X.bpf_code[X.bpf_off[v]] << 16) | (uint32_t)(X.last[v] - X.first[v]);
   };
+  // Phi rows: stem rows with one bp-frequency entry and no gap column whose
+  // children are all gamma rows.  Their G0 row is linear in per-y tables
+  // (dag_stem.hip): pf [sum_c w_c Phi_{code,len,key(c)} + xSL Gamma_{code,len}]
+  // + xwg sum_c w_c Gamma_{key(c)}, so the gamma schedule holds them as
+  // combination rows (no MATCH, no sweep).
+  auto is_phi = [&](const Example& X, int v) {
+    const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
+    if (e1 == e0 || 2 * (e1 - e0) + 1 > 255) return false;
+    if (X.bpf_off[v + 1] - X.bpf_off[v] != 1 || X.prof5[(size_t)X.first[v] * 5 + 4] != 0.0f) return false;
+    for (uint32_t k = e0; k < e1; ++k)
+      if (!is_gamma(X, X.edge_to[k])) return false;
+    return !is_gamma(X, v);
+  };
+  std::vector<uint64_t> phi_raw;  // child gamma key:32 | code:16 | len:16 (sorted: by child key)
   for (int e = 0; e < n; ++e) {
     const Example& X = ds->ex[e];
-    for (int v = 0; v < X.n_nodes(); ++v)
+    for (int v = 0; v < X.n_nodes(); ++v) {
       if (is_gamma(X, v)) P.gam_key.push_back(gamma_key(X, v));
+      if (is_phi(X, v)) {
+        P.gam_key.push_back(gamma_key(X, v));
+        for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k)
+          phi_raw.push_back(((uint64_t)gamma_key(X, X.edge_to[k]) << 32) | gamma_key(X, v));
+      }
+    }
   }
   std::sort(P.gam_key.begin(), P.gam_key.end());
   P.gam_key.erase(std::unique(P.gam_key.begin(), P.gam_key.end()), P.gam_key.end());
@@ -299,6 +326,18 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
   if (!gam_on) P.gam_key.clear();
   auto gamma_idx = [&](uint32_t key) {
     return (uint32_t)(std::lower_bound(P.gam_key.begin(), P.gam_key.end(), key) - P.gam_key.begin());
+  };
+  std::sort(phi_raw.begin(), phi_raw.end());
+  phi_raw.erase(std::unique(phi_raw.begin(), phi_raw.end()), phi_raw.end());
+  const bool phi_on = gam_on && !phi_raw.empty() && phi_raw.size() < 0x4000 && !std::getenv("SK_NO_PHI");
+  if (phi_on)
+    for (uint64_t k : phi_raw) {
+      P.phi_al.push_back((uint32_t)k);
+      P.phi_g.push_back(gamma_idx((uint32_t)(k >> 32)));
+    }
+  auto phi_idx = [&](uint32_t key_p, uint32_t key_c) {
+    const uint64_t k = ((uint64_t)key_c << 32) | key_p;
+    return (uint32_t)(std::lower_bound(phi_raw.begin(), phi_raw.end(), k) - phi_raw.begin());
   };
   P.ex_node_base.push_back(0);
   P.ex_edge_base.push_back(0);
@@ -593,6 +632,8 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       P.ex_xg_base.push_back((int32_t)P.xgrow.size());
       P.ex_xgch_base.push_back((int32_t)P.xg_ch.size());
       P.ex_gr_base.push_back((int32_t)P.gr_info.size());
+      P.ex_gra_base.push_back((int32_t)P.gra_gidx.size());
+      P.ex_phk_base.push_back((int32_t)P.phk_idx.size());
       std::vector<uint32_t> gslot(nn, 0xffff);
       std::vector<int> gfree;
       int gslots = 0, nlxg = 0;
@@ -607,18 +648,44 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
           continue;
         }
         const bool loop = level[v] == 0;
+        const bool phi = phi_on && is_phi(X, v);
         uint32_t nch = 0;
-        if (!loop) {
+        if (phi) {
+          // components: per child c a Phi row (type 2) and its Gamma row
+          // (type 4), then Gamma_{code,len} of the row itself (type 3)
+          const uint32_t kp = gamma_key(X, v);
+          for (uint32_t k = e0; k < e1; ++k) {
+            const int c = X.edge_to[k];
+            const uint32_t kc = gamma_key(X, c);
+            const uint32_t pi = phi_idx(kp, kc);
+            for (int ty : {2, 4}) {
+              P.xg_ch.push_back(((ty == 2 ? 0x4000u | pi : 0x8000u | gamma_idx(kc))) | (X.edge_gaps[k] << 16));
+              P.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
+              P.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
+              P.xg_cty.push_back((uint8_t)ty);
+            }
+            P.phk_idx.push_back(pi);
+          }
+          P.xg_ch.push_back(0x8000u | gamma_idx(kp));
+          P.xg_clg.push_back(0u);
+          P.xg_cpf.push_back(0.0f);
+          P.xg_cty.push_back(3);
+          P.gra_gidx.push_back(gamma_idx(kp));
+          P.gra_row.push_back((uint32_t)P.xgrow.size());
+          nch = 2 * (e1 - e0) + 1;
+        } else if (!loop) {
           for (uint32_t k = e0; k < e1; ++k) {
             const int c = X.edge_to[k];
             if (gam_on && is_gamma(X, c)) {
               P.xg_ch.push_back((0x8000u | gamma_idx(gamma_key(X, c))) | (X.edge_gaps[k] << 16));
               P.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
               P.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
+              P.xg_cty.push_back(1);
             } else {
               P.xg_ch.push_back(gslot[c] | (X.edge_gaps[k] << 16));
               P.xg_clg.push_back(0u);
               P.xg_cpf.push_back(1.0f);
+              P.xg_cty.push_back(0);
             }
             ++nch;
           }
@@ -645,12 +712,19 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         xr.bp0 = b1 > b0 ? X.bpf_p[b0] : 0.0f;
         xr.P = Pw[v];
         xr.c = (P.nd_b[P.ex_node_base.back() + nid[v]] >> 16) |
-               ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16);
+               ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16) | (phi ? 0x80000000u : 0u);
         P.xgrow.push_back(xr);
         P.xg_node.push_back((uint32_t)nid[v]);
         ++nlxg;
       }
-      if (gslots >= 0x8000) {  // slot ids share the record with the gamma flag
+      if (phi_on) {  // this example's phi keys as a bitset (items take unions)
+        const size_t W = (P.phi_al.size() + 63) / 64;
+        const size_t base = P.ex_phi_bits.size();
+        P.ex_phi_bits.resize(base + W, 0ull);
+        for (size_t j = (size_t)P.ex_phk_base.back(); j < P.phk_idx.size(); ++j)
+          P.ex_phi_bits[base + P.phk_idx[j] / 64] |= 1ull << (P.phk_idx[j] % 64);
+      }
+      if (gslots >= 0x4000) {  // slot ids share the record with the gamma / phi flags
         err = "too many live DAG rows";
         return SK_ERR_UNSUPPORTED;
       }
@@ -1429,9 +1503,43 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     ctx->last_cells = cells;
   }
 
+  // the items' phi keys (the union over their x's; gapless y only), for the
+  // workgroups' Phi tables (dag_stem.hip)
+  std::vector<int32_t> item_phi_off, item_phi;
+  const bool phi_on = stem && !PX.phi_al.empty() && !PX.gam_key.empty();
+  if (phi_on) {
+    // union of the x's key bitsets, keys ordered by gamma key (the kernel
+    // forms one H row per gamma key and wave)
+    const size_t W = (PX.phi_al.size() + 63) / 64;
+    std::vector<uint64_t> acc(W);
+    std::vector<int32_t> keys;
+    item_phi_off.assign(1, 0);
+    for (size_t i = 0; i < items.size(); ++i) {
+      const int4 it = items[i];
+      if (PY.ex_gapless[it.x]) {
+        std::fill(acc.begin(), acc.end(), 0ull);
+        for (int t = it.y; t < it.y + it.z; ++t) {
+          const uint64_t* b = PX.ex_phi_bits.data() + (size_t)ixs[t] * W;
+          for (size_t w = 0; w < W; ++w) acc[w] |= b[w];
+        }
+        keys.clear();
+        for (size_t w = 0; w < W; ++w)
+          for (uint64_t m = acc[w]; m; m &= m - 1) keys.push_back((int32_t)(w * 64 + __builtin_ctzll(m)));
+        // (phi keys are numbered in gamma key order: the bits come sorted)
+        item_phi.insert(item_phi.end(), keys.begin(), keys.end());
+      }
+      item_phi_off.push_back((int32_t)item_phi.size());
+    }
+    if (std::getenv("SK_PHI_STATS"))
+      std::fprintf(stderr, "[phi] keys=%zu items=%zu item keys=%zu pairs=%lld phi components=%zu rows=%zu\n",
+                   PX.phi_al.size(), items.size(), item_phi.size(), (long long)n, PX.phk_idx.size(),
+                   PX.xgrow.size());
+  }
+
   // ---- device work arena
   const size_t nb = (size_t)n;
   size_t need = 0;
+  need += (item_phi_off.size() + item_phi.size()) * 4 + 512;
   need += 256 * 8 + 16 * 8 + (size_t)(max_len + 4) * 8 * 2;
   need += 1024;
   need += items.size() * sizeof(int4) + nb * (4 + 8) + nb * 8 * 2 + nb * 4 * 2 + 64 + 8 * 256;
@@ -1455,6 +1563,8 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   int32_t* d_bx = A.take<int32_t>(std::max<size_t>(big_x.size(), 1));
   int32_t* d_by = A.take<int32_t>(std::max<size_t>(big_x.size(), 1));
   int64_t* d_bo = A.take<int64_t>(std::max<size_t>(big_x.size(), 1));
+  int32_t* d_iphi_off = A.take<int32_t>(std::max<size_t>(item_phi_off.size(), 1));
+  int32_t* d_iphi = A.take<int32_t>(std::max<size_t>(item_phi.size(), 1));
 
   // parameter tables
   std::vector<double> co(256), st(16);
@@ -1493,14 +1603,21 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
                                hipMemcpyHostToDevice, S));
     SK_HIP(ctx, hipMemcpyAsync(d_ixs, ixs.data(), nb * 4, hipMemcpyHostToDevice, S));
     SK_HIP(ctx, hipMemcpyAsync(d_oidx, ioidx.data(), nb * 8, hipMemcpyHostToDevice, S));
+    if (phi_on) {
+      SK_HIP(ctx, hipMemcpyAsync(d_iphi_off, item_phi_off.data(), item_phi_off.size() * 4,
+                                 hipMemcpyHostToDevice, S));
+      if (!item_phi.empty())
+        SK_HIP(ctx, hipMemcpyAsync(d_iphi, item_phi.data(), item_phi.size() * 4, hipMemcpyHostToDevice, S));
+    }
     const double gap2 = kp->loop_gap * kp->loop_gap;
     const size_t nnd = std::max<size_t>(PX.nd_a.size(), 1);
     const size_t nxc = std::max<size_t>(PX.xr_ch.size(), 1), nxg = std::max<size_t>(PX.xgrow.size(), 1),
                  nxgc = std::max<size_t>(PX.xg_ch.size(), 1),
-                 ngh = std::max<size_t>(PX.ex_nl.size() * PX.gam_key.size(), 1);
+                 ngh = std::max<size_t>(PX.ex_nl.size() * PX.gam_key.size(), 1),
+                 nphk = std::max<size_t>(PX.phk_idx.size(), 1);
     if (!xs_->prep) {
       void* p = nullptr;
-      SK_HIP(ctx, hipMalloc(&p, (3 * nnd + nxc + nxg + nxgc + ngh) * sizeof(double)));
+      SK_HIP(ctx, hipMalloc(&p, (3 * nnd + nxc + nxg + nxgc + ngh + nphk) * sizeof(double)));
       xs_->prep = static_cast<double*>(p);
       xs_->buf.ptrs.push_back(p);
       xs_->prep_loop_gap = -1.0;
@@ -1513,6 +1630,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     pn.xg_SL = pn.xr_chw + nxc;
     pn.xg_chw = pn.xg_SL + nxg;
     pn.gam_h = pn.xg_chw + nxgc;
+    pn.phk_w = pn.gam_h + ngh;
     if (!(xs_->prep_loop_gap == kp->loop_gap)) {  // once per dataset and loop_gap
       SK_HIP(ctx, sk::launch_prep(xs_->dev, pn, d_gp_loop, gap2, S));
       xs_->prep_loop_gap = kp->loop_gap;
@@ -1527,7 +1645,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       const int64_t slab = (int64_t)(PX.max_slots + 1) * 64 * C.maxk;
       // + the workgroups' Gamma tables
       const int64_t gtab = (int64_t)PX.gam_key.size() * 64 * C.maxk;
-      const size_t b = (size_t)C.grid * (C.nwaves * slab + gtab) * sizeof(double);
+      // + their Phi tables and sums
+      const int64_t ptab = phi_on ? (int64_t)PX.phi_al.size() * (64 * C.maxk + 1) : 0;
+      const size_t b = (size_t)C.grid * (C.nwaves * slab + gtab + ptab) * sizeof(double);
       size_t& r = (two_streams && (c & 1)) ? scratch_x : scratch_need;
       r = std::max(r, b);
     }
@@ -1590,6 +1710,11 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SL.gam_on = !PX.gam_key.empty();
       SL.gam_doubles = (int64_t)PX.gam_key.size() * SL.lds_max_nl;
       SL.gam = SL.scratch + (size_t)C.grid * C.nwaves * SL.slab_doubles;
+      SL.phi_on = phi_on ? 1 : 0;
+      SL.phi_doubles = phi_on ? (int64_t)PX.phi_al.size() * (SL.lds_max_nl + 1) : 0;
+      SL.phi = SL.gam + (size_t)C.grid * SL.gam_doubles;
+      SL.item_phi_off = d_iphi_off + C.item_off;
+      SL.item_phi = d_iphi;
 #ifdef SK_STAMPS
       SL.stamps = d_stamps;
 #endif
@@ -2199,6 +2324,7 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, hipSetDevice(ctx->device));
   HostPack& P = ds->pack;
   P.xr_ch.insert(P.xr_ch.end(), 8, 0u);  // the kernel prefetches 4 records past a row
+  P.xg_ch.insert(P.xg_ch.end(), 8, 0u);
   DevSet& D = ds->dev;
   DeviceBuffers& B = ds->buf;
   D.n_examples = (int32_t)ds->ex.size();
@@ -2264,6 +2390,20 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.ex_gapless, &D.ex_gapless));
   SK_HIP(ctx, upload(B, P.gam_key, &D.gam_key));
   D.n_gam = (int32_t)P.gam_key.size();
+  SK_HIP(ctx, upload(B, P.xg_cty, &D.xg_cty));
+  {
+    std::vector<int32_t> b1 = P.ex_gra_base, b2 = P.ex_phk_base;
+    b1.push_back((int32_t)P.gra_gidx.size());
+    b2.push_back((int32_t)P.phk_idx.size());
+    SK_HIP(ctx, upload(B, b1, &D.ex_gra_base));
+    SK_HIP(ctx, upload(B, b2, &D.ex_phk_base));
+  }
+  SK_HIP(ctx, upload(B, P.gra_gidx, &D.gra_gidx));
+  SK_HIP(ctx, upload(B, P.gra_row, &D.gra_row));
+  SK_HIP(ctx, upload(B, P.phk_idx, &D.phk_idx));
+  SK_HIP(ctx, upload(B, P.phi_al, &D.phi_al));
+  SK_HIP(ctx, upload(B, P.phi_g, &D.phi_g));
+  D.n_phi = (int32_t)P.phi_al.size();
   D.max_nl = P.max_nl;
   D.max_edges = P.max_edges;
   D.max_bpf = P.max_bpf;

@@ -1,10 +1,12 @@
-"""Gamma rows of the DAG stem kernel (dag_stem.hip): x loop
-rows with one bp-frequency entry and no gap column are not swept per pair,
-their G0 rows come from the y's Gamma table.  The schedule with them
-(default) and without them (SK_NO_GAMMA, read when a dataset is packed) agree
-to rounding, and both match the oracle, on inputs that mix the cases: single
-sequences, gapless alignments (several bp-frequency entries per node: the
-general Gamma seed), gapped alignments (no Gamma for that y), length bands and
+"""Gamma and phi rows of the DAG stem kernel (dag_stem.hip):
+x loop rows with one bp-frequency entry and no gap column are not swept per
+pair, their G0 rows come from the y's Gamma table; stem rows whose children
+are all such rows are combinations of the y's Phi and Gamma rows.  The
+schedules with both (default), without phi rows (SK_NO_PHI) and without
+either (SK_NO_GAMMA; both read when a dataset is packed) agree to rounding,
+and all match the oracle, on inputs that mix the cases: single sequences,
+gapless alignments (several bp-frequency entries per node: the general
+seeds), gapped alignments (no Gamma / Phi for that y), length bands and
 separate row / column sets."""
 import os
 
@@ -25,26 +27,28 @@ def _inputs(seed):
             mutate_alignment(base[0], 2, seed + 3, gap=0.0)]
 
 
-def _gram(ctx, items, kern, no_gamma):
-    old = os.environ.pop("SK_NO_GAMMA", None)
+def _gram(ctx, items, kern, switch=None):
+    saved = {k: os.environ.pop(k, None) for k in ("SK_NO_GAMMA", "SK_NO_PHI")}
     try:
-        if no_gamma:
-            os.environ["SK_NO_GAMMA"] = "1"
+        if switch:
+            os.environ[switch] = "1"
         ds, om = make_examples(items)
         return ctx.gram(ds, kern), om
     finally:
-        os.environ.pop("SK_NO_GAMMA", None)
-        if old is not None:
-            os.environ["SK_NO_GAMMA"] = old
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
 
 
 @pytest.mark.parametrize("band", [0, 4])
 def test_gamma_on_off_and_oracle(gpu_ctx, band):
     items = _inputs(0x6A44A + band)
     kern = ska.SuStemKernel(loop_gap=0.4, len_band=band)
-    on, om = _gram(gpu_ctx, items, kern, False)
-    off, _ = _gram(gpu_ctx, items, kern, True)
-    assert rel_err(on, off) < 1e-12
+    on, om = _gram(gpu_ctx, items, kern)
+    no_phi, _ = _gram(gpu_ctx, items, kern, "SK_NO_PHI")
+    off, _ = _gram(gpu_ctx, items, kern, "SK_NO_GAMMA")
+    assert rel_err(on, off) < 1e-12 and rel_err(no_phi, off) < 1e-12
     n = len(items)
     ref = np.array([[po.su_stem(om[i], om[j], 0.4, kern.params.beta, band) for j in range(n)]
                     for i in range(n)])
@@ -53,8 +57,8 @@ def test_gamma_on_off_and_oracle(gpu_ctx, band):
 
 
 def test_gamma_row_and_column_sets(gpu_ctx):
-    """Gamma keys belong to the row (x) set; the column set's Gamma tables are
-    built from them."""
+    """Gamma and phi keys belong to the row (x) set; the column set's Gamma
+    and Phi tables are built from them."""
     train, om = make_examples(_inputs(0x6A450))
     test, omt = make_examples([ska.random_sequences(1, 70, 0x6A451)[0],
                                mutate_alignment(ska.random_sequences(1, 66, 0x6A452)[0], 2, 3, gap=0.0)])
