@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1335,6 +1336,13 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   const bool stem = kind_has_stem(kp->kind), str = kind_has_str(kp->kind);
   const HostPack& PX = xs_->pack;
   const HostPack& PY = ys_->pack;
+  // SK_HOST_STATS: host planning time per phase (diagnostic)
+  const bool host_stats = std::getenv("SK_HOST_STATS") != nullptr;
+  auto now_ms = [] {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  const double th0 = host_stats ? now_ms() : 0.0;
+  double th1 = th0, th2 = th0;
 
   // ---- host-side work lists
   // stem items: pairs grouped by y, chunks, largest first, in classes by the
@@ -1365,10 +1373,20 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     }
     // within one y, costliest x first: the waves of a workgroup take the
     // item's pairs round-robin, so equal-cost rounds and a cheap last round
-    for (int j = 0; j < ny; ++j)
-      std::stable_sort(byy.begin() + cnt[j], byy.begin() + cnt[j + 1], [&](int64_t a, int64_t b) {
-        return PX.ex_nl[x[a]] > PX.ex_nl[x[b]];
-      });
+    // (one packed key per pair, ties by input order: deterministic)
+    {
+      std::vector<uint64_t> key;
+      for (int j = 0; j < ny; ++j) {
+        const int64_t b = cnt[j], e = cnt[j + 1];
+        if (e - b < 2) continue;
+        key.resize(e - b);
+        for (int64_t t = b; t < e; ++t)
+          key[t - b] = ((uint64_t)(0xffffffffu - (uint32_t)PX.ex_nl[x[byy[t]]]) << 32) | (uint32_t)(t - b);
+        std::sort(key.begin(), key.end());
+        std::vector<int64_t> tmp(byy.begin() + b, byy.begin() + e);
+        for (int64_t t = b; t < e; ++t) byy[t] = tmp[(uint32_t)key[t - b]];
+      }
+    }
     ixs.resize(n);
     ioidx.resize(n);
     for (int64_t t = 0; t < n; ++t) {
@@ -1503,6 +1521,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     ctx->last_cells = cells;
   }
 
+  if (host_stats) th1 = now_ms();
   // the items' phi keys (the union over their x's; gapless y only), for the
   // workgroups' Phi tables (dag_stem.hip)
   std::vector<int32_t> item_phi_off, item_phi;
@@ -1536,6 +1555,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
                    PX.xgrow.size());
   }
 
+  if (host_stats) th2 = now_ms();
   // ---- device work arena
   const size_t nb = (size_t)n;
   size_t need = 0;
@@ -1676,6 +1696,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     SK_HIP(ctx, hipMalloc(&d_stamps, 16 * sizeof(unsigned long long)));
     SK_HIP(ctx, hipMemsetAsync(d_stamps, 0, 16 * sizeof(unsigned long long), S));
 #endif
+    if (host_stats)
+      std::fprintf(stderr, "[host] pairs=%lld plan %.2f ms, phi keys %.2f ms, uploads+prep %.2f ms\n",
+                   (long long)n, th1 - th0, th2 - th1, now_ms() - th2);
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     if (two_streams) {
       SK_HIP(ctx, hipEventRecord(ctx->evk, S));
