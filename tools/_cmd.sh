@@ -1,5 +1,5 @@
 set -o pipefail
-for v in "" build/libsk_skl1.so build/libsk_skl0.so; do
-  SK_LIB_PATH=$v timeout -k 10 400 python3 -u bench.py --config ns --no-cpu-baseline > gpurun_out/v.log 2>&1 || { tail -20 gpurun_out/v.log; exit 1; }
-  python3 -c "import json; d=json.loads(open('gpurun_out/v.log').read().strip().splitlines()[-1]); print('$v', round(d['value']), round(d['roofline']['kernel_ms_per_launch'],1))"
-done
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/t.log 2>&1 || { tail -40 gpurun_out/t.log; exit 1; }
+tail -2 gpurun_out/t.log
+SK_HOST_STATS=1 timeout -k 10 300 python3 -u bench.py --config ns --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/hs.log 2>&1; grep -a "\[host\]" gpurun_out/hs.log | tail -2
+bash tools/gpu_quick.sh ns
