@@ -638,8 +638,33 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       std::vector<uint32_t> gslot(nn, 0xffff);
       std::vector<int> gfree;
       int gslots = 0, nlxg = 0;
-      for (int v = 0; v < nn; ++v) {
-        if (level[v] < 0) continue;
+      // row order: post-order, each phi row moved to just before its first
+      // parent (it has no row children, so any earlier place is valid): the
+      // parent then takes it from registers (distance 1), and the row before
+      // it, usually a swept one, prefetches its first components
+      std::vector<int> order;
+      {
+        std::vector<int> first_parent(nn, nn);
+        for (int v = 0; v < nn; ++v)
+          for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k)
+            first_parent[X.edge_to[k]] = std::min(first_parent[X.edge_to[k]], v);
+        std::vector<std::vector<int>> before(nn + 1);
+        const bool move = phi_on && !std::getenv("SK_PHI_POSTORDER");
+        for (int v = 0; v < nn; ++v) {
+          if (level[v] < 0) continue;
+          if (move && is_phi(X, v)) before[first_parent[v]].push_back(v);
+          else order.push_back(v);
+        }
+        std::vector<int> o2;
+        o2.reserve(order.size() + 8);
+        for (int v : order) {
+          for (int u : before[v]) o2.push_back(u);
+          o2.push_back(v);
+        }
+        for (int u : before[nn]) o2.push_back(u);  // roots
+        order.swap(o2);
+      }
+      for (int v : order) {
         const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
         const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
         if (gam_on && is_gamma(X, v)) {
