@@ -80,9 +80,49 @@ struct StrLaunch {
   const int32_t* ys = nullptr;
   int64_t n_pairs = 0;
   double* out = nullptr;
+  const int64_t* oidx = nullptr;  // out[oidx[k]] (nullptr: out[k])
   unsigned long long* pair_counter = nullptr;
   int32_t lds_max_len = 0;
 };
+
+// Profile string kernel, fast path (dyadic profiles without empty columns,
+// both examples weighted or neither; profile_string.hip): per-position
+// operands x role v_l = (sum_k st[k][l] x_k) / xs * w, y role v_l = y_l / ys
+// * w, so a cell's weighted subst_score is sum_l vx_l vy_l.
+struct StrPos {
+  double v[4];
+};
+// one-hot columns (single sequences): the residue code and the weight
+struct StrCode {
+  float w;
+  int32_t code;
+};
+struct StrFastLaunch {
+  DevSet xset, yset;
+  const StrPos* xtab = nullptr;  // by x-set position (onehot: StrCode)
+  const StrPos* ytab = nullptr;  // by y-set position (onehot: StrCode)
+  const double* st = nullptr;    // 16: the substitution table (onehot)
+  int32_t onehot = 0;
+  const double* gpow = nullptr;  // gap^k (the reference's repeated products), k <= max_len
+  double gap = 0.0;
+  const int32_t* xs = nullptr;   // pair k: x = xs[k], y = ys[k] -> out[oidx ? oidx[k] : k]
+  const int32_t* ys = nullptr;
+  const int64_t* oidx = nullptr;
+  int64_t n_pairs = 0;
+  double* out = nullptr;
+  unsigned long long* pair_counter = nullptr;
+  int32_t lds_max_len = 0;  // >= 64
+};
+__host__ __device__ inline size_t str_fast_wave_lds_bytes(int maxlen, bool onehot) {
+  return ((size_t)maxlen * (onehot ? sizeof(StrCode) : sizeof(StrPos)) + (size_t)2 * (maxlen + 2) * 8 + 15) &
+         ~(size_t)15;
+}
+constexpr size_t kStrFastLds0 = 16 * 8;  // the substitution table
+hipError_t launch_str_tab(const float4* prof, const float* pos_w, int64_t n, const double* st, StrPos* xrole,
+                          StrPos* yrole, hipStream_t stream);
+hipError_t launch_str_code_tab(const float4* prof, const float* pos_w, int64_t n, StrCode* tab,
+                               hipStream_t stream);
+hipError_t launch_str_fast(const StrFastLaunch& P, int grid, int nwaves, hipStream_t stream);
 
 // Per-position BPLA score operands, computed per call by sk_bpla_tab_kernel
 // (dyadic profile columns only, see bpla.hip): x role v = u_l / xs with

@@ -11,6 +11,9 @@
 // through a per-wave LDS row.  Row-local K1/G1 stay in registers.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
+#include "bpla_fast.h"
 #include "device_set.h"
 #include "launch.h"
 
@@ -163,7 +166,7 @@ __global__ void __launch_bounds__(256) sk_profile_string_kernel(StrLaunch P) {
     // the lane that owned row Lx holds the result
     const int owner = Lx == 0 ? 0 : ((Lx - 1) & 63);
     result = (Lx == 0 || Ly == 0) ? 1.0 : __shfl(result, owner, 64);
-    if (lane == 0) P.out[pr] = result;
+    if (lane == 0) P.out[P.oidx ? P.oidx[pr] : (int64_t)pr] = result;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -184,6 +187,221 @@ hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st) 
   }
   hipLaunchKernelGGL(sk_profile_string_kernel, dim3(grid), dim3(64 * nwaves),
                      str_lds_bytes(P, nwaves), st, P);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Fast path: profiles whose columns are dyadic (multiples of 1/256: single
+// sequences, alignments of 2^k rows, IUPAC codes) and never empty.  There
+// subst_score's float weight n = xs * ys exactly, so with per-position
+// operands (sk_str_tab_kernel) the weighted score of a cell is
+// sum_l vx_l vy_l: four FMAs instead of 16 products, a float sum and a
+// divide.  The DP (string_kernel.cpp:10-62, as the general kernel above):
+//   v = G0[i-1][j-1] * w_x w_y subst;  K1 = v + K1[i][j-1];  G1 = v + G1[i][j-1] g
+//   K0 = K1 + K0[i-1][j];  G0 = G1 + G0[i-1][j] g;  row 0: (1, g^j); column 0: (1, g^i)
+// runs on the systolic schedule of the BPLA fast path (bpla.hip): lane l
+// owns row 64s + l + 1, the row above arrives from lane l-1 by DPP
+// wave_shr, strips are streamed, and the steps fall in wave-uniform windows
+// (lane w starts its next row) and interiors (no per-lane control flow).
+// The result K0[Lx][Ly] is the last output of the lane that owns row Lx.
+__global__ void __launch_bounds__(256) sk_str_tab_kernel(const float4* __restrict__ prof,
+                                                         const float* __restrict__ pos_w, int64_t n,
+                                                         const double* __restrict__ st,
+                                                         StrPos* __restrict__ xrole,
+                                                         StrPos* __restrict__ yrole) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const float4 c = prof[p];
+  const double s = (double)(c.x + c.y + c.z + c.w);  // exact for dyadic columns
+  const double w = (double)pos_w[p];
+  const float cv[4] = {c.x, c.y, c.z, c.w};
+  StrPos X, Y;
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const double u = st[l] * (double)c.x + st[4 + l] * (double)c.y + st[8 + l] * (double)c.z +
+                     st[12 + l] * (double)c.w;
+    X.v[l] = s > 0.0 ? u / s * w : 0.0;
+    Y.v[l] = s > 0.0 ? (double)cv[l] / s * w : 0.0;
+  }
+  xrole[p] = X;
+  yrole[p] = Y;
+}
+
+hipError_t launch_str_tab(const float4* prof, const float* pos_w, int64_t n, const double* st, StrPos* xrole,
+                          StrPos* yrole, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sk_str_tab_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, prof, pos_w,
+                     n, st, xrole, yrole);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) sk_str_code_tab_kernel(const float4* __restrict__ prof,
+                                                              const float* __restrict__ pos_w, int64_t n,
+                                                              StrCode* __restrict__ tab) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  StrCode c;
+  c.w = pos_w[p];
+  c.code = onehot_code(prof[p]);
+  tab[p] = c;
+}
+
+hipError_t launch_str_code_tab(const float4* prof, const float* pos_w, int64_t n, StrCode* tab,
+                               hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sk_str_code_tab_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, prof,
+                     pos_w, n, tab);
+  return hipGetLastError();
+}
+
+// One pair on one wavefront; ycol: the y operands (LDS), bnd: the strip
+// boundary row {K0, G0} per column (LDS, row 0 on entry).  OH: one-hot
+// columns, subst = st[code_x][code_y] w_x w_y (the general kernel's one-hot
+// case); else the dyadic factors.
+template <bool OH>
+__device__ __forceinline__ double str_fast_pair(const StrFastLaunch& P, int x, int Ly, const void* ycol,
+                                                double* bnd, const double* st, int lane) {
+  typedef typename std::conditional<OH, StrCode, StrPos>::type Op;
+  const Op* xtab = reinterpret_cast<const Op*>(P.xtab);
+  const double gap = P.gap;
+  const int Lx = __builtin_amdgcn_readfirstlane(P.xset.ex_len[x]);
+  const int xpb = __builtin_amdgcn_readfirstlane(P.xset.ex_pos_base[x]);
+  if (Lx == 0 || Ly == 0) return 1.0;
+  const int Lys = max(Ly, 64);
+  const int nstrips = (Lx + 63) / 64;
+  const int T = (nstrips - 1) * Lys + ((Lx - 1) & 63) + Ly;
+  const char* ybase = reinterpret_cast<const char*>(ycol);
+  // my row operands and G0 of the row above at column 0, the next strip's
+  Op xn = xtab[xpb + min(lane, Lx - 1)];
+  double dn = P.gpow[lane];  // G0[i-1][0] = g^(i-1)
+  Op xr = xn;
+  unsigned yofs = 0;
+  double lK1 = 0.0, lG1 = 0.0, lK0 = 0.0, lG0 = 0.0;  // my (i, j-1) values
+  double dG = 0.0;                                     // G0[i-1][j-1]
+
+  auto cell = [&](double uK, double uG, bool c1) __attribute__((always_inline)) {
+    const Op yc = *reinterpret_cast<const Op*>(ybase + yofs);
+    double v;
+    if constexpr (OH) {
+      v = dG * (double)xr.w * (double)yc.w * st[xr.code * 4 + yc.code];
+    } else {
+      double s = xr.v[0] * yc.v[0];
+      s = __builtin_fma(xr.v[1], yc.v[1], s);
+      s = __builtin_fma(xr.v[2], yc.v[2], s);
+      s = __builtin_fma(xr.v[3], yc.v[3], s);
+      v = dG * s;
+    }
+    const double K1 = c1 ? v : v + lK1;
+    const double G1 = c1 ? v : __builtin_fma(lG1, gap, v);
+    lK1 = K1;
+    lG1 = G1;
+    lK0 = K1 + uK;
+    lG0 = __builtin_fma(uG, gap, G1);
+  };
+  // interior step: every lane inside strip s; lane 0 at column jb
+  auto interior = [&](int jb) __attribute__((always_inline)) {
+    const double* bj = bnd + 2 * jb;
+    const double uK = wave_shr1(lK0, bj[0]);
+    const double uG = wave_shr1(lG0, bj[1]);
+    cell(uK, uG, false);
+    if (lane == 63) {
+      double* bw = bnd + 2 * (jb - 63);
+      bw[0] = lK0;
+      bw[1] = lG0;
+    }
+    dG = uG;
+    yofs += (unsigned)sizeof(Op);
+  };
+  // window step w of strip s: lane w starts its row at column 1
+  auto window = [&](int s, int w) __attribute__((always_inline)) {
+    const bool wrap = lane == w;
+    if (wrap) {
+      xr = xn;
+      dG = dn;
+      yofs = 0;
+    }
+    const int jl = lane <= w ? w - lane + 1 : Lys + w - lane + 1;
+    const bool on = jl <= Ly && (lane <= w ? s < nstrips : s > 0);
+    const int jb = w + 1;
+    const double* bj = bnd + 2 * (jb <= Ly ? jb : 0);
+    const double uK = wave_shr1(lK0, bj[0]);
+    const double uG = wave_shr1(lG0, bj[1]);
+    if (on) {
+      cell(uK, uG, wrap);
+      if (lane == 63) {
+        double* bw = bnd + 2 * jl;
+        bw[0] = lK0;
+        bw[1] = lG0;
+      }
+    }
+    dG = uG;
+    yofs += (unsigned)sizeof(Op);
+  };
+  for (int s = 0; s <= nstrips; ++s) {
+    const int Ws = s * Lys;
+    const int wend = min(64, T - Ws);
+    if (wend <= 0) break;
+    for (int w = 0; w < wend; ++w) window(s, w);
+    if (s + 1 < nstrips) {
+      const int i1 = 64 * (s + 1) + lane;  // 0-based row of my next strip
+      xn = xtab[xpb + min(i1, Lx - 1)];
+      dn = P.gpow[min(i1, Lx)];
+    }
+    const int tend = s < nstrips ? min(Ws + Lys, T) : 0;
+    for (int t = Ws + 64; t < tend; ++t) interior(t - Ws + 1);
+  }
+  const int owner = (Lx - 1) & 63;
+  const double r = __shfl(lK0, owner, 64);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return r;
+}
+
+template <bool OH>
+__global__ void __launch_bounds__(256) sk_str_fast_kernel(StrFastLaunch P) {
+  typedef typename std::conditional<OH, StrCode, StrPos>::type Op;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int maxlen = P.lds_max_len;
+  double* st = reinterpret_cast<double*>(smem);
+  if (threadIdx.x < 16) st[threadIdx.x] = OH ? P.st[threadIdx.x] : 0.0;
+  __syncthreads();
+  unsigned char* wbase = smem + kStrFastLds0 + (size_t)wave * str_fast_wave_lds_bytes(maxlen, OH);
+  Op* ycol = reinterpret_cast<Op*>(wbase);
+  double* bnd = reinterpret_cast<double*>(ycol + maxlen);
+  const Op* ytab = reinterpret_cast<const Op*>(P.ytab);
+  // pairs dealt cyclically to the waves (costs within a call are alike)
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t pr = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; pr < P.n_pairs; pr += nw) {
+    const int x = __builtin_amdgcn_readfirstlane(P.xs[pr]);
+    const int y = __builtin_amdgcn_readfirstlane(P.ys[pr]);
+    const int Ly = __builtin_amdgcn_readfirstlane(P.yset.ex_len[y]);
+    const int ypb = P.yset.ex_pos_base[y];
+    const int Lys = max(Ly, 64);
+    for (int j = lane; j < Ly; j += 64) ycol[j] = ytab[ypb + j];
+    for (int j = lane; j <= Lys; j += 64) {  // row 0: K0 = 1, G0 = g^j
+      bnd[2 * j] = 1.0;
+      bnd[2 * j + 1] = j <= Ly ? P.gpow[j] : 0.0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double r = str_fast_pair<OH>(P, x, Ly, ycol, bnd, st, lane);
+    if (lane == 0) P.out[P.oidx ? P.oidx[pr] : pr] = r;
+  }
+}
+
+hipError_t launch_str_fast(const StrFastLaunch& P, int grid, int nwaves, hipStream_t stream) {
+  const size_t lds = kStrFastLds0 + (size_t)nwaves * str_fast_wave_lds_bytes(P.lds_max_len, P.onehot != 0);
+  const void* fn = P.onehot ? (const void*)sk_str_fast_kernel<true> : (const void*)sk_str_fast_kernel<false>;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  if (P.onehot)
+    hipLaunchKernelGGL(sk_str_fast_kernel<true>, dim3(grid), dim3(64 * nwaves), lds, stream, P);
+  else
+    hipLaunchKernelGGL(sk_str_fast_kernel<false>, dim3(grid), dim3(64 * nwaves), lds, stream, P);
   return hipGetLastError();
 }
 

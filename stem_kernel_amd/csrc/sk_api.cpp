@@ -73,6 +73,9 @@ struct HostPack {
       ex_len, ex_pos_base, ex_has_w;
   // every profile entry of the example a multiple of 1/256 (BPLA fast path)
   std::vector<uint8_t> ex_dyadic;
+  // dyadic and no empty profile column: the string kernel's fast path;
+  // every column one residue: its one-hot variant
+  std::vector<uint8_t> ex_str_fast, ex_onehot;
   // y examples the register-class stem kernel cannot take (more than 2048
   // non-leaf nodes, or a stem edge gap over 1023: its packed 11/11/10-bit
   // records); they go to sk_dag_stem_big_kernel (level-order arrays)
@@ -782,6 +785,23 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
           dy = dy && v == std::rint(v);
         }
       P.ex_dyadic.push_back(dy ? 1 : 0);
+      bool full = true;
+      for (int i = 0; i < X.len; ++i) {
+        const float* c = &X.prof5[(size_t)i * 5];
+        full = full && (c[0] + c[1] + c[2] + c[3]) > 0.0f;
+      }
+      P.ex_str_fast.push_back(dy && full ? 1 : 0);
+      bool oh = true;  // the device's onehot_code test (profile_string.hip)
+      for (int i = 0; i < X.len && oh; ++i) {
+        const float* c = &X.prof5[(size_t)i * 5];
+        int ones = 0, zeros = 0;
+        for (int k = 0; k < 4; ++k) {
+          ones += c[k] == 1.0f;
+          zeros += c[k] == 0.0f;
+        }
+        oh = ones == 1 && zeros == 3;
+      }
+      P.ex_onehot.push_back(oh ? 1 : 0);
     }
     P.ex_node_base.push_back((int32_t)P.nd_a.size());
     P.ex_edge_base.push_back((int32_t)P.ed.size());
@@ -1581,9 +1601,43 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   }
 
   if (host_stats) th2 = now_ms();
+  // string kernel: pairs of dyadic, never-empty profiles (both weighted or
+  // neither) take the fast path (profile_string.hip), first; the rest the
+  // general kernel, the permutation undone through oidx
+  // (one-hot pairs first, then the other fast pairs, then the rest)
+  std::vector<int32_t> spx, spy;
+  std::vector<int64_t> soidx;
+  int64_t n_soh = 0, n_sfast = 0;  // one-hot pairs; fast pairs (one-hot included)
+  if (str && kp->kind != SK_NAIVE_STR && !std::getenv("SK_STR_GENERAL")) {
+    auto cat = [&](int64_t k) {
+      const int a = x[k], b = y[k];
+      if (PX.ex_has_w[a] != PY.ex_has_w[b]) return 2;
+      if (PX.ex_onehot[a] && PY.ex_onehot[b]) return 0;
+      return PX.ex_str_fast[a] && PY.ex_str_fast[b] ? 1 : 2;
+    };
+    int64_t cnt3[3] = {0, 0, 0};
+    for (int64_t k = 0; k < n; ++k) ++cnt3[cat(k)];
+    n_soh = cnt3[0];
+    n_sfast = cnt3[0] + cnt3[1];
+    if (cnt3[0] != n && cnt3[1] != n && cnt3[2] != n) {
+      spx.reserve(n);
+      spy.reserve(n);
+      soidx.reserve(n);
+      for (int c = 0; c < 3; ++c)
+        for (int64_t k = 0; k < n; ++k)
+          if (cat(k) == c) {
+            spx.push_back(x[k]);
+            spy.push_back(y[k]);
+            soidx.push_back(k);
+          }
+    }
+  }
+  const size_t n_str_pos = n_sfast ? PX.pos_prof.size() + (ys_ == xs_ ? 0 : PY.pos_prof.size()) : 0;
+
   // ---- device work arena
   const size_t nb = (size_t)n;
   size_t need = 0;
+  need += soidx.size() * 8 + n_str_pos * (2 * sizeof(sk::StrPos) + sizeof(sk::StrCode)) + 1024;
   need += (item_phi_off.size() + item_phi.size()) * 4 + 512;
   need += 256 * 8 + 16 * 8 + (size_t)(max_len + 4) * 8 * 2;
   need += 1024;
@@ -1610,6 +1664,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   int64_t* d_bo = A.take<int64_t>(std::max<size_t>(big_x.size(), 1));
   int32_t* d_iphi_off = A.take<int32_t>(std::max<size_t>(item_phi_off.size(), 1));
   int32_t* d_iphi = A.take<int32_t>(std::max<size_t>(item_phi.size(), 1));
+  int64_t* d_soidx = soidx.empty() ? nullptr : A.take<int64_t>(soidx.size());
+  sk::StrPos* d_stab = (n_sfast > n_soh) ? A.take<sk::StrPos>(2 * n_str_pos) : nullptr;
+  sk::StrCode* d_ctab = n_soh ? A.take<sk::StrCode>(n_str_pos) : nullptr;
 
   // parameter tables
   std::vector<double> co(256), st(16);
@@ -1636,8 +1693,10 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   // here, ahead of the stem launches
   const bool side = stem && str;
   if (str) {
-    SK_HIP(ctx, hipMemcpyAsync(d_px, x, nb * 4, hipMemcpyHostToDevice, S));
-    SK_HIP(ctx, hipMemcpyAsync(d_py, y, nb * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_px, spx.empty() ? x : spx.data(), nb * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, hipMemcpyAsync(d_py, spy.empty() ? y : spy.data(), nb * 4, hipMemcpyHostToDevice, S));
+    if (d_soidx)
+      SK_HIP(ctx, hipMemcpyAsync(d_soidx, soidx.data(), soidx.size() * 8, hipMemcpyHostToDevice, S));
     if (side) {
       SK_HIP(ctx, hipEventRecord(ctx->evf, S));
       SK_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->evf, 0));
@@ -1828,9 +1887,10 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     T.gpow = d_gp_str;
     T.gap = kp->gap;
     T.naive = kp->kind == SK_NAIVE_STR ? 1 : 0;
-    T.xs = d_px;
-    T.ys = d_py;
-    T.n_pairs = n;
+    T.xs = d_px + n_sfast;
+    T.ys = d_py + n_sfast;
+    T.oidx = d_soidx ? d_soidx + n_sfast : nullptr;
+    T.n_pairs = n - n_sfast;
     T.out = str_out;
     T.pair_counter = reinterpret_cast<unsigned long long*>(d_ctr + 8);
     T.lds_max_len = (std::max(PY.max_len, 1) + 1) & ~1;
@@ -1841,9 +1901,53 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     const size_t lds = sk::str_lds_bytes(T, w);
     if (lds > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for string kernel LDS");
     const int per_cu = std::max(1, std::min<int>((int)(163840 / lds), 8));
-    const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (n + w - 1) / w);
+    const int64_t g = std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (n - n_sfast + w - 1) / w));
     SK_HIP(ctx, hipEventRecord(ctx->ev2, SS));
-    SK_HIP(ctx, sk::launch_str(T, (int)g, w, SS));
+    for (int oh = 1; oh >= 0; --oh) {
+      const int64_t b = oh ? 0 : n_soh, e = oh ? n_soh : n_sfast;
+      if (e <= b) continue;
+      const size_t npx = PX.pos_prof.size(), npy = PY.pos_prof.size();
+      const void *tx, *ty;
+      if (oh) {  // [npx] x set | [npy] y set
+        SK_HIP(ctx, sk::launch_str_code_tab(xs_->dev.pos_prof, xs_->dev.pos_w, (int64_t)npx, d_ctab, SS));
+        if (ys_ != xs_)
+          SK_HIP(ctx, sk::launch_str_code_tab(ys_->dev.pos_prof, ys_->dev.pos_w, (int64_t)npy, d_ctab + npx, SS));
+        tx = d_ctab;
+        ty = ys_ != xs_ ? d_ctab + npx : d_ctab;
+      } else {   // [npx] x role | [npx] y role (| [npy] x role, unused | [npy] y role)
+        SK_HIP(ctx, sk::launch_str_tab(xs_->dev.pos_prof, xs_->dev.pos_w, (int64_t)npx, d_st, d_stab,
+                                       d_stab + npx, SS));
+        tx = d_stab;
+        ty = d_stab + npx;
+        if (ys_ != xs_) {
+          SK_HIP(ctx, sk::launch_str_tab(ys_->dev.pos_prof, ys_->dev.pos_w, (int64_t)npy, d_st, d_stab + 2 * npx,
+                                         d_stab + 2 * npx + npy, SS));
+          ty = d_stab + 2 * npx + npy;
+        }
+      }
+      sk::StrFastLaunch F;
+      F.xset = xs_->dev;
+      F.yset = ys_->dev;
+      F.xtab = static_cast<const sk::StrPos*>(tx);
+      F.ytab = static_cast<const sk::StrPos*>(ty);
+      F.st = d_st;
+      F.onehot = oh;
+      F.gpow = d_gp_str;
+      F.gap = kp->gap;
+      F.xs = d_px + b;
+      F.ys = d_py + b;
+      F.oidx = d_soidx ? d_soidx + b : nullptr;
+      F.n_pairs = e - b;
+      F.out = str_out;
+      F.lds_max_len = (std::max(PY.max_len, 64) + 1) & ~1;
+      const size_t wl = sk::str_fast_wave_lds_bytes(F.lds_max_len, oh != 0);
+      if (wl + sk::kStrFastLds0 > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for string kernel LDS");
+      const int per_cu_w = (int)std::max<size_t>(1, std::min<size_t>(16, (163840 - sk::kStrFastLds0) / wl));
+      const int fw = std::min(4, per_cu_w);
+      const int64_t fg = std::min<int64_t>((int64_t)ctx->n_cu * std::max(1, per_cu_w / fw), (e - b + fw - 1) / fw);
+      SK_HIP(ctx, sk::launch_str_fast(F, (int)fg, fw, SS));
+    }
+    if (n_sfast < n) SK_HIP(ctx, sk::launch_str(T, (int)g, w, SS));
     SK_HIP(ctx, hipEventRecord(ctx->ev3, SS));
     if (side) {  // join before the combine
       SK_HIP(ctx, hipEventRecord(ctx->evj, ctx->side));
