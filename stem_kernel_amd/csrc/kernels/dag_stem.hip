@@ -160,7 +160,7 @@ __device__ __forceinline__ void wave_sync() {
 #define SK_W16 8
 #endif
 #ifndef SK_NPF16  // rows prefetched per row in the MAXK 16 class
-#define SK_NPF16 2
+#define SK_NPF16 1
 #endif
 #ifndef SK_PW  // MATCH pass width in 64-node groups
 #define SK_PW 4
