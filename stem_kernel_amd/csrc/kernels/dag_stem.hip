@@ -159,6 +159,12 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_W16  // waves per workgroup of the MAXK 16 class
 #define SK_W16 8
 #endif
+#ifndef SK_NPF12  // rows prefetched per row in the MAXK <= 12 classes
+#define SK_NPF12 2
+#endif
+#ifndef SK_NPF20  // rows prefetched per row in the MAXK 20 class (8 waves)
+#define SK_NPF20 2
+#endif
 #ifndef SK_NPF16  // rows prefetched per row in the MAXK 16 class
 #define SK_NPF16 1
 #endif
@@ -696,7 +702,8 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      land during the sweep; this row itself, when a child of the next,
     //      is added from registers in D.
     // rows prefetched per row: two where the register budget allows
-    constexpr int NPF = (MAXK <= 12 || (MAXK == 16 && SK_NPF16 == 2) || (MAXK == 20 && SK_W20 == 8)) ? 2 : 1;
+    constexpr int NPF = ((MAXK <= 12 && SK_NPF12 == 2) || (MAXK == 16 && SK_NPF16 == 2) ||
+                         (MAXK == 20 && SK_W20 == 8 && SK_NPF20 == 2)) ? 2 : 1;
     uint32_t nxt_done = 0;
     double egd = 0.0, egt0 = 0.0, egt1 = 0.0;
     double T0[MAXK], T1[MAXK];

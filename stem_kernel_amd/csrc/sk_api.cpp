@@ -1608,7 +1608,10 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   std::vector<int32_t> spx, spy;
   std::vector<int64_t> soidx;
   int64_t n_soh = 0, n_sfast = 0;  // one-hot pairs; fast pairs (one-hot included)
-  if (str && kp->kind != SK_NAIVE_STR && !std::getenv("SK_STR_GENERAL")) {
+  // (the fast kernels' per-wave LDS rows must fit a CU: else the general one)
+  const int str_lds_len = (std::max(PY.max_len, 64) + 1) & ~1;
+  if (str && kp->kind != SK_NAIVE_STR && !std::getenv("SK_STR_GENERAL") &&
+      sk::str_fast_wave_lds_bytes(str_lds_len, false) + sk::kStrFastLds0 <= 163840) {
     auto cat = [&](int64_t k) {
       const int a = x[k], b = y[k];
       if (PX.ex_has_w[a] != PY.ex_has_w[b]) return 2;
