@@ -780,6 +780,21 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     if (pslot == 0xffffu) {
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) S[k] = egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
+    } else if (pslot == 0xfffeu) {
+      // read only by the next row, from registers: not stored
+      const double cw = combo ? 1.0 : xwg;
+      double g1[MAXK];
+      if (combo) {
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k) g1[k] = 0.0;
+      } else {
+#pragma unroll
+        for (int k = 0; k < MAXK; ++k) g1[k] = R[lane + 64 * k];
+      }
+      SCHED_FENCE();
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k)
+        S[k] = egd * (g1[k] + cw * S[k]) + egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
     } else {
       double* __restrict__ orow = slab + (size_t)pslot * stride + lane;
       // all R reads issued before the first store (one LDS round trip)

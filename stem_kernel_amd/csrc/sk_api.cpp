@@ -667,6 +667,22 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         for (int u : before[nn]) o2.push_back(u);  // roots
         order.swap(o2);
       }
+      // rows read only by the next row, among its first four children, are
+      // never stored: the next row takes them from registers (slot 0xfffe)
+      std::vector<uint8_t> nostore(nn, 0);
+      if (!std::getenv("SK_STORE_ALL")) {
+        std::vector<int> npar(nn, 0), emitted;
+        for (int v = 0; v < nn; ++v)
+          for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) ++npar[X.edge_to[k]];
+        for (int v : order)
+          if (!(gam_on && is_gamma(X, v))) emitted.push_back(v);
+        for (size_t i = 0; i + 1 < emitted.size(); ++i) {
+          const int v = emitted[i], r = emitted[i + 1];
+          if (npar[v] != 1 || level[r] <= 0 || level[v] < 0 || (phi_on && is_phi(X, r))) continue;
+          for (uint32_t k = X.edge_off[r]; k < X.edge_off[r + 1] && k < X.edge_off[r] + 4; ++k)
+            if (X.edge_to[k] == v) nostore[v] = 1;
+        }
+      }
       for (int v : order) {
         const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
         const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
@@ -721,9 +737,11 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         }
         for (uint32_t k = e0; k < e1; ++k) {
           const int c = X.edge_to[k];
-          if (level[c] >= 0 && last_parent[c] == v && gslot[c] != 0xffff) gfree.push_back(gslot[c]);
+          if (level[c] >= 0 && last_parent[c] == v && gslot[c] < 0x4000) gfree.push_back(gslot[c]);
         }
-        if (last_parent[v] >= 0) {
+        if (nostore[v]) {
+          gslot[v] = 0xfffe;
+        } else if (last_parent[v] >= 0) {
           int sl;
           if (!gfree.empty()) {
             sl = gfree.back();
