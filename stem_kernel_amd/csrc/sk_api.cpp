@@ -641,31 +641,107 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       std::vector<uint32_t> gslot(nn, 0xffff);
       std::vector<int> gfree;
       int gslots = 0, nlxg = 0;
-      // row order: post-order, each phi row moved to just before its first
-      // parent (it has no row children, so any earlier place is valid): the
-      // parent then takes it from registers (distance 1), and the row before
-      // it, usually a swept one, prefetches its first components
+      // row order: a depth-first post-order whose last-visited child of a
+      // row is, where it can be, one that row alone reads among its first
+      // four records (stored nowhere: the row takes it from registers; see
+      // below), the reference numbering with SK_REF_ORDER; then each phi row
+      // moved to just before its first parent (it has no row children, so
+      // any earlier place is valid): the parent takes it from registers too
+      // (distance 1), and the row before it, usually a swept one, prefetches
+      // its first components
       std::vector<int> order;
       {
-        std::vector<int> first_parent(nn, nn);
+        std::vector<int> npar(nn, 0), cand(nn, -1);
         for (int v = 0; v < nn; ++v)
-          for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k)
-            first_parent[X.edge_to[k]] = std::min(first_parent[X.edge_to[k]], v);
+          for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) ++npar[X.edge_to[k]];
+        for (int v = 0; v < nn; ++v) {
+          if (level[v] <= 0 || (phi_on && is_phi(X, v))) continue;
+          for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1] && k < X.edge_off[v] + 4; ++k) {
+            const int c = X.edge_to[k];
+            if (npar[c] == 1 && level[c] >= 0 && !(gam_on && is_gamma(X, c))) {
+              cand[v] = c;
+              break;
+            }
+          }
+        }
+        if (std::getenv("SK_REF_ORDER")) {
+          for (int v = 0; v < nn; ++v)
+            if (level[v] >= 0) order.push_back(v);
+        } else {
+          std::vector<uint8_t> seen(nn, 0);
+          std::vector<std::pair<int, int>> st;  // (row, next child index; -1: candidate done)
+          auto dfs = [&](int s) {
+            if (seen[s] || level[s] < 0) return;
+            seen[s] = 1;
+            st.push_back({s, 0});
+            while (!st.empty()) {
+              auto& [v, i] = st.back();
+              const int ne = (int)(X.edge_off[v + 1] - X.edge_off[v]);
+              int next = -1;
+              while (i >= 0 && i < ne && next < 0) {
+                const int c = X.edge_to[X.edge_off[v] + i++];
+                if (c != cand[v] && !seen[c] && level[c] >= 0) next = c;
+              }
+              if (next < 0 && i >= 0) {
+                i = -1;
+                if (cand[v] >= 0 && !seen[cand[v]]) next = cand[v];
+              }
+              if (next < 0) {
+                order.push_back(v);
+                st.pop_back();
+              } else {
+                seen[next] = 1;
+                st.push_back({next, 0});
+              }
+            }
+          };
+          for (uint32_t r : X.roots) dfs((int)r);
+          for (int v = nn - 1; v >= 0; --v) dfs(v);
+        }
+        std::vector<int> pos(nn, nn), first_parent(nn, nn);
+        for (int i = 0; i < (int)order.size(); ++i) pos[order[i]] = i;
+        for (int v = 0; v < nn; ++v)
+          for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) {
+            const int c = X.edge_to[k];
+            if (pos[v] < nn && (first_parent[c] == nn || pos[v] < pos[first_parent[c]])) first_parent[c] = v;
+          }
         std::vector<std::vector<int>> before(nn + 1);
         const bool move = phi_on && !std::getenv("SK_PHI_POSTORDER");
-        for (int v = 0; v < nn; ++v) {
-          if (level[v] < 0) continue;
+        std::vector<int> o1;
+        for (int v : order) {
           if (move && is_phi(X, v)) before[first_parent[v]].push_back(v);
-          else order.push_back(v);
+          else o1.push_back(v);
         }
         std::vector<int> o2;
         o2.reserve(order.size() + 8);
-        for (int v : order) {
-          for (int u : before[v]) o2.push_back(u);
+        for (int v : o1) {
+          auto& b = before[v];
+          const auto it = std::find(b.begin(), b.end(), cand[v]);
+          if (it != b.end()) {
+            std::rotate(it, it + 1, b.end());  // the candidate last
+            for (int u : b) o2.push_back(u);
+          } else if (!b.empty() && cand[v] >= 0 && !o2.empty() && o2.back() == cand[v]) {
+            o2.pop_back();
+            for (int u : b) o2.push_back(u);
+            o2.push_back(cand[v]);
+          } else {
+            for (int u : b) o2.push_back(u);
+          }
           o2.push_back(v);
         }
         for (int u : before[nn]) o2.push_back(u);  // roots
         order.swap(o2);
+      }
+      // each row's slot is freed at its last parent in this order
+      std::vector<int> glast(nn, -1);
+      {
+        std::vector<int> gpos(nn, -1);
+        for (int i = 0; i < (int)order.size(); ++i) gpos[order[i]] = i;
+        for (int v : order)
+          for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) {
+            const int c = X.edge_to[k];
+            if (glast[c] < 0 || gpos[v] > gpos[glast[c]]) glast[c] = v;
+          }
       }
       // rows read only by the next row, among its first four children, are
       // never stored: the next row takes them from registers (slot 0xfffe)
@@ -737,7 +813,10 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         }
         for (uint32_t k = e0; k < e1; ++k) {
           const int c = X.edge_to[k];
-          if (level[c] >= 0 && last_parent[c] == v && gslot[c] < 0x4000) gfree.push_back(gslot[c]);
+          if (level[c] >= 0 && glast[c] == v && gslot[c] < 0x4000) {
+            gfree.push_back(gslot[c]);
+            gslot[c] |= 0x10000;  // freed (a second edge to c must not free it again)
+          }
         }
         if (nostore[v]) {
           gslot[v] = 0xfffe;
@@ -770,6 +849,13 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         P.ex_phi_bits.resize(base + W, 0ull);
         for (size_t j = (size_t)P.ex_phk_base.back(); j < P.phk_idx.size(); ++j)
           P.ex_phi_bits[base + P.phk_idx[j] / 64] |= 1ull << (P.phk_idx[j] % 64);
+      }
+      if (std::getenv("SK_PACK_STATS")) {  // diagnostic: rows, unstored rows, slots
+        static long s_rows = 0, s_nost = 0, s_slots = 0;
+        s_rows += nlxg;
+        for (int v = 0; v < nn; ++v) s_nost += nostore[v];
+        s_slots += gslots;
+        if (e + 1 == n) fprintf(stderr, "[sk pack] gamma schedule: %ld rows, %ld unstored, %ld slots\n", s_rows, s_nost, s_slots);
       }
       if (gslots >= 0x4000) {  // slot ids share the record with the gamma / phi flags
         err = "too many live DAG rows";
