@@ -165,6 +165,9 @@ struct sk_context {
   // tail
   hipStream_t cls = nullptr;
   hipEvent_t evk = nullptr, evx = nullptr;
+  // a fourth stream: the 4-D kernel's span launches run in parts on all four
+  hipStream_t aux = nullptr;
+  hipEvent_t eva = nullptr;
   double last_stem_ms = 0.0, last_str_ms = 0.0, last_cells = 0.0;
   int32_t last_launches = 0;
   // kernel instantiations the last compute call launched (sk_last_classes):
@@ -1364,20 +1367,28 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
         }
       }
     }
-    // work items {pair, i} per span d1, concatenated
+    // work items {pair, i} per span d1 and part, concatenated: the pairs are
+    // dealt to nh parts whose launches run on their own streams (main, class,
+    // side, aux), so each span's tail overlaps the other parts' launches (the
+    // boundary columns of k tiles are per launch item: one stream then)
+    int nh = std::getenv("SK4_STREAMS") ? std::atoi(std::getenv("SK4_STREAMS")) : 4;
+    if (std::getenv("SK_SERIAL_CLASSES") || ktiles) nh = 1;
+    nh = std::max(1, std::min({nh, 4, (int)prs.size()}));
+    const hipStream_t hs[4] = {S, ctx->cls, ctx->side, ctx->aux};
     std::vector<int2> items;
-    std::vector<int64_t> ioff(maxn + 2, 0);
-    for (int d1 = 0; d1 <= maxn; ++d1) {
-      ioff[d1] = (int64_t)items.size();
-      for (size_t p = 0; p < prs.size(); ++p)
-        for (int i = 0; i + d1 <= prs[p].n; ++i) items.push_back(make_int2((int)p, i));
-    }
-    ioff[maxn + 1] = (int64_t)items.size();
+    std::vector<int64_t> ioff((size_t)(maxn + 1) * nh + 1, 0);
+    for (int d1 = 0; d1 <= maxn; ++d1)
+      for (int h = 0; h < nh; ++h) {
+        ioff[(size_t)d1 * nh + h] = (int64_t)items.size();
+        for (size_t p = h; p < prs.size(); p += nh)
+          for (int i = 0; i + d1 <= prs[p].n; ++i) items.push_back(make_int2((int)p, i));
+      }
+    ioff.back() = (int64_t)items.size();
     if (!ali_phmm) n_band = blo.size();
     const size_t phmm_bytes =
         ali_phmm ? prs.size() * sk::phmm_pair_bytes(max_n1, max_m1) : 0;
     // boundary columns after the rings: at most the d1 = 0 launch's items
-    const size_t kb_bytes = ktiles ? (size_t)(ioff[1] - ioff[0]) * (size_t)kb_stride * 8 : 0;
+    const size_t kb_bytes = ktiles ? (size_t)(ioff[nh] - ioff[0]) * (size_t)kb_stride * 8 : 0;
     rc = ensure_scratch(ctx, std::max(ring_bytes + kb_bytes + 64, phmm_bytes));
     if (rc) return rc;
     if (Bt.cap_pairs < prs.size() || Bt.cap_items < items.size()) {
@@ -1439,14 +1450,26 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       H.band_hi = Bt.band + Bt.cap_band;
       SK_HIP(ctx, sk::launch_phmm(H, S));
     }
-    for (int d1 = 0; d1 <= maxn; ++d1) {
-      L.d1 = d1;
-      L.items = Bt.items + ioff[d1];
-      L.n_items = ioff[d1 + 1] - ioff[d1];
-      SK_HIP(ctx, sk::launch_stem4d(L, cpl, S));
-      if (L.n_items) ctx->last_s4d_classes |= 1u << ((cpl == 1 ? 0 : cpl == 2 ? 1 : cpl == 4 ? 2 : 3) +
-                                                     (L.band_lo ? 4 : 0));
-      ++launches;
+    if (nh > 1) {
+      SK_HIP(ctx, hipEventRecord(ctx->evk, S));
+      for (int h = 1; h < nh; ++h) SK_HIP(ctx, hipStreamWaitEvent(hs[h], ctx->evk, 0));
+    }
+    for (int d1 = 0; d1 <= maxn; ++d1)
+      for (int h = 0; h < nh; ++h) {
+        const size_t q = (size_t)d1 * nh + h;
+        L.d1 = d1;
+        L.items = Bt.items + ioff[q];
+        L.n_items = ioff[q + 1] - ioff[q];
+        if (!L.n_items) continue;
+        SK_HIP(ctx, sk::launch_stem4d(L, cpl, hs[h]));
+        ctx->last_s4d_classes |= 1u << ((cpl == 1 ? 0 : cpl == 2 ? 1 : cpl == 4 ? 2 : 3) +
+                                        (L.band_lo ? 4 : 0));
+        ++launches;
+      }
+    for (int h = 1; h < nh; ++h) {
+      hipEvent_t e = h == 1 ? ctx->evx : h == 2 ? ctx->evj : ctx->eva;
+      SK_HIP(ctx, hipEventRecord(e, hs[h]));
+      SK_HIP(ctx, hipStreamWaitEvent(S, e, 0));
     }
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
     SK_HIP(ctx, hipStreamSynchronize(S));
@@ -2386,6 +2409,8 @@ int sk_open(int device, void* hip_stream, sk_context** out) {
   }
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->cls, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->eva, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->evf, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->evk, hipEventDisableTiming) != hipSuccess ||
@@ -2411,7 +2436,8 @@ int sk_close(sk_context* ctx) {
   if (ctx->s4d.band) (void)hipFree(ctx->s4d.band);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->cls) (void)hipStreamDestroy(ctx->cls);
-  for (hipEvent_t e : {ctx->evf, ctx->evj, ctx->evk, ctx->evx})
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+  for (hipEvent_t e : {ctx->evf, ctx->evj, ctx->evk, ctx->evx, ctx->eva})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3})
     if (e) (void)hipEventDestroy(e);
