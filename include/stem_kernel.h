@@ -378,6 +378,12 @@ const char *sk_svm_last_error(void);
  * pairs (non-leaf nodes). */
 int sk_last_timing(const sk_context *ctx, double *stem_ms, double *string_ms,
                    double *cells, int32_t *launches);
+/* Summed durations of the last compute call's dominant-kernel launches (DAG
+ * stem, 4-D stem or BPLA), each timed by HIP events around it on its own
+ * stream, and their count: *ms_sum / *n_launches is the average launch
+ * duration a kernel-trace profiler reports.  Launches on several streams
+ * overlap, so the sum can exceed sk_last_timing's span. */
+int sk_last_launch_ms(const sk_context *ctx, double *ms_sum, int32_t *n_launches);
 /* Kernel instantiations launched by the last compute call (parity-coverage
  * diagnostic): *stem_maxk_mask has bit MAXK/4 set for every DAG stem register
  * class run (MAXK = 4, 8, ..., 32 64-node slots per lane) and bit 0 when the

@@ -168,6 +168,12 @@ struct sk_context {
   // a fourth stream: the 4-D kernel's span launches run in parts on all four
   hipStream_t aux = nullptr;
   hipEvent_t eva = nullptr;
+  // per-launch events of the dominant kernel (sk_last_launch_ms): a start and
+  // an end event around each launch on the launch's own stream
+  std::vector<hipEvent_t> lev;
+  size_t lev_used = 0;
+  double last_launch_ms_sum = 0.0;
+  int32_t last_launch_n = 0;
   double last_stem_ms = 0.0, last_str_ms = 0.0, last_cells = 0.0;
   int32_t last_launches = 0;
   // kernel instantiations the last compute call launched (sk_last_classes):
@@ -180,6 +186,37 @@ struct sk_context {
 
 namespace sk {
 hipStream_t ctx_stream(sk_context* ctx) { return ctx->stream; }
+
+// start or end event of one dominant-kernel launch, on the launch's stream
+hipError_t lev_mark(sk_context* ctx, hipStream_t s) {
+  if (ctx->lev_used == ctx->lev.size()) {
+    hipEvent_t e = nullptr;
+    const hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) return r;
+    ctx->lev.push_back(e);
+  }
+  return hipEventRecord(ctx->lev[ctx->lev_used++], s);
+}
+
+// after the launch streams are synchronized: adds the marked launches'
+// durations to the call's sum
+hipError_t lev_collect(sk_context* ctx) {
+  for (size_t i = 0; i + 1 < ctx->lev_used; i += 2) {
+    float ms = 0.f;
+    const hipError_t r = hipEventElapsedTime(&ms, ctx->lev[i], ctx->lev[i + 1]);
+    if (r != hipSuccess) return r;
+    ctx->last_launch_ms_sum += ms;
+    ++ctx->last_launch_n;
+  }
+  ctx->lev_used = 0;
+  return hipSuccess;
+}
+
+void lev_reset(sk_context* ctx) {
+  ctx->lev_used = 0;
+  ctx->last_launch_ms_sum = 0.0;
+  ctx->last_launch_n = 0;
+}
 int ctx_device(sk_context* ctx) { return ctx->device; }
 void*& ctx_comm(sk_context* ctx) { return ctx->comm; }
 void comm_destroy(void* comm);
@@ -1173,7 +1210,9 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
       units = (n_fast + w - 1) / w;
     }
     const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, units);
+    SK_HIP(ctx, sk::lev_mark(ctx, S));
     SK_HIP(ctx, sk::launch_bpla_fast(F, (int)g, w, S));
+    SK_HIP(ctx, sk::lev_mark(ctx, S));
   }
   if (n_fast < n) {
     sk::BplaLaunch G = T;
@@ -1188,10 +1227,13 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
     if (lds > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
     const int per_cu = std::max(1, std::min<int>((int)(163840 / lds), 8));
     const int64_t g = std::min<int64_t>((int64_t)ctx->n_cu * per_cu, (G.n_pairs + w - 1) / w);
+    SK_HIP(ctx, sk::lev_mark(ctx, S));
     SK_HIP(ctx, sk::launch_bpla(G, (int)g, w, S));
+    SK_HIP(ctx, sk::lev_mark(ctx, S));
   }
   SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
   SK_HIP(ctx, hipStreamSynchronize(S));
+  SK_HIP(ctx, sk::lev_collect(ctx));
   float ms = 0.f;
   SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_stem_ms = ms;
@@ -1461,7 +1503,9 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
         L.items = Bt.items + ioff[q];
         L.n_items = ioff[q + 1] - ioff[q];
         if (!L.n_items) continue;
+        SK_HIP(ctx, sk::lev_mark(ctx, hs[h]));
         SK_HIP(ctx, sk::launch_stem4d(L, cpl, hs[h]));
+        SK_HIP(ctx, sk::lev_mark(ctx, hs[h]));
         ctx->last_s4d_classes |= 1u << ((cpl == 1 ? 0 : cpl == 2 ? 1 : cpl == 4 ? 2 : 3) +
                                         (L.band_lo ? 4 : 0));
         ++launches;
@@ -1473,6 +1517,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     }
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
     SK_HIP(ctx, hipStreamSynchronize(S));
+    SK_HIP(ctx, sk::lev_collect(ctx));
     float ms = 0.f;
     SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     total_ms += ms;
@@ -1496,6 +1541,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     return fail(ctx, SK_ERR_UNSUPPORTED, "unknown kernel kind");
   ctx->last_stem_ms = ctx->last_str_ms = ctx->last_cells = 0.0;
   ctx->last_launches = 0;
+  sk::lev_reset(ctx);
   ctx->last_stem_classes = ctx->last_s4d_classes = 0;
   if (n == 0) return SK_OK;
   const int nx = (int)xs_->ex.size(), ny = (int)ys_->ex.size();
@@ -1955,7 +2001,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
 #ifdef SK_STAMPS
       SL.stamps = d_stamps;
 #endif
+      SK_HIP(ctx, sk::lev_mark(ctx, on_cls ? ctx->cls : S));
       SK_HIP(ctx, sk::launch_stem(SL, C.grid, C.nwaves, on_cls ? ctx->cls : S));
+      SK_HIP(ctx, sk::lev_mark(ctx, on_cls ? ctx->cls : S));
       ctx->last_stem_classes |= 1u << (C.maxk / 4);
     }
     if (two_streams) {
@@ -1984,7 +2032,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       BL.scratch = ctx->scratch;
       BL.stride = big_stride;
       BL.wave_doubles = big_wave;
+      SK_HIP(ctx, sk::lev_mark(ctx, S));
       SK_HIP(ctx, sk::launch_stem_big(BL, big_grid, S));
+      SK_HIP(ctx, sk::lev_mark(ctx, S));
       ctx->last_stem_classes |= 1u;
     }
     SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
@@ -2093,6 +2143,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     float ms = 0.f;
     SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->last_stem_ms = ms;
+    SK_HIP(ctx, sk::lev_collect(ctx));
   }
   if (str) {
     float ms = 0.f;
@@ -2441,6 +2492,7 @@ int sk_close(sk_context* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3})
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->lev) (void)hipEventDestroy(e);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SK_OK;
@@ -3071,6 +3123,13 @@ int sk_last_timing(const sk_context* ctx, double* stem_ms, double* string_ms, do
   if (string_ms) *string_ms = ctx->last_str_ms;
   if (cells) *cells = ctx->last_cells;
   if (launches) *launches = ctx->last_launches;
+  return SK_OK;
+}
+
+int sk_last_launch_ms(const sk_context* ctx, double* ms_sum, int32_t* n_launches) {
+  if (!ctx) return SK_ERR_INVALID;
+  if (ms_sum) *ms_sum = ctx->last_launch_ms_sum;
+  if (n_launches) *n_launches = ctx->last_launch_n;
   return SK_OK;
 }
 

@@ -584,6 +584,13 @@ class Context:
         self._chk(lib().sk_last_timing(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return dict(stem_ms=a.value, string_ms=b.value, cells=c.value, launches=d.value)
 
+    def last_launch_ms(self):
+        """Per-launch HIP-event durations of the last call's dominant kernel:
+        (summed ms, launch count); launches on several streams overlap."""
+        a, b = C.c_double(), C.c_int32()
+        self._chk(lib().sk_last_launch_ms(self._h, C.byref(a), C.byref(b)))
+        return dict(ms_sum=a.value, launches=b.value)
+
     def last_classes(self):
         """Kernel instantiations the last compute call launched: the DAG stem
         register classes (MAXK values; 0 = the big-y kernel, dag_stem_big.hip)
