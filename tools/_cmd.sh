@@ -1,4 +1,5 @@
 set -o pipefail
 export TMPDIR=/tmp
-bash tools/gpu_bench.sh ns r02f_ns --no-tests || exit 1
-bash tools/gpu_bench.sh c3 r02f_c3 --no-tests || exit 1
+bash tools/gpu_bench.sh c5 r02f_c5 --no-tests || exit 1
+bash tools/gpu_bench.sh c2 r02f_c2 --no-tests || exit 1
+bash tools/gpu_bench.sh c4 r02f_c4 --no-tests || exit 1
