@@ -3,9 +3,10 @@ x loop rows with one bp-frequency entry and no gap column are not swept per
 pair, their G0 rows come from the y's Gamma table; stem rows whose children
 are all such rows are combinations of the y's Phi and Gamma rows.  The
 schedules with both (default), without phi rows (SK_NO_PHI), without
-either (SK_NO_GAMMA) and with every read row stored (SK_STORE_ALL: by
-default a row read only by the next one stays in registers; all three read
-when a dataset is packed) agree to rounding,
+either (SK_NO_GAMMA), with every read row stored (SK_STORE_ALL: by default a
+row read only by the next one stays in registers) and in the reference
+numbering (SK_REF_ORDER: by default a depth-first order; all four read when a
+dataset is packed) agree to rounding,
 and all match the oracle, on inputs that mix the cases: single sequences,
 gapless alignments (several bp-frequency entries per node: the general
 seeds), gapped alignments (no Gamma / Phi for that y), length bands and
@@ -30,7 +31,7 @@ def _inputs(seed):
 
 
 def _gram(ctx, items, kern, switch=None):
-    saved = {k: os.environ.pop(k, None) for k in ("SK_NO_GAMMA", "SK_NO_PHI", "SK_STORE_ALL")}
+    saved = {k: os.environ.pop(k, None) for k in ("SK_NO_GAMMA", "SK_NO_PHI", "SK_STORE_ALL", "SK_REF_ORDER")}
     try:
         if switch:
             os.environ[switch] = "1"
@@ -51,7 +52,11 @@ def test_gamma_on_off_and_oracle(gpu_ctx, band):
     no_phi, _ = _gram(gpu_ctx, items, kern, "SK_NO_PHI")
     off, _ = _gram(gpu_ctx, items, kern, "SK_NO_GAMMA")
     stored, _ = _gram(gpu_ctx, items, kern, "SK_STORE_ALL")
+    ref_order, _ = _gram(gpu_ctx, items, kern, "SK_REF_ORDER")
     assert rel_err(on, off) < 1e-12 and rel_err(no_phi, off) < 1e-12 and rel_err(on, stored) < 1e-14
+    assert rel_err(on, ref_order) < 1e-12
+    lm = gpu_ctx.last_launch_ms()
+    assert lm["launches"] >= 1 and lm["ms_sum"] > 0.0
     n = len(items)
     ref = np.array([[po.su_stem(om[i], om[j], 0.4, kern.params.beta, band) for j in range(n)]
                     for i in range(n)])

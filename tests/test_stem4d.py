@@ -250,3 +250,25 @@ def test_stem4d_alignment_constraints_long(gpu_ctx, band):
     y = np.array([1, 0, 2, 2, 4, 3, 3], np.int32)
     got = gpu_ctx.pairs(ds, kern, x, y)
     assert rel_err(got, _oracle(seqs, kern, list(zip(x, y)))) < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("band", [0, 5])
+def test_stem4d_stream_parts_identical(gpu_ctx, band, monkeypatch):
+    """A batch's pairs dealt to 1-4 parts whose span launches run on their own
+    streams (SK4_STREAMS): every value bit-identical (each pair's planes are
+    computed by the same waves in the same order whatever the part), and each
+    span launch timed by its own events (sk_last_launch_ms)."""
+    seqs = _seqs()
+    ds, _ = make_examples(seqs)
+    kern = ska.StemKernel4D(band=band)
+    base = None
+    for parts in (1, 2, 3, 4):
+        monkeypatch.setenv("SK4_STREAMS", str(parts))
+        got = gpu_ctx.gram(ds, kern)
+        lm = gpu_ctx.last_launch_ms()
+        assert lm["launches"] >= 1 and lm["ms_sum"] > 0.0
+        if base is None:
+            base = got
+        else:
+            assert np.array_equal(got, base)

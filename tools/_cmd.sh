@@ -1,5 +1,4 @@
 set -o pipefail
 export TMPDIR=/tmp
-bash tools/gpu_bench.sh c5 r02f_c5 --no-tests || exit 1
-bash tools/gpu_bench.sh c2 r02f_c2 --no-tests || exit 1
-bash tools/gpu_bench.sh c4 r02f_c4 --no-tests || exit 1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1 || { tail -30 gpurun_out/pt.log; exit 1; }
+tail -1 gpurun_out/pt.log
