@@ -417,6 +417,13 @@ def main():
                 "traffic_frac": (traffic / (tot_ms / n_launch * 1e-3) / (peak * 1e9)
                                  if traffic is not None and unit == "GB/s" and tot_ms > 0 else None),
                 "algorithmic_per_launch": alg / n_launch, "model": model,
+                # the same bytes over the plain average launch duration (what
+                # rocprof's kernel stats show), ignoring that launches overlap
+                "frac_per_launch": ach / peak * tot_ms / sum_ms if sum_ms > 0 else None,
+                "note": ("frac > 1: the kernel moves fewer bytes than the model counts "
+                         "(rows kept in registers / LDS); measured HBM traffic is traffic_frac "
+                         "of peak, so HBM no longer bounds it")
+                        if ach / peak > 1.0 else None,
             },
             "cpu_baseline": cpu,
             "parity": parity,
