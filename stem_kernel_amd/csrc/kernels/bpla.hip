@@ -366,9 +366,8 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
   double acc = 0.0;                      // sum of my row's M cells (exp) / max (SW)
 
   // cell (i, j) from d = (i-1, j-1), u = (i-1, j) and l = (i, j-1); c1: j == 1
-  auto cell = [&](double dM, double dX, double dY, double uM, double uX, double uY, bool c1,
-                  double& nM, double& nX, double& nY) __attribute__((always_inline)) {
-    const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+  auto cell = [&](const BplaPos& yc, double dM, double dX, double dY, double uM, double uX, double uY,
+                  bool c1, double& nM, double& nX, double& nY) __attribute__((always_inline)) {
     double s = xr.v[0] * yc.v[0];
     s = __builtin_fma(xr.v[1], yc.v[1], s);
     s = __builtin_fma(xr.v[2], yc.v[2], s);
@@ -394,14 +393,43 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
   };
 
   // step of an interior: lane 0's column jb (uniform); every lane active
+  // (SK_BPLA_PF: this step's y column and boundary values were loaded a step
+  // earlier, the next step's are loaded here, so the LDS latency overlaps the
+  // cell's arithmetic; the last step's loads land past the row, never used)
+#ifdef SK_BPLA_PF
+  BplaPos ycp;
+  double bp0 = 0.0, bp1 = 0.0, bp2 = 0.0;
+  auto interior_load = [&](int jb) __attribute__((always_inline)) {
+    ycp = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+    const double* bj = bnd + 3 * jb;
+    bp0 = bj[0];
+    bp1 = bj[1];
+    bp2 = bj[2];
+  };
+#endif
   auto interior = [&](int jb, double& dM, double& dX, double& dY, double& uM, double& uX,
                       double& uY) __attribute__((always_inline)) {
+#ifdef SK_BPLA_PF
+    const BplaPos yc = ycp;
+    uM = wave_shr1(lM, bp0);
+    uX = wave_shr1(lX, bp1);
+    uY = wave_shr1(lY, bp2);
+    {
+      ycp = *reinterpret_cast<const BplaPos*>(ybase + yofs + (unsigned)sizeof(BplaPos));
+      const double* bj = bnd + 3 * (jb + 1);
+      bp0 = bj[0];
+      bp1 = bj[1];
+      bp2 = bj[2];
+    }
+#else
+    const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
     const double* bj = bnd + 3 * jb;
     uM = wave_shr1(lM, bj[0]);
     uX = wave_shr1(lX, bj[1]);
     uY = wave_shr1(lY, bj[2]);
+#endif
     double nM, nX, nY;
-    cell(dM, dX, dY, uM, uX, uY, false, nM, nX, nY);
+    cell(yc, dM, dX, dY, uM, uX, uY, false, nM, nX, nY);
     lM = nM;
     lX = nX;
     lY = nY;
@@ -446,8 +474,9 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
     uX = wave_shr1(lX, bj[1]);
     uY = wave_shr1(lY, bj[2]);
     if (on) {
+      const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
       double nM, nX, nY;
-      cell(dM, dX, dY, uM, uX, uY, wrap, nM, nX, nY);
+      cell(yc, dM, dX, dY, uM, uX, uY, wrap, nM, nX, nY);
       lM = nM;
       lX = nX;
       lY = nY;
@@ -485,6 +514,9 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
     }
     const int tend = s < nstrips ? min(Ws + Lys, T) : 0;
     int t = Ws + 64;
+#ifdef SK_BPLA_PF
+    if (t < tend) interior_load(t - Ws + 1);
+#endif
     for (; t + 1 < tend; t += 2) {
       interior(t - Ws + 1, aM, aX, aY, bM, bX, bY);
       interior(t - Ws + 2, bM, bX, bY, aM, aX, aY);
@@ -549,8 +581,15 @@ __global__ void __launch_bounds__(256) sk_bpla_fast_kernel(BplaLaunch P) {
 // the item's pairs (P.chunk at a time) from an LDS counter.  Per wave only
 // the boundary row (24 B per column) and the chunk table, so 16 waves fit a
 // CU.
+// SK_BPLA_WPE (build-time): ask the register allocator for that many waves
+// per SIMD (96 VGPRs give 5)
+#ifdef SK_BPLA_WPE
+#define SK_BPLA_ITEMS_ATTR __attribute__((amdgpu_waves_per_eu(SK_BPLA_WPE)))
+#else
+#define SK_BPLA_ITEMS_ATTR
+#endif
 template <bool SW, bool BP>
-__global__ void __launch_bounds__(512) sk_bpla_fast_items_kernel(BplaLaunch P) {
+__global__ void __launch_bounds__(1024) SK_BPLA_ITEMS_ATTR sk_bpla_fast_items_kernel(BplaLaunch P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -563,7 +602,9 @@ __global__ void __launch_bounds__(512) sk_bpla_fast_items_kernel(BplaLaunch P) {
   double* bnd = reinterpret_cast<double*>(wb);
   int4* ci = reinterpret_cast<int4*>(bnd + 3 * (maxlen + 2));
   double* ksum = reinterpret_cast<double*>(ci + kBplaChunkMax);
-  const int chunk = SW ? 1 : __builtin_amdgcn_readfirstlane(min(max(P.chunk, 1), kBplaChunkMax));
+  // P.chunk = 0: per item, the fewest pairs per chunk that give every wave
+  // one chunk (the workgroup waits for its slowest wave at the item's end)
+  const int nw = (int)(blockDim.x >> 6);
   fill_exp_table(etab);
   for (;;) {
     if (threadIdx.x == 0) {
@@ -581,6 +622,9 @@ __global__ void __launch_bounds__(512) sk_bpla_fast_items_kernel(BplaLaunch P) {
     const int ypb = P.yset.ex_pos_base[y];
     for (int j = threadIdx.x; j < Ly; j += blockDim.x) ycol[j] = P.ytab[ypb + j];
     __syncthreads();
+    const int chunk = SW ? 1
+                         : __builtin_amdgcn_readfirstlane(
+                               min(max(P.chunk > 0 ? P.chunk : (item.y + nw - 1) / nw, 1), kBplaChunkMax));
     // the wave's next chunk of the item: lane 0 draws, through an SGPR
     auto next_k = [&]() {
       int v = 0;

@@ -1184,17 +1184,28 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
     F.lds_max_len = (std::max(PY.max_len, 64) + 1) & ~1;
     int w, per_cu;
     int64_t units;
-    if (d_items) {  // y-grouped: 8-wave workgroups sharing the y columns
+    if (d_items) {  // y-grouped: workgroups of up to 16 waves sharing the y columns
       F.items = d_items;
       F.n_items = (int32_t)items.size();
       // pairs a wave streams back to back (SK_BPLA_CHUNK: 1..kBplaChunkMax)
+      // (0: per item, as many as give each wave one chunk)
       F.chunk = 4;
       if (const char* e = std::getenv("SK_BPLA_CHUNK")) F.chunk = std::atoi(e);
-      F.chunk = std::min(std::max(F.chunk, 1), sk::kBplaChunkMax);
-      w = kItemWaves;
+      F.chunk = std::min(std::max(F.chunk, 0), sk::kBplaChunkMax);
+      // waves per workgroup and workgroups per CU (SK_BPLA_IWAVES /
+      // SK_BPLA_IWG: geometry experiments; the VGPR budget caps the waves
+      // a SIMD holds, whatever is asked)
+      // Default: one 16-wave workgroup per CU (C4: 11.1 against 11.7 ms
+      // per launch for two 8-wave ones: the y columns staged once for 16
+      // waves), halved while its LDS does not fit, the CU's 16 waves then
+      // made up by more workgroups.
+      static const int iw = std::getenv("SK_BPLA_IWAVES") ? std::atoi(std::getenv("SK_BPLA_IWAVES")) : 16;
+      static const int iwg = std::getenv("SK_BPLA_IWG") ? std::atoi(std::getenv("SK_BPLA_IWG")) : 0;
+      w = std::min(std::max(iw, 1), 16);
+      while (w > 1 && sk::bpla_items_lds_bytes(F.lds_max_len, w) > 163840) w /= 2;
       const size_t l = sk::bpla_items_lds_bytes(F.lds_max_len, w);
       if (l > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
-      per_cu = std::max(1, std::min<int>((int)(163840 / l), 2));
+      per_cu = std::max(1, std::min<int>((int)(163840 / l), iwg > 0 ? iwg : std::max(1, 16 / w)));
       units = F.n_items;
     } else {
       const size_t wl = sk::bpla_fast_wave_lds_bytes(F.lds_max_len);
