@@ -1,23 +1,26 @@
-"""rocprofv3 database (rocpd sqlite, the default output format) -> the
-kernel stats CSV that `rocprofv3 --stats --output-format csv` writes
-(Name, Calls, TotalDurationNs, AverageNs, Percentage).
-
-    python tools/rocpd_stats.py gpurun_out/prof_c4/c4_results.db profiles/x_kernel_stats.csv
-"""
-import csv
+"""Kernel statistics (rocprofv3 --stats CSV columns) from a rocprofv3 rocpd
+SQLite output (a run made without --output-format csv)."""
+import math
 import sqlite3
 import sys
 
 
 def main(db, out):
     c = sqlite3.connect(db)
-    rows = list(c.execute("select name, total_calls, total_duration, average, percentage "
-                          "from top_kernels order by total_duration desc"))
-    with open(out, "w", newline="") as f:
-        w = csv.writer(f, quoting=csv.QUOTE_ALL)
-        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
-        for name, calls, tot_us, avg_us, pct in rows:  # the view reports microseconds
-            w.writerow([name, calls, round(tot_us * 1e3), f"{avg_us * 1e3:.3f}", f"{pct:.4f}"])
+    t = {r[0].split("_0")[0]: r[0] for r in c.execute("select name from sqlite_master where type='table'")}
+    rows = c.execute(f"select s.display_name, d.end - d.start from {t['rocpd_kernel_dispatch']} d "
+                     f"join {t['rocpd_info_kernel_symbol']} s on d.kernel_id = s.id").fetchall()
+    agg = {}
+    for name, dur in rows:
+        agg.setdefault(name, []).append(dur)
+    tot = sum(sum(v) for v in agg.values())
+    with open(out, "w") as f:
+        f.write('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n')
+        for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+            n, s = len(v), sum(v)
+            avg = s / n
+            sd = math.sqrt(sum((x - avg) ** 2 for x in v) / n)
+            f.write(f'"{name}",{n},{s},{avg:.6f},{100.0 * s / tot:.2f},{min(v)},{max(v)},{sd:.6f}\n')
 
 
 if __name__ == "__main__":
