@@ -382,7 +382,10 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
       nM = fast_exp(beta * s, etab, P.ec) * __builtin_fma(fb, dX + dY + dM, 1.0);
       nX = cbg * uM + cbe * uX;
       nY = c1 ? 0.0 : bg * (lM + lX) + be * lY;  // column 0 is zero
-      acc += row_ok ? nM : 0.0;
+      // every lane sums its cells; a row that does not exist (past the
+      // chunk's last row, never an input of a real one) is dropped at its
+      // hand-off, so no per-cell select
+      acc += nM;
     } else {
       nM = fmax(fmax(fmax(0.0, fb * dM), fb * dX), fb * dY) + s;
       nX = fmax(fb * uM + gap, fb * uX + ext);
