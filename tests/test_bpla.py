@@ -155,3 +155,29 @@ def test_bpla_chunks_of_long_rows(gpu_ctx):
     ref = {(a, b): po.kernel_value(kern.params.kind, om[a], om[b], kern.params)
            for a in range(n) for b in (0, 4)}
     assert rel_err(got, [ref[p] for p in zip(x.tolist(), y.tolist())]) < TOL
+
+
+@pytest.mark.gpu
+def test_bpla_items_workgroup_halved_for_long_rows(gpu_ctx):
+    """y-grouped items of long rows: a 16-wave workgroup's LDS (y columns +
+    a boundary row per wave) no longer fits a CU, so the engine halves it
+    (L = 420: 8 waves; L = 700: 4 waves).  SW modes against the oracle at
+    both lengths; the exp sums overflow to inf past a few hundred columns
+    as in the reference, so exp mode is compared where it is finite (the
+    L = 420 pairs, beta = 0.005) and must be inf where the oracle is."""
+    seqs = ska.random_sequences(2, 700, 0x5EED0043) + ska.random_sequences(2, 420, 0x5EED0053)
+    ds, om = make_examples(seqs)
+    n = len(seqs)
+    x = np.tile(np.arange(n, dtype=np.int32), 40)
+    for ycols, kern in (((0, 2), ska.BPLAKernel(SW=True)),
+                        ((0, 3), ska.BPLAKernel(SW=True, noBP=True)),
+                        ((2, 3), ska.BPLAKernel(beta=0.005))):
+        y = np.repeat(np.array(ycols, np.int32), x.size // 2)
+        got = gpu_ctx.pairs(ds, kern, x, y)
+        ref = {(a, b): po.kernel_value(kern.params.kind, om[a], om[b], kern.params)
+               for a in range(n) for b in ycols}
+        want = np.array([ref[p] for p in zip(x.tolist(), y.tolist())])
+        fin = np.isfinite(want)
+        assert fin.sum() >= x.size // 4
+        assert np.array_equal(np.isinf(got), np.isinf(want))
+        assert rel_err(got[fin], want[fin]) < TOL
