@@ -653,9 +653,26 @@ __global__ void __launch_bounds__(1024) SK_BPLA_ITEMS_ATTR sk_bpla_fast_items_ke
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       bpla_fast_chunk<SW, BP>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
+      double kv = lane < np ? ksum[lane] : 0.0;
+      // A pair whose sums overflow to inf (long rows, as in the reference)
+      // poisons the pairs after it in the chunk: their first row sees its
+      // last row through the fb = 0 coefficients, and 0 * inf = NaN.  Such a
+      // chunk (rare: never on finite sums) is redone one pair at a time.
+      if (!SW && np > 1 && __builtin_amdgcn_ballot_w64(lane < np && !__builtin_isfinite(kv)) != 0) {
+        for (int q = 0; q < np; ++q) {
+          const int lq = __shfl(len, q, 64), bq = __shfl(pb, q, 64);
+          if (lane == 0) ci[0] = make_int4(bq, lq, 0, 0);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          bpla_fast_chunk<SW, BP>(P, 1, ci, ksum, Ly, ycol, bnd, etab, lane);
+          const double v = ksum[0];
+          if (lane == q) kv = v;
+        }
+      }
       if (lane < np) {
         const int64_t pr = (int64_t)item.x + k + lane;
-        P.out[P.oidx ? P.oidx[pr] : pr] = SW ? ksum[lane] : 1.0 + ksum[lane];
+        P.out[P.oidx ? P.oidx[pr] : pr] = SW ? kv : 1.0 + kv;
       }
     }
     __syncthreads();
