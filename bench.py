@@ -32,6 +32,14 @@ c3 4-D stem kernel 1024 x L200, c4 BPLA 2048 alignments L~200, c5 DAG stem
 
 Timed region: inputs (packed examples) already resident in HBM; each step =
 the kernel launches for the slice + the all-gather.
+
+Ranks: under torchrun (RANK set) each process is one rank; ``--gpus N``
+without a launcher starts its own N worker processes (spawn_ranks) before any
+GPU call, so ``python3 bench.py --gpus 8`` runs as-is.
+
+Roofline: see roofline() -- measured HBM bytes (profiles/<kind>_traffic.json,
+stamped with the kernel source hash; stale profiles are not used) over the
+launches' span for the HBM-bound kernels, the survey model beside it.
 """
 from __future__ import annotations
 
@@ -71,7 +79,10 @@ def parse():
     ap.add_argument("--full", action="store_true", help="time every slice (whole Gram)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-pairs", type=int, default=None, help="pairs in the CPU sample")
-    ap.add_argument("--pmc-json", default=None)
+    ap.add_argument("--pmc-json", default=None, help="traffic profile (default profiles/<kind>_traffic.json)")
+    ap.add_argument("--cpu-stub", default=None, metavar="MODULE:FUNC",
+                    help="test harness: FUNC(data, params, x, y) compute + gloo all-gather instead of "
+                         "the GPU (no measurement)")
     return ap.parse_args()
 
 
@@ -130,20 +141,100 @@ def stem4d_cells(lens, x, y):
     return float(np.sum((n + 1) * (n + 2) / 2 * (m + 1) * (m + 2) / 2))
 
 
-def roofline(kind, shapes, x, y, ms):
-    """(bound, achieved, unit, peak, model, algorithmic work of the launches)."""
+def algorithmic(kind, shapes, x, y):
+    """(bound, unit, peak, model description, algorithmic work of the pairs)."""
     lens = shapes[:, 4]
     if kind in ("ss", "stem"):
-        b = dag_bytes(shapes, x, y)
-        return "hbm", b / (ms * 1e-3) / 1e9, "GB/s", PEAK_HBM_GBS, \
-            "SURVEY §8d: 32*|Vx|*|Vy| + S(x) + S(y) + 8 bytes per pair", b
+        return "hbm", "GB/s", PEAK_HBM_GBS, \
+            "SURVEY §8d: 32*|Vx|*|Vy| + S(x) + S(y) + 8 bytes per pair", dag_bytes(shapes, x, y)
     if kind == "stem4d":
-        b = 72.0 * stem4d_cells(lens, x, y)
-        return "hbm", b / (ms * 1e-3) / 1e9, "GB/s", PEAK_HBM_GBS, \
-            "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", b
-    f = 24.0 * float(np.sum(lens[x].astype(np.float64) * lens[y]))
-    return "valu", f / (ms * 1e-3) / 1e12, "TFLOP/s", PEAK_FP64_TFS, \
-        "SURVEY §8d: 24 flop per cell (exp counted as 1), Lx*Ly cells", f
+        return "hbm", "GB/s", PEAK_HBM_GBS, \
+            "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
+            72.0 * stem4d_cells(lens, x, y)
+    return "valu", "TFLOP/s", PEAK_FP64_TFS, \
+        "SURVEY §8d: 24 flop per cell (exp counted as 1), Lx*Ly cells", \
+        24.0 * float(np.sum(lens[x].astype(np.float64) * lens[y]))
+
+
+def load_profile(kind, length, path=None):
+    """profiles/<kind>_traffic.json (tools/measure.sh -> tools/profile_summary.py)
+    and whether it was measured on these kernel sources (provenance hash)."""
+    from stem_kernel_amd import provenance
+    path = path or os.path.join(ROOT, "profiles", f"{kind}_traffic.json")
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, None, path
+    if pm.get("kernel") != kind or pm.get("length") != length:
+        return None, None, path
+    return pm, pm.get("source_hash") == provenance.source_hash(), path
+
+
+def roofline(kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, cells, pmc_json=None):
+    """The dominant kernel's roofline.
+
+    HBM-bound kernels (DAG stem, 4-D stem): the headline `achieved` is the
+    MEASURED HBM bytes per launch (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, per
+    cell, scaled to this run's cells) over the launches' span per launch (the
+    launches run on several streams and overlap: span / launches), so `frac`
+    cannot pass 1.  The survey's algorithmic bytes give `model_frac` (same
+    time base) and `model_frac_per_launch` (over the average launch duration,
+    no overlap credit).  A profile measured on other kernel sources is
+    `stale`: then `traffic` is null and `frac` falls back to the model per
+    launch (`basis` says which).  FP64 kernels (BPLA): algorithmic flops per
+    launch over the average launch duration."""
+    bound, unit, peak, model, alg = algorithmic(kind, shapes, xs, ys)
+    n_launch = max(1, n_launch)
+    avg_s = sum_ms / n_launch * 1e-3
+    eff_s = span_ms / n_launch * 1e-3
+    alg_pl = alg / n_launch
+    scale = 1e9 if unit == "GB/s" else 1e12
+    pm, fresh, path = load_profile(kind, length, pmc_json)
+    rel = os.path.relpath(path, ROOT)
+    traffic = None
+    if pm is not None and pm.get("hbm_bytes_per_cell"):
+        traffic = pm["hbm_bytes_per_cell"] * float(np.sum(cells)) / n_launch
+    r = {"bound": bound, "peak": peak, "unit": unit, "kernel": None,
+         "kernel_ms_per_launch": avg_s * 1e3, "launches": n_launch,
+         "overlap": sum_ms / span_ms if span_ms > 0 else None,
+         "effective_ms_per_launch": eff_s * 1e3,
+         "algorithmic_per_launch": alg_pl, "model": model,
+         "profile": rel if pm is not None else None,
+         "profile_source_hash": pm.get("source_hash") if pm else None,
+         "profile_git_head": pm.get("git_head") if pm else None,
+         "stale": (not fresh) if pm is not None else None}
+    if bound == "hbm":
+        r["model_frac"] = alg_pl / eff_s / scale / peak if eff_s > 0 else None
+        r["model_frac_per_launch"] = alg_pl / avg_s / scale / peak if avg_s > 0 else None
+        if traffic is not None and fresh and eff_s > 0:
+            r["achieved"] = traffic / eff_s / scale
+            r["basis"] = ("measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, " + rel +
+                          ") / (launches' span / launches)")
+            r["traffic"] = traffic
+        else:
+            r["achieved"] = alg_pl / avg_s / scale if avg_s > 0 else 0.0
+            r["basis"] = ("survey model bytes per launch / average launch duration (no fresh "
+                          "measured traffic: " + ("stale profile" if pm is not None else "no profile") + ")")
+            r["traffic"] = None
+            if traffic is not None:
+                r["traffic_stale_value"] = traffic
+        r["traffic_per_cell"] = pm.get("hbm_bytes_per_cell") if pm else None
+        r["algorithmic_per_cell"] = alg / float(np.sum(cells)) if np.sum(cells) else None
+    else:
+        r["achieved"] = alg_pl / avg_s / scale if avg_s > 0 else 0.0
+        r["basis"] = "algorithmic flops per launch / average launch duration"
+        r["traffic"] = traffic if fresh else None
+    r["frac"] = r["achieved"] / peak
+    lds = (pm or {}).get("lds")
+    if lds:
+        r["issue"] = {"fresh": bool(fresh), "lds_busy_frac": lds.get("lds_busy_frac"),
+                      "lds_bank_conflict_share": lds.get("bank_conflict_share"),
+                      "valu_per_cell": lds.get("valu_per_cell"),
+                      "salu_per_cell": lds.get("salu_per_cell"),
+                      "lds_insts_per_cell": lds.get("lds_insts_per_cell"),
+                      "source": rel + " (rocprofv3 --pmc SQ_LDS_IDX_ACTIVE ... GRBM_GUI_ACTIVE pass)"}
+    return r
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -205,9 +296,230 @@ def cpu_baseline(cfg, data, n_pairs, seed=7):
                       f"may use: affinity capped by OMP_NUM_THREADS), {dt:.1f}s wall"}, pairs, vals
 
 
+# ------------------------------------------------------------------ ranks
+def spawn_ranks(a):
+    """`--gpus N` started without a launcher (RANK unset): start N fresh
+    worker processes of this script -- before this process makes any GPU call
+    -- with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+    MASTER_PORT set, one GPU each, and exit with the first failing rank's
+    status (the others are then stopped: a rank that died leaves its peers
+    waiting in a collective).  The reference's MPI Gram is launched by mpirun
+    the same way (common/kernel_matrix.cpp:495-527)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in live:
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+    return rc
+
+
+class GpuEngine:
+    """The product path: one GPU per rank, the engine's C ABI, its own RCCL
+    communicator (sk_comm_init; torch.distributed only carries the 128-byte id
+    from rank 0)."""
+
+    def __init__(self, a, cfg, rank, world, local):
+        import torch
+        import torch.distributed as dist
+
+        import stem_kernel_amd as ska
+        from stem_kernel_amd import shard
+        self.torch, self.dist, self.ska, self.a = torch, dist, ska, a
+        self.dist_on = world > 1
+        if self.dist_on:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", rank=rank, world_size=world)
+        self.dev = torch.device("cuda", local)
+        t0 = time.perf_counter()
+        self.data, self.ds = build_inputs(cfg, a)
+        self.t_build = time.perf_counter() - t0
+        stream = torch.cuda.current_stream(self.dev)
+        self.ctx = ska.Context(local, stream=stream.cuda_stream)
+        t0 = time.perf_counter()
+        self.ctx.upload(self.ds)
+        torch.cuda.synchronize(self.dev)
+        self.t_upload = time.perf_counter() - t0
+        self.kern = make_kernel(cfg["kernel"])
+        if self.dist_on:
+            shard.rccl_init(self.ctx)
+        else:
+            import ctypes
+            uid = ctypes.create_string_buffer(128)
+            ska.lib().sk_comm_unique_id(uid, 128)
+            self.ctx.comm_init(uid.raw, 0, 1)
+        self.world, self.rank = world, rank
+
+    def alloc(self, per):
+        t = self.torch
+        self.per = per
+        self.out = t.zeros(per, dtype=t.float64, device=self.dev)
+        self.gathered = t.empty(per * self.world, dtype=t.float64, device=self.dev)
+
+    def step(self, x, y):
+        self.ctx.pairs_device(self.ds, self.kern, x, y, self.out.data_ptr())
+        tm = dict(self.ctx.last_timing(), **self.ctx.last_launch_ms())
+        self.ctx.allgather(self.out.data_ptr(), self.per, self.gathered.data_ptr())
+        return tm
+
+    def full(self):
+        self.ctx.gram_sharded(self.ds, self.kern, normalize=False)
+        return dict(self.ctx.last_timing(), **self.ctx.last_launch_ms())
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def barrier(self):
+        if self.dist_on:
+            self.dist.barrier()
+
+    def reduce_max_sum(self, elapsed, pairs):
+        t = self.torch.tensor([elapsed, float(pairs)], dtype=self.torch.float64, device=self.dev)
+        mx, sm = t.clone(), t.clone()
+        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(sm, op=self.dist.ReduceOp.SUM)
+        return float(mx[0]), float(sm[1])
+
+    def close(self):
+        if self.dist_on:
+            self.dist.destroy_process_group()
+
+
+class CpuStubEngine(GpuEngine):
+    """--cpu-stub MODULE:FUNC -- the same ranks, plan, timing and JSON line
+    with the GPU compute replaced by FUNC(data, kernel_params, x, y) -> values
+    (a test supplies it, e.g. tests/bench_stub.py over the C oracle) and the
+    all-gather by torch.distributed over gloo: exercises the N-rank bench path
+    on a machine without a GPU.  After the timed steps the last step's
+    gathered buffers are checked slice by slice against FUNC on every rank's
+    cells.  Not a measurement (no roofline, no CPU baseline)."""
+
+    def __init__(self, a, cfg, rank, world, local):
+        import importlib
+
+        import torch
+        import torch.distributed as dist
+
+        import stem_kernel_amd as ska
+        mod, fn = a.cpu_stub.split(":")
+        self.compute = getattr(importlib.import_module(mod), fn)
+        self.torch, self.dist, self.ska, self.a = torch, dist, ska, a
+        self.dist_on = world > 1
+        if self.dist_on:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        t0 = time.perf_counter()
+        self.data, self.ds = build_inputs(cfg, a)
+        self.t_build = time.perf_counter() - t0
+        self.t_upload = 0.0
+        self.kern = make_kernel(cfg["kernel"])
+        self.world, self.rank = world, rank
+        self.checked = 0
+
+    def values(self, x, y):
+        return np.asarray(self.compute(self.data, self.kern.params, x, y), dtype=np.float64)
+
+    def alloc(self, per):
+        self.per = per
+
+    def step(self, x, y):
+        t = self.torch
+        buf = t.zeros(self.per, dtype=t.float64)
+        buf[: x.size] = t.from_numpy(self.values(x, y))
+        parts = [t.empty(self.per, dtype=t.float64) for _ in range(self.world)]
+        if self.dist_on:
+            self.dist.all_gather(parts, buf)
+        else:
+            parts[0].copy_(buf)
+        self.last = parts
+        return {"stem_ms": 1e-3, "ms_sum": 1e-3, "launches": 1, "cells": float(x.size)}
+
+    def verify(self, slice_of_rank):
+        """Every rank's gathered slice of the last step equals FUNC on it."""
+        for r in range(self.world):
+            rx, ry = slice_of_rank(r)
+            if not np.array_equal(self.last[r][: rx.size].numpy(), self.values(rx, ry)):
+                raise AssertionError(f"cpu stub: rank {r}'s gathered slice differs")
+            self.checked += rx.size
+
+    def full(self):
+        raise SystemExit("--full is the GPU product path (sk_gram_sharded)")
+
+    def sync(self):
+        pass
+
+    def reduce_max_sum(self, elapsed, pairs):
+        t = self.torch.tensor([elapsed, float(pairs)], dtype=self.torch.float64)
+        mx, sm = t.clone(), t.clone()
+        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(sm, op=self.dist.ReduceOp.SUM)
+        return float(mx[0]), float(sm[1])
+
+
+# ------------------------------------------------------------------ plan
+def make_plan(kind, n, world, rank, S):
+    """Step slices of the shipped cyclic plan (cells k % world == rank).
+    Returns (slice_of(step, rank) -> (x, y), per: buffer size, description)."""
+    iu, ju = np.triu_indices(n)
+    iu = iu.astype(np.int32)
+    ju = ju.astype(np.int32)
+    G = S // world
+    kcell = np.arange(iu.size, dtype=np.int64)
+    if kind in ("ss", "stem") and G <= n // 2:
+        # folded column pairs (j, n-1-j) dealt round-robin to G column groups
+        colg = np.empty(n, np.int64)
+        for p in range(n // 2):
+            colg[p] = colg[n - 1 - p] = p % G
+        if n % 2:
+            colg[n // 2] = (n // 2) % G
+        cell_g = colg[ju]
+        groups = {}
+
+        def slice_of(t, r=rank):
+            g = t % G
+            if g not in groups:
+                groups[g] = np.flatnonzero(cell_g == g)
+            sel = groups[g]
+            sel = sel[kcell[sel] % world == r]
+            return iu[sel], ju[sel]
+        # exact buffer size: the largest (group, rank) share
+        per = int(np.bincount(cell_g * world + kcell % world, minlength=G * world).max())
+        desc = f"column group (step mod {G}) of {G} folded-pair groups, cells k % {world} == rank"
+    else:
+        def slice_of(t, r=rank):
+            s = (t * world + r) % S
+            return iu[s::S], ju[s::S]
+        per = int(np.ceil(iu.size / S))
+        desc = f"cells k % {S} == step*{world} + rank"
+    return slice_of, max(per, 1), desc, iu.size
+
+
 # ------------------------------------------------------------------ main
 def main():
     a = parse()
+    if a.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(a))
     cfg = CONFIGS[a.config]
     a.n = a.n or cfg["n"]
     if a.length is None:
@@ -218,97 +530,31 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    import torch
-    import torch.distributed as dist
-    import stem_kernel_amd as ska
+    eng = (CpuStubEngine if a.cpu_stub else GpuEngine)(a, cfg, rank, world, local)
+    shapes = np.array([eng.ds.shape(i) for i in range(a.n)], dtype=np.float64)
 
-    dist_on = world > 1
-    if dist_on:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    dev = torch.device("cuda", local)
-
-    # ---- inputs (identical on every rank), built on host threads
-    t0 = time.perf_counter()
-    data, ds = build_inputs(cfg, a)
-    t_build = time.perf_counter() - t0
-    stream = torch.cuda.current_stream(dev)
-    ctx = ska.Context(local, stream=stream.cuda_stream)
-    t0 = time.perf_counter()
-    ctx.upload(ds)
-    torch.cuda.synchronize(dev)
-    t_upload = time.perf_counter() - t0
-    shapes = np.array([ds.shape(i) for i in range(a.n)], dtype=np.float64)
-    kern = make_kernel(kind)
-
-    iu, ju = np.triu_indices(a.n)
-    iu = iu.astype(np.int32)
-    ju = ju.astype(np.int32)
-    # the engine's own RCCL communicator (sk_comm_init; torch only carries
-    # the 128-byte id from rank 0)
-    from stem_kernel_amd import shard
-    if dist_on:
-        shard.rccl_init(ctx)
-    else:
-        import ctypes
-        uid = ctypes.create_string_buffer(128)
-        ska.lib().sk_comm_unique_id(uid, 128)
-        ctx.comm_init(uid.raw, 0, 1)
     S = a.slices
     if a.full:
         a.steps, a.warmup = 1, 0
-    n_slices_needed = (a.warmup + a.steps) * world
-    S = max(S, n_slices_needed)
+    S = max(S, (a.warmup + a.steps) * world)
     S = -(-S // world) * world  # a multiple of N: rank r's slices are cells k % N == r
-    G = S // world
-    if kind in ("ss", "stem") and G <= a.n // 2:
-        # folded column pairs dealt round-robin to G column groups
-        colg = np.empty(a.n, np.int64)
-        for p in range(a.n // 2):
-            colg[p] = colg[a.n - 1 - p] = p % G
-        if a.n % 2:
-            colg[a.n // 2] = (a.n // 2) % G
-        cell_g = colg[ju]
-        kcell = np.arange(iu.size, dtype=np.int64)
-        groups = {}
-
-        def slice_of_step(t):
-            g = t % G
-            if g not in groups:
-                groups[g] = np.flatnonzero(cell_g == g)
-            sel = groups[g]
-            sel = sel[kcell[sel] % world == rank]
-            return iu[sel], ju[sel]
-        per = max(int(np.count_nonzero(cell_g == g)) for g in range(G))
-        per = -(-per // world)
-        step_kind = f"column group (step mod {G}) of {G} folded-pair groups, cells k % {world} == rank"
-    else:
-        def slice_of_step(t):
-            s = (t * world + rank) % S
-            return iu[s::S], ju[s::S]
-        per = int(np.ceil(iu.size / S))
-        step_kind = f"cells k % {S} == step*{world} + rank"
-    out = torch.zeros(per, dtype=torch.float64, device=dev)
-    gathered = torch.empty(per * world, dtype=torch.float64, device=dev)
-    full_gram = [None]
+    slice_of, per, step_kind, n_cells = make_plan(kind, a.n, world, rank, S)
+    eng.alloc(per)
 
     def run_step(step):
         if a.full:  # the product path: sk_gram_sharded over all ranks
-            full_gram[0] = ctx.gram_sharded(ds, kern, normalize=False)
+            from stem_kernel_amd import shard
+            tm = eng.full()
             x, y = shard.rank_pairs(a.n, world, rank)
-            return x, y, dict(ctx.last_timing(), **ctx.last_launch_ms())
-        x, y = slice_of_step(step)
-        ctx.pairs_device(ds, kern, x, y, out.data_ptr())
-        tm = dict(ctx.last_timing(), **ctx.last_launch_ms())
-        ctx.allgather(out.data_ptr(), per, gathered.data_ptr())
-        return x, y, tm
+            return x, y, tm
+        x, y = slice_of(step)
+        return x, y, eng.step(x, y)
 
     for w in range(a.warmup):
         run_step(w)
-    torch.cuda.synchronize(dev)
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    eng.sync()
+    eng.barrier()
+    eng.sync()
     t0 = time.perf_counter()
     local_pairs = 0
     k_ms, work, cells, launches, l_ms = [], [], [], [], []
@@ -320,61 +566,42 @@ def main():
         launches.append(tm["launches"])
         l_ms.append(tm["ms_sum"])
         work.append((x, y))
-    torch.cuda.synchronize(dev)
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    eng.sync()
+    eng.barrier()
+    eng.sync()
     elapsed = time.perf_counter() - t0
-    if dist_on:
-        t = torch.tensor([elapsed, float(local_pairs)], dtype=torch.float64, device=dev)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0])
-        total_pairs = float(sm[1])
+    if eng.dist_on:
+        elapsed, total_pairs = eng.reduce_max_sum(elapsed, local_pairs)
     else:
         total_pairs = float(local_pairs)
+    if a.cpu_stub:
+        last = a.warmup + a.steps - 1
+        eng.verify(lambda r: slice_of(last, r))
 
     if rank == 0:
         value = total_pairs / elapsed
-        # dominant kernel (stem / 4-D / BPLA): each launch timed by HIP events
-        # around it on its own stream (sk_last_launch_ms) -- the average a
-        # kernel-trace profile reports.  Launches on several streams overlap
-        # (`overlap` of them on average), each then sharing the GPU, so the
-        # rate is taken over the launches' span (sk_last_timing): achieved =
-        # algorithmic bytes per launch / (average duration / overlap)
-        tot_ms = float(np.sum(k_ms))
-        sum_ms = float(np.sum(l_ms))
         xs = np.concatenate([w[0] for w in work])
         ys = np.concatenate([w[1] for w in work])
-        bound, ach, unit, peak, model, alg = roofline(kind, shapes, xs, ys, tot_ms)
-        n_launch = max(1, int(np.sum(launches)))
-        traffic, traffic_src = None, None
-        pmc_json = a.pmc_json or os.path.join(ROOT, "profiles", f"{kind}_traffic.json")
-        try:
-            with open(pmc_json) as f:
-                pm = json.load(f)
-            if pm.get("length") == a.length and pm.get("kernel") == kind:
-                traffic = pm["hbm_bytes_per_cell"] * float(np.sum(cells)) / n_launch
-                traffic_src = (f"not measured in this run: {os.path.relpath(pmc_json, ROOT)} "
-                               f"(rocprofv3 FETCH_SIZE/WRITE_SIZE passes, {pm.get('source', '?')}) "
-                               f"bytes per cell x this run's cells per launch")
-        except Exception:
-            pass
+        # dominant kernel (stem / 4-D / BPLA): each launch timed by HIP events
+        # around it on its own stream (sk_last_launch_ms), the launches' span
+        # by sk_last_timing
+        rf = None
+        if not a.cpu_stub:
+            rf = roofline(kind, a.length, shapes, xs, ys, float(np.sum(k_ms)), float(np.sum(l_ms)),
+                          int(np.sum(launches)), cells, a.pmc_json)
+            rf["kernel"] = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
+                            "stem4d": "sk_stem4d_kernel", "bpla": "sk_bpla_fast_kernel"}[kind]
         cpu, parity = None, None
-        if not a.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-            cpu, cpairs, cvals = cpu_baseline(cfg, data, a.cpu_pairs)
+        if not a.no_cpu_baseline and world == 1 and not a.cpu_stub:  # rank 0 at N=1 only
+            cpu, cpairs, cvals = cpu_baseline(cfg, eng.data, a.cpu_pairs)
             # the baseline's oracle values double as a parity check of the
             # benched kernel classes on the same inputs (1e-6 relative)
             cx = np.array([p[0] for p in cpairs], np.int32)
             cy = np.array([p[1] for p in cpairs], np.int32)
-            got = ctx.pairs(ds, kern, cx, cy)
+            got = eng.ctx.pairs(eng.ds, eng.kern, cx, cy)
             err = float(np.max(np.abs(got - cvals) / np.maximum(np.abs(cvals), 1e-300)))
             parity = {"pairs": int(cx.size), "max_rel_err": err, "tol": 1e-6,
                       "ok": bool(err < 1e-6), "against": "C oracle (cpu_baseline sample)"}
-        kname = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
-                 "stem4d": "sk_stem4d_kernel", "bpla": "sk_bpla_kernel"}[kind]
         kdesc = {
             "ss": "SuStemStrKernel(alpha=0.2,beta=0.3,loop_gap=0.2,gap=0.8,band=10)",
             "stem": "SuStemKernel(beta=0.3,loop_gap=0.2,band=10)",
@@ -394,11 +621,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (splitmix64 ACGU sequences, Nussinov-Boltzmann bpp stand-in for "
-                    "ViennaRNA; no checkpoints)",
+            "data": ("cpu stub (test compute + gloo all-gather; not a measurement)" if a.cpu_stub else
+                     "synthetic (splitmix64 ACGU sequences, Nussinov-Boltzmann bpp stand-in for "
+                     "ViennaRNA; no checkpoints)"),
             "config": {
                 "workload": f"{a.config}: {a.n}x{a.n} {kdesc} Gram, L={cfg['L']}, "
-                            f"step = 1/{S} of the {iu.size} upper-triangle pairs per GPU",
+                            f"step = 1/{S} of the {n_cells} upper-triangle pairs per GPU",
                 "step_cells": step_kind,
                 "n_sequences": a.n, "length": cfg["L"], "pairs_per_step_per_gpu": per,
                 "kernel": kdesc, "basepair_th": 0.01,
@@ -406,36 +634,21 @@ def main():
                                + (" -- full Gram via sk_gram_sharded" if a.full else ""),
                 "mean_nodes": float(shapes[:, 0].mean()), "mean_edges": float(shapes[:, 1].mean()),
                 "mean_bpfreq": float(shapes[:, 2].mean()),
-                "host_build_s": round(t_build, 2), "upload_s": round(t_upload, 3),
+                "host_build_s": round(eng.t_build, 2), "upload_s": round(eng.t_upload, 3),
             },
-            "roofline": {
-                "bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
-                "traffic": traffic, "traffic_source": traffic_src, "kernel": kname,
-                "kernel_ms_per_launch": sum_ms / n_launch, "launches": n_launch,
-                "overlap": sum_ms / tot_ms if tot_ms > 0 else None,
-                "effective_ms_per_launch": tot_ms / n_launch,
-                "traffic_frac": (traffic / (tot_ms / n_launch * 1e-3) / (peak * 1e9)
-                                 if traffic is not None and unit == "GB/s" and tot_ms > 0 else None),
-                "algorithmic_per_launch": alg / n_launch, "model": model,
-                # the same bytes over the plain average launch duration (what
-                # rocprof's kernel stats show), ignoring that launches overlap
-                "frac_per_launch": ach / peak * tot_ms / sum_ms if sum_ms > 0 else None,
-                "note": ("frac > 1: the kernel moves fewer bytes than the model counts "
-                         "(rows kept in registers / LDS); measured HBM traffic is traffic_frac "
-                         "of peak, so HBM no longer bounds it")
-                        if ach / peak > 1.0 else None,
-            },
+            "roofline": rf,
             "cpu_baseline": cpu,
             "parity": parity,
             "cells_per_step": float(np.mean(cells)),
         }
+        if a.cpu_stub:
+            line["stub_checked_pairs"] = eng.checked
         print(json.dumps(line), flush=True)
         if parity is not None and not parity["ok"]:
             print(f"PARITY FAILURE: max relative error {parity['max_rel_err']:.3g} > 1e-6",
                   file=sys.stderr, flush=True)
             sys.exit(3)
-    if dist_on:
-        dist.destroy_process_group()
+    eng.close()
 
 
 if __name__ == "__main__":

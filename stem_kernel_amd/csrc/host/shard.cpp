@@ -186,6 +186,28 @@ int sk_comm_allgather(sk_context* ctx, const double* send_dev, int64_t count, do
   return SK_OK;
 }
 
+// Every rank enters every collective whatever its own status: a local
+// failure (allocation, an unsupported example, a HIP error) is carried into
+// the all-gather as a zero buffer and then agreed on by a max all-reduce of
+// the ranks' status codes, so every rank returns an error instead of its
+// peers waiting in ncclAllGather forever.
+namespace {
+int agree_status(sk_context* ctx, int32_t* d_st, int rc) {
+  hipStream_t S = sk::ctx_stream(ctx);
+  int32_t h[2] = {-rc, 0};
+  ncclComm_t c = static_cast<ncclComm_t>(sk::ctx_comm(ctx));
+  if (hipMemcpyAsync(d_st, h, sizeof(int32_t), hipMemcpyHostToDevice, S) != hipSuccess ||
+      ncclAllReduce(d_st, d_st + 1, 1, ncclInt32, ncclMax, c, S) != ncclSuccess ||
+      hipMemcpyAsync(h + 1, d_st + 1, sizeof(int32_t), hipMemcpyDeviceToHost, S) != hipSuccess ||
+      hipStreamSynchronize(S) != hipSuccess)
+    return rc ? rc : sk::ctx_fail(ctx, SK_ERR_HIP, "sk_gram_sharded: status all-reduce");
+  if (rc) return rc;
+  if (h[1]) return sk::ctx_fail(ctx, -h[1], "sk_gram_sharded: another rank failed (status " +
+                                              std::to_string(-h[1]) + ")");
+  return SK_OK;
+}
+}  // namespace
+
 int sk_gram_sharded(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp, int normalize,
                     double* out) {
   if (!ctx || !ds || !kp || !out) return sk::ctx_fail(ctx, SK_ERR_INVALID, "null argument");
@@ -203,24 +225,43 @@ int sk_gram_sharded(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp,
   int rc = sk_shard_cells(n, rank, world, x.data(), y.data());
   if (rc) return sk::ctx_fail(ctx, rc, "sk_gram_sharded: plan");
   hipStream_t S = sk::ctx_stream(ctx);
+  int32_t* d_st = nullptr;
+  if (hipMalloc(&d_st, 2 * sizeof(int32_t)) != hipSuccess) {
+    // cannot take part in the status agreement: abort the communicator so
+    // the peers' collectives fail instead of waiting
+    (void)ncclCommAbort(static_cast<ncclComm_t>(c));
+    sk::ctx_comm(ctx) = nullptr;
+    return sk::ctx_fail(ctx, SK_ERR_ALLOC, "sk_gram_sharded: status word (communicator aborted)");
+  }
   double* d = nullptr;
-  if (hipMalloc(&d, (size_t)per * (world + 1) * sizeof(double)) != hipSuccess)
-    return sk::ctx_fail(ctx, SK_ERR_ALLOC, "sk_gram_sharded: device buffers");
-  double* d_mine = d;
-  double* d_all = d + per;
+  if (hipMalloc(&d, (size_t)per * (world + 1) * sizeof(double)) != hipSuccess) {
+    d = nullptr;
+    rc = sk::ctx_fail(ctx, SK_ERR_ALLOC, "sk_gram_sharded: device buffers");
+  }
+  rc = agree_status(ctx, d_st, rc);  // all ranks have their buffers (or all stop)
   std::vector<double> g;
-  rc = hipMemsetAsync(d_mine, 0, (size_t)per * sizeof(double), S) == hipSuccess ? SK_OK : SK_ERR_HIP;
-  if (rc == SK_OK && mine > 0) rc = sk_pairs_device(ctx, ds, kp, x.data(), y.data(), mine, d_mine);
-  if (rc == SK_OK) rc = sk_comm_allgather(ctx, d_mine, per, d_all);
   if (rc == SK_OK) {
-    g.resize((size_t)per * world);
-    if (hipMemcpyAsync(g.data(), d_all, g.size() * sizeof(double), hipMemcpyDeviceToHost, S) !=
-            hipSuccess ||
-        hipStreamSynchronize(S) != hipSuccess)
-      rc = sk::ctx_fail(ctx, SK_ERR_HIP, "sk_gram_sharded: gather copy");
+    double* d_mine = d;
+    double* d_all = d + per;
+    int lrc = hipMemsetAsync(d_mine, 0, (size_t)per * sizeof(double), S) == hipSuccess
+                  ? SK_OK
+                  : sk::ctx_fail(ctx, SK_ERR_HIP, "sk_gram_sharded: memset");
+    if (lrc == SK_OK && mine > 0) lrc = sk_pairs_device(ctx, ds, kp, x.data(), y.data(), mine, d_mine);
+    if (lrc != SK_OK) (void)hipMemsetAsync(d_mine, 0, (size_t)per * sizeof(double), S);
+    // the all-gather runs on every rank, failed or not
+    const int grc = sk_comm_allgather(ctx, d_mine, per, d_all);
+    rc = agree_status(ctx, d_st, lrc != SK_OK ? lrc : grc);
+    if (rc == SK_OK) {
+      g.resize((size_t)per * world);
+      if (hipMemcpyAsync(g.data(), d_all, g.size() * sizeof(double), hipMemcpyDeviceToHost, S) !=
+              hipSuccess ||
+          hipStreamSynchronize(S) != hipSuccess)
+        rc = sk::ctx_fail(ctx, SK_ERR_HIP, "sk_gram_sharded: gather copy");
+    }
   }
   (void)hipStreamSynchronize(S);
-  (void)hipFree(d);
+  if (d) (void)hipFree(d);
+  (void)hipFree(d_st);
   if (rc) return rc;
   return sk_shard_assemble(n, world, g.data(), per, normalize, out);
 }

@@ -84,8 +84,8 @@ __global__ void __launch_bounds__(256) sk_bpla_kernel(BplaLaunch P) {
   for (;;) {
     unsigned long long pr = 0;
     if (lane == 0) pr = atomicAdd(P.pair_counter, 1ull);
-    pr = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(pr >> 32)) << 32) |
-         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)pr);
+    pr = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(pr >> 32), 0) << 32) |
+         (unsigned)__builtin_amdgcn_readlane((unsigned)pr, 0);
     if ((int64_t)pr >= P.n_pairs) break;
     const int x = P.xs[pr], y = P.ys[pr];
     const int Lx = sx.ex_len[x], Ly = sy.ex_len[y];
@@ -561,8 +561,8 @@ __global__ void __launch_bounds__(256) sk_bpla_fast_kernel(BplaLaunch P) {
   auto next_pair = [&]() {
     unsigned long long v = 0;
     if (lane == 0) v = atomicAdd(P.pair_counter, 1ull);
-    return (int64_t)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
-                     (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v));
+    return (int64_t)(((unsigned long long)__builtin_amdgcn_readlane((unsigned)(v >> 32), 0) << 32) |
+                     (unsigned)__builtin_amdgcn_readlane((unsigned)v, 0));
   };
   for (int64_t pr = next_pair(); pr < P.n_pairs; pr = next_pair()) {
     const int x = __builtin_amdgcn_readfirstlane(P.xs[pr]);
@@ -632,7 +632,7 @@ __global__ void __launch_bounds__(1024) SK_BPLA_ITEMS_ATTR sk_bpla_fast_items_ke
     auto next_k = [&]() {
       int v = 0;
       if (lane == 0) v = atomicAdd(&sh[1], chunk);
-      return __builtin_amdgcn_readfirstlane(v);
+      return __builtin_amdgcn_readlane(v, 0);
     };
     for (int k = next_k(); k < item.y; k = next_k()) {
       const int np = min(chunk, item.y - k);

@@ -467,8 +467,8 @@ __global__ void __launch_bounds__(256) sk_bpla_grad_wave_kernel(BplaGradLaunch P
   auto next_pair = [&]() {
     unsigned long long v = 0;
     if (lane == 0) v = atomicAdd(P.pair_counter, 1ull);
-    return (int64_t)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
-                     (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v));
+    return (int64_t)(((unsigned long long)__builtin_amdgcn_readlane((unsigned)(v >> 32), 0) << 32) |
+                     (unsigned)__builtin_amdgcn_readlane((unsigned)v, 0));
   };
   for (int64_t pr = next_pair(); pr < P.n_pairs; pr = next_pair()) {
     const int x = __builtin_amdgcn_readfirstlane(P.xs[pr]);

@@ -1066,7 +1066,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
       int nt = 0;
       // generic-pointer atomic on the LDS counter
       if (lane == 0) nt = atomicAdd(reinterpret_cast<int*>(const_cast<int32_t*>((const int32_t*)ctl)) + 1, 1);
-      t = __builtin_amdgcn_readfirstlane(nt);
+      t = __builtin_amdgcn_readlane(nt, 0);
     }
   }
 }

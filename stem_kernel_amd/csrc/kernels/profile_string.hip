@@ -76,8 +76,8 @@ __global__ void __launch_bounds__(256) sk_profile_string_kernel(StrLaunch P) {
     unsigned long long pr = 0;
     if (lane == 0) pr = atomicAdd(P.pair_counter, 1ull);
     // broadcast lane 0's ticket through an SGPR (wave-uniform from here on)
-    pr = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(pr >> 32)) << 32) |
-         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)pr);
+    pr = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(pr >> 32), 0) << 32) |
+         (unsigned)__builtin_amdgcn_readlane((unsigned)pr, 0);
     if ((int64_t)pr >= P.n_pairs) break;
     const int x = P.xs[pr], y = P.ys[pr];
     const int Lx = sx.ex_len[x], Ly = sy.ex_len[y];

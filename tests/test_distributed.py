@@ -216,3 +216,69 @@ def test_gloo_world2_gradient_gram_matches_single_process():
     for rank in (0, 1):
         assert np.array_equal(res[rank][0], K) and np.array_equal(res[rank][1], G)
     assert np.allclose(np.diag(K), 1.0) and np.all(G[:, np.arange(n), np.arange(n)] == 0.0)
+
+
+def _bench(args, timeout=300):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, cwd=root, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints ONE line
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("config,n,length", [("ns", 10, 40), ("c4", 6, 30)])
+def test_bench_spawns_its_own_ranks(config, n, length):
+    """`bench.py --gpus 2` with no launcher starts two worker ranks itself
+    (gloo here, through the CPU compute stub), runs the cyclic plan's step
+    slices, all-gathers them and reports the whole job; the gathered slices
+    of every rank are checked against the stub inside the run."""
+    line = _bench(["--gpus", "2", "--config", config, "--n", str(n), "--length", str(length),
+                   "--steps", "2", "--warmup", "1", "--cpu-stub", "tests.bench_stub:compute"])
+    assert line["n_gpus"] == 2 and line["steps"] == 2
+    assert line["stub_checked_pairs"] > 0
+    assert line["value"] > 0 and line["roofline"] is None
+
+
+def test_bench_rank_failure_stops_the_job():
+    """A failing rank ends the whole job with its status (its peer is stopped
+    instead of waiting in a collective forever)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--config", "ns",
+                        "--n", "6", "--length", "30", "--cpu-stub", "tests.bench_stub:fail_on_rank1"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "injected rank-1 failure" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_plan_with_gpu_values_matches_gram(gpu_ctx, world):
+    """sk_gram_sharded's world > 1 data path on one GPU: every rank's cells
+    of the cyclic plan computed by the engine (sk_pairs, as sk_gram_sharded's
+    sk_pairs_device does), padded to the all-gather's equal buffers and
+    unscattered by sk_shard_assemble, equal sk_gram bit for bit -- raw and
+    normalised, with n(n+1)/2 not a multiple of the world size."""
+    import stem_kernel_amd as ska
+
+    n = 11  # 66 cells: 66 % 4 != 0, 66 % 8 != 0; world 3 divides it
+    seqs = ska.random_sequences(n, 90, 0x5EED0007)
+    ds = ska.Dataset.synthetic(seqs, th=0.01, threads=4)
+    kern = ska.SuStemStrKernel()
+    for normalize in (False, True):
+        ref = gpu_ctx.gram(ds, kern, normalize=normalize)
+        parts = []
+        for r in range(world):
+            x, y = shard.rank_pairs(n, world, r)
+            parts.append(gpu_ctx.pairs(ds, kern, x, y))
+        got = shard.assemble(parts, n, world, normalize=normalize)
+        assert np.array_equal(got, ref)
