@@ -144,6 +144,10 @@ int sk_dataset_add_synthetic(sk_dataset *ds, int32_t n, const char *const *seqs,
 int sk_dataset_add_synthetic_rows(sk_dataset *ds, int32_t n, int32_t n_rows,
                                   const char *const *rows, const char *const *labels,
                                   float th, int32_t n_threads);
+/* Append a copy of example i of src (its built DAG, profile and weights: no
+ * rebuild) to dst, e.g. to assemble the pair a per-pair Kernel::operator()
+ * call evaluates from examples built once.  dst must not be uploaded yet. */
+int sk_dataset_add_copy(sk_dataset *dst, const sk_dataset *src, int32_t i);
 int sk_dataset_size(const sk_dataset *ds);
 /* label of example i (pointer valid while ds lives) */
 const char *sk_dataset_label(const sk_dataset *ds, int i);

@@ -61,6 +61,7 @@ SIGNATURES = {
     "sk_dataset_add_synthetic_rows": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_char_p),
                                                 C.POINTER(C.c_char_p), C.c_float, C.c_int32]),
     "sk_dataset_size": (C.c_int, [_P]),
+    "sk_dataset_add_copy": (C.c_int, [_P, _P, C.c_int32]),
     "sk_dataset_label": (C.c_char_p, [_P, C.c_int]),
     "sk_dataset_shape": (C.c_int, [_P, C.c_int, _I32P, _I32P, _I32P, _I32P, _I32P]),
     "sk_dataset_dag": (C.c_int, [_P, C.c_int, _U32P, _U32P, _U32P, _U32P, _F32P, _U32P,

@@ -2539,6 +2539,18 @@ int sk_dataset_add(sk_dataset* ds, const char* label, int n_rows, const char* co
   return SK_OK;
 }
 
+int sk_dataset_add_copy(sk_dataset* dst, const sk_dataset* src, int32_t i) {
+  if (!dst || !src || i < 0 || (size_t)i >= src->ex.size()) return SK_ERR_INVALID;
+  if (dst->uploaded) return SK_ERR_INVALID;
+  try {
+    dst->ex.push_back(src->ex[(size_t)i]);
+    dst->labels.push_back(src->labels[(size_t)i]);
+  } catch (const std::bad_alloc&) {
+    return SK_ERR_ALLOC;
+  }
+  return SK_OK;
+}
+
 int sk_dataset_add_synthetic_rows(sk_dataset* ds, int32_t n, int32_t n_rows,
                                   const char* const* rows, const char* const* labels, float th,
                                   int32_t n_threads) {
