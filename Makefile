@@ -33,7 +33,7 @@ CLI := $(ROOT)stem_kernel_amd/bin/stem_kernel_lite
 cli: $(CLI)
 $(CLI): $(ROOT)stem_kernel_amd/csrc/cli/stem_kernel_lite.cpp $(ROOT)include/stem_kernel_compat.hpp $(ROOT)include/stem_kernel.h $(LIB)
 	@mkdir -p $(dir $@)
-	g++ -O2 -std=c++17 -Wall -Wextra -I$(ROOT)include $< -L$(ROOT)stem_kernel_amd -lstem_kernel_amd -lz \
+	g++ -O2 -std=c++17 -Wall -Wextra -I$(ROOT)include $< -L$(ROOT)stem_kernel_amd -lstem_kernel_amd -lz -ldl \
 	  -Wl,-rpath,'$$ORIGIN/..' -o $@
 
 $(BUILD)/%.o: $(ROOT)stem_kernel_amd/csrc/%.cpp $(HDRS)

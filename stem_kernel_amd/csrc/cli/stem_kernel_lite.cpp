@@ -17,11 +17,13 @@
 //
 // Differences, by necessity: base-pairing probabilities come from the
 // engine's GPU McCaskill (sk_fold_mccaskill) instead of ViennaRNA;
-// --noLonelyPairs and --use-alifold are refused; .bz2 output is refused (no
-// libbz2 headers here).  The
+// --noLonelyPairs and --use-alifold are refused; .bz2 output goes through the
+// system's libbz2.so.1 (loaded at run time: the image has the library but not
+// its headers).  The
 // reference's default kernel (SuStemStr without --log) only estimates memory
 // and never runs App::execute (main.cpp:176-183, `//res = app.execute();`);
 // here every kernel choice computes its matrix.
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -245,40 +247,70 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-void write_text(const std::string& path, const std::string& text) {
-  static std::string err;
-  if (path.size() >= 4 && path.compare(path.size() - 4, 4, ".bz2") == 0) {
-    err = path + ": bzip2 output is not available in this build";
-    throw err.c_str();
-  }
-  if (path.size() >= 3 && path.compare(path.size() - 3, 3, ".gz") == 0) {
-    gzFile g = gzopen(path.c_str(), "wb");
-    if (!g || gzwrite(g, text.data(), (unsigned)text.size()) != (int)text.size() || gzclose(g) != Z_OK) {
+// bzip2 output (common/framework.h:142-147's bzip2_compressor) through the
+// system libbz2, loaded at run time: the BZ2_bzWrite* entry points of its
+// stable C ABI (bzlib.h's BZFILE is opaque).
+class Bz2Writer {
+ public:
+  explicit Bz2Writer(const std::string& path) {
+    static std::string err;
+    void* h = dlopen("libbz2.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("libbz2.so", RTLD_NOW | RTLD_LOCAL);
+    if (h) {
+      open_ = reinterpret_cast<OpenFn>(dlsym(h, "BZ2_bzWriteOpen"));
+      write_ = reinterpret_cast<WriteFn>(dlsym(h, "BZ2_bzWrite"));
+      close_ = reinterpret_cast<CloseFn>(dlsym(h, "BZ2_bzWriteClose"));
+    }
+    if (!open_ || !write_ || !close_) {
+      err = path + ": bzip2 output needs libbz2.so.1";
+      throw err.c_str();
+    }
+    f_ = std::fopen(path.c_str(), "wb");
+    int e = 0;
+    if (f_) bz_ = open_(&e, f_, 9, 0, 0);
+    if (!f_ || !bz_ || e != 0) {
+      if (f_) std::fclose(f_);
+      f_ = nullptr;
       err = path + ": cannot open for writing";
       throw err.c_str();
     }
-    return;
   }
-  std::ofstream out(path);
-  if (!out) {
-    err = path + ": cannot open for writing";
-    throw err.c_str();
+  ~Bz2Writer() {
+    int e = 0;
+    unsigned in = 0, out = 0;
+    if (bz_) close_(&e, bz_, 0, &in, &out);
+    if (f_) std::fclose(f_);
   }
-  out << text;
-}
+  void write(const std::string& s) {
+    int e = 0;
+    for (size_t o = 0; o < s.size(); o += 1u << 30) {
+      const int n = (int)std::min<size_t>(s.size() - o, 1u << 30);
+      write_(&e, bz_, const_cast<char*>(s.data() + o), n);
+    }
+  }
 
-// streaming text output (plain, or gzip by suffix) for predict mode
+ private:
+  typedef void* (*OpenFn)(int*, FILE*, int, int, int);
+  typedef void (*WriteFn)(int*, void*, void*, int);
+  typedef void (*CloseFn)(int*, void*, int, unsigned*, unsigned*);
+  OpenFn open_ = nullptr;
+  WriteFn write_ = nullptr;
+  CloseFn close_ = nullptr;
+  FILE* f_ = nullptr;
+  void* bz_ = nullptr;
+};
+
+// text output (plain, gzip or bzip2 by suffix, as the reference's filtering
+// stream picks them, common/framework.h:142-152); predict mode streams
+// through it
 class TextSink {
  public:
   explicit TextSink(const std::string& path) : path_(path) {
     static std::string err;
-    if (path.size() >= 4 && path.compare(path.size() - 4, 4, ".bz2") == 0) {
-      err = path + ": bzip2 output is not available in this build";
-      throw err.c_str();
-    }
-    if (path.size() >= 3 && path.compare(path.size() - 3, 3, ".gz") == 0) gz_ = gzopen(path.c_str(), "wb");
+    if (path.size() >= 4 && path.compare(path.size() - 4, 4, ".bz2") == 0) bz_.reset(new Bz2Writer(path));
+    else if (path.size() >= 3 && path.compare(path.size() - 3, 3, ".gz") == 0) gz_ = gzopen(path.c_str(), "wb");
     else out_.open(path);
-    if (gz_ ? false : !out_.is_open()) {
+    if (!bz_ && (gz_ ? false : !out_.is_open())) {
       err = path + ": cannot open for writing";
       throw err.c_str();
     }
@@ -287,15 +319,22 @@ class TextSink {
     if (gz_) gzclose(gz_);
   }
   void write(const std::string& s) {
-    if (gz_) gzwrite(gz_, s.data(), (unsigned)s.size());
+    if (bz_) bz_->write(s);
+    else if (gz_) gzwrite(gz_, s.data(), (unsigned)s.size());
     else out_ << s;
   }
 
  private:
   std::string path_;
+  std::unique_ptr<Bz2Writer> bz_;
   gzFile gz_ = nullptr;
   std::ofstream out_;
 };
+
+void write_text(const std::string& path, const std::string& text) {
+  TextSink sink(path);
+  sink.write(text);
+}
 
 void flush_if_large(std::ostringstream& buf, std::unique_ptr<TextSink>& sink, const std::string& path,
                     bool final_flush = false) {

@@ -2469,6 +2469,7 @@ int sk_open(int device, void* hip_stream, sk_context** out) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return SK_ERR_HIP;
     c->own_stream = true;
   }
+  // a failure part-way releases what was created (sk_close skips nulls)
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->cls, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
@@ -2476,11 +2477,12 @@ int sk_open(int device, void* hip_stream, sk_context** out) {
       hipEventCreateWithFlags(&c->evf, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->evk, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->evx, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&c->evx, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess) {
+    sk_close(c.release());
     return SK_ERR_HIP;
-  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess)
-    return SK_ERR_HIP;
+  }
   *out = c.release();
   return SK_OK;
 }
@@ -2488,7 +2490,11 @@ int sk_open(int device, void* hip_stream, sk_context** out) {
 int sk_close(sk_context* ctx) {
   if (!ctx) return SK_OK;
   (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  // work may still be queued on any of the context's streams (e.g. after an
+  // error part-way through a multi-stream call): drain them all before the
+  // buffers they read are freed
+  for (hipStream_t st : {ctx->stream, ctx->side, ctx->cls, ctx->aux})
+    if (st) (void)hipStreamSynchronize(st);
   sk::comm_destroy(ctx->comm);
   ctx->comm = nullptr;
   if (ctx->scratch) (void)hipFree(ctx->scratch);

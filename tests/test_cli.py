@@ -129,6 +129,19 @@ def test_cli_train_gz_and_options(gpu_ctx, fa_files):
 
 
 @pytest.mark.gpu
+def test_cli_train_bz2_equals_plain(gpu_ctx, fa_files):
+    """`.bz2` output (common/framework.h:142-147's bzip2 filter) holds the
+    same text as the plain file."""
+    import bz2
+    d, pos, neg, _ = fa_files
+    plain, packed = d / "gram_plain.txt", d / "gram_packed.txt.bz2"
+    for out in (plain, packed):
+        r = _run(["-n", out, "+1", d / "pos.fa", "-1", d / "neg.fa"])
+        assert r.returncode == 0, r.stdout + r.stderr
+    assert bz2.open(packed, "rt").read() == plain.read_text()
+
+
+@pytest.mark.gpu
 def test_cli_predict_rows_and_norms(gpu_ctx, fa_files, tmp_path):
     d, pos, neg, test = fa_files
     out, norms = tmp_path / "rows.txt", tmp_path / "norms.txt"
