@@ -272,7 +272,7 @@ hipError_t launch_bpla(const BplaLaunch& P, int grid, int nwaves, hipStream_t st
 __global__ void __launch_bounds__(256) sk_bpla_tab_kernel(const float4* __restrict__ prof,
                                                           const float4* __restrict__ lru,
                                                           int64_t n, const double* __restrict__ tb,
-                                                          BplaPos* __restrict__ xrole,
+                                                          double xscale, BplaPos* __restrict__ xrole,
                                                           BplaPos* __restrict__ yrole) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(256) sk_bpla_tab_kernel(const float4* __restri
   for (int l = 0; l < 4; ++l) {
     const double u = tb[l] * (double)c.x + tb[4 + l] * (double)c.y + tb[8 + l] * (double)c.z +
                      tb[12 + l] * (double)c.w;
-    X.v[l] = s > 0.0f ? u / (double)s : 0.0;
+    X.v[l] = s > 0.0f ? u / (double)s * xscale : 0.0;
     Y.v[l] = s > 0.0f ? (double)cv[l] / (double)s : 0.0;
   }
   X.pr = Y.pr = w.y;
@@ -297,12 +297,17 @@ __global__ void __launch_bounds__(256) sk_bpla_tab_kernel(const float4* __restri
 }
 
 hipError_t launch_bpla_tab(const float4* prof, const float4* lru, int64_t n, const double* table,
-                           BplaPos* xrole, BplaPos* yrole, hipStream_t st) {
+                           double xscale, BplaPos* xrole, BplaPos* yrole, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(sk_bpla_tab_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                     prof, lru, n, table, xrole, yrole);
+                     prof, lru, n, table, xscale, xrole, yrole);
   return hipGetLastError();
 }
+
+template <bool BP>
+__device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, const int4* ci, double* ksum,
+                                                 int Ly, const BplaPos* ycol, double* bnd, const double* etab,
+                                                 int lane);
 
 // A chunk of np pairs sharing y on one wavefront: their x rows are streamed
 // back to back as one sequence of rows (chunk row G = first row of pair p +
@@ -326,6 +331,10 @@ template <bool SW, bool BP>
 __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, const int4* ci,
                                                 double* ksum, int Ly, const BplaPos* ycol,
                                                 double* bnd, const double* etab, int lane) {
+  if (!SW) {  // the exp path runs two rows per lane
+    bpla_fast_chunk2<BP>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
+    return;
+  }
   const double alpha = P.alpha, beta = P.beta, gap = P.gap, ext = P.ext;
   const double bg = P.beta_gap, be = P.beta_ext;
   const int4 last = ci[np - 1];
@@ -379,7 +388,7 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
       s = alpha * (double)pp + (double)uu * s;
     }
     if (!SW) {
-      nM = fast_exp(beta * s, etab, P.ec) * __builtin_fma(fb, dX + dY + dM, 1.0);
+      nM = fast_exp(beta * s, etab) * __builtin_fma(fb, dX + dY + dM, 1.0);
       nX = cbg * uM + cbe * uX;
       nY = c1 ? 0.0 : bg * (lM + lX) + be * lY;  // column 0 is zero
       // every lane sums its cells; a row that does not exist (past the
@@ -543,6 +552,210 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The exp path (local_alignment_exp) with TWO rows per lane: lane l of
+// strip s computes chunk rows A = 128s + 2l + 1 and B = A + 1 at one column
+// per step, a step behind lane l-1, so a 64-step window serves 128 rows and
+// the per-step shared work -- the y column read from LDS, the three DPP
+// shifts of the row above, the boundary-row traffic of lane 63, the
+// window's per-lane control -- is paid once per two cells.  Row A's "up" is
+// lane l-1's row B (DPP; lane 0: the boundary row in LDS), row B's "up" is
+// this lane's row A of the same step and its diagonal row A's previous
+// output (registers).  Every pair is padded to an even row count (a dummy
+// row after an odd last row; its cells are computed and dropped) so a lane's
+// two rows always belong to one pair and a pair's first row is always an A
+// row (fb = 0 there).  Rows that do not exist are dropped at the hand-off
+// (okA / okB), as in the one-row schedule.  xtab holds the x operands with
+// beta folded in (v[l] * beta), so the exponent is
+// fma(uu, s, alpha * beta * pp) (BP) or s (LA).
+template <bool BP>
+__device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, const int4* ci, double* ksum,
+                                                 int Ly, const BplaPos* ycol, double* bnd, const double* etab,
+                                                 int lane) {
+  const double ab = P.alpha * P.beta;
+  const double bg = P.beta_gap, be = P.beta_ext;
+  const int4 last = ci[np - 1];
+  const int Rt = __builtin_amdgcn_readfirstlane(last.z + last.y + (last.y & 1));  // padded rows
+  const int Lys = max(Ly, 64);
+  for (int j = lane; j < 3 * (Lys + 1); j += 64) bnd[j] = 0.0;  // row 0
+  if (lane < np) ksum[lane] = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (Rt == 0 || Ly == 0) return;  // no cells: K = 1
+  const int Rp = Rt >> 1;          // row pairs
+  const int nstrips = (Rp + 63) / 64;
+  const int T = (nstrips - 1) * Lys + ((Rp - 1) & 63) + Ly;  // steps
+  const char* ybase = reinterpret_cast<const char*>(ycol);
+
+  // row pair (chunk rows GA = 2 * Q + 1, GA + 1) -> pair, existence, fb, xtab index
+  auto map_pair = [&](int Q, int& pp, bool& oka, bool& okb, double& fbv, int& xi) __attribute__((always_inline)) {
+    const int G = 2 * Q + 1;
+    int q = 0;
+    for (int k = 1; k < np; ++k) q += G - 1 >= ci[k].z ? 1 : 0;
+    const int4 c = ci[q];
+    const int i = G - c.z;  // odd, <= c.y when the row exists
+    oka = G <= Rt;
+    okb = oka && i + 1 <= c.y;
+    pp = q;
+    fbv = i == 1 ? 0.0 : 1.0;
+    xi = oka ? c.x + i - 1 : ci[0].x;
+  };
+  int pn, xi;
+  bool okan, okbn;
+  double fbn;
+  map_pair(lane, pn, okan, okbn, fbn, xi);
+  BplaPos xnA = P.xtab[xi], xnB = P.xtab[okbn ? xi + 1 : xi];  // the next strip's operands
+  BplaPos xA = xnA, xB = xnB;
+  int p = 0;
+  bool okA = false, okB = false;
+  double fb = 1.0, cbg = bg, cbe = be;  // row A's: 0 / 0 / 0 on a pair's first row
+  unsigned yofs = 0;
+  double aM = 0.0, aX = 0.0, aY = 0.0;  // row A at (., j-1)
+  double bM = 0.0, bX = 0.0, bY = 0.0;  // row B at (., j-1)
+  double accA = 0.0, accB = 0.0;
+
+  auto expo = [&](const BplaPos& xr, const BplaPos& yc) __attribute__((always_inline)) {
+    double s = xr.v[0] * yc.v[0];
+    s = __builtin_fma(xr.v[1], yc.v[1], s);
+    s = __builtin_fma(xr.v[2], yc.v[2], s);
+    s = __builtin_fma(xr.v[3], yc.v[3], s);
+    if (BP) {
+      // BPLAScore (bpla_kernel.cpp:55-60): float products as written
+      const float pp = f32_dot2(xr.pr, yc.pr, xr.pl, yc.pl);
+      const float uu = xr.pu * yc.pu;
+      s = __builtin_fma((double)uu, s, ab * (double)pp);
+    }
+    return fast_exp(s, etab);
+  };
+  // both cells of a step: d = row above at (j-1), u = row above at j (lane
+  // l-1's row B); c1: column 1 (left is column 0: zero)
+  auto cells = [&](const BplaPos& yc, double dM, double dX, double dY, double uM, double uX, bool c1)
+                   __attribute__((always_inline)) {
+    const double eA = expo(xA, yc);
+    const double eB = expo(xB, yc);
+    const double nMA = eA * __builtin_fma(fb, dX + dY + dM, 1.0);
+    const double nXA = cbg * uM + cbe * uX;
+    const double nYA = c1 ? 0.0 : bg * (aM + aX) + be * aY;
+    const double nMB = eB * (1.0 + (aX + aY + aM));  // diagonal: row A at j-1
+    const double nXB = bg * nMA + be * nXA;
+    const double nYB = c1 ? 0.0 : bg * (bM + bX) + be * bY;
+    aM = nMA;
+    aX = nXA;
+    aY = nYA;
+    bM = nMB;
+    bX = nXB;
+    bY = nYB;
+    accA += nMA;
+    accB += nMB;
+  };
+
+  // interior step: lane 0's column jb, every lane active
+  auto interior = [&](int jb, double& dM, double& dX, double& dY, double& uM, double& uX, double& uY)
+                      __attribute__((always_inline)) {
+    const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+    const double* bj = bnd + 3 * jb;
+    uM = wave_shr1(bM, bj[0]);
+    uX = wave_shr1(bX, bj[1]);
+    uY = wave_shr1(bY, bj[2]);
+    cells(yc, dM, dX, dY, uM, uX, false);
+    if (lane == 63) {  // lane 63's column is jb - 63
+      double* bw = bnd + 3 * (jb - 63);
+      bw[0] = bM;
+      bw[1] = bX;
+      bw[2] = bY;
+    }
+    yofs += (unsigned)sizeof(BplaPos);
+  };
+
+  // window step w of strip s: lane w starts its rows of strip s at column 1,
+  // handing its finished rows' sums to their pair (rows that exist only);
+  // lanes below are at column w - lane + 1 of strip s, lanes above at column
+  // Lys + w - lane + 1 of strip s-1
+  auto window = [&](int s, int w, double& dM, double& dX, double& dY, double& uM, double& uX, double& uY)
+                    __attribute__((always_inline)) {
+    const bool wrap = lane == w;
+    if (wrap) {
+      const double h = (okA ? accA : 0.0) + (okB ? accB : 0.0);
+      if (okA) ksum[p] += h;
+      accA = accB = 0.0;
+      xA = xnA;
+      xB = xnB;
+      p = pn;
+      okA = okan;
+      okB = okbn;
+      fb = fbn;
+      cbg = bg * fbn;
+      cbe = be * fbn;
+      yofs = 0;
+      dM = dX = dY = 0.0;
+      aM = aX = aY = 0.0;  // row A's column 0 (row B's diagonal at column 1)
+    }
+    const int jl = lane <= w ? w - lane + 1 : Lys + w - lane + 1;
+    const bool on = jl <= Ly && (lane <= w ? s < nstrips : s > 0);
+    const int jb = w + 1;  // lane 0's column (strip s)
+    const double* bj = bnd + 3 * (jb <= Ly ? jb : 0);
+    uM = wave_shr1(bM, bj[0]);
+    uX = wave_shr1(bX, bj[1]);
+    uY = wave_shr1(bY, bj[2]);
+    if (on) {
+      const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+      cells(yc, dM, dX, dY, uM, uX, wrap);
+      if (lane == 63) {
+        double* bw = bnd + 3 * jl;
+        bw[0] = bM;
+        bw[1] = bX;
+        bw[2] = bY;
+      }
+    }
+    yofs += (unsigned)sizeof(BplaPos);
+  };
+
+  // d* = values received a step earlier, u* = this step's; the unrolled
+  // pairs of steps swap their roles (no register copies)
+  double pM = 0.0, pX = 0.0, pY = 0.0, qM = 0.0, qX = 0.0, qY = 0.0;
+  for (int s = 0; s <= nstrips; ++s) {
+    const int Ws = s * Lys;
+    const int wend = min(64, T - Ws);
+    if (wend <= 0) break;
+    int w = 0;
+    for (; w + 1 < wend; w += 2) {
+      window(s, w, pM, pX, pY, qM, qX, qY);
+      window(s, w + 1, qM, qX, qY, pM, pX, pY);
+    }
+    if (w < wend) {
+      window(s, w, pM, pX, pY, qM, qX, qY);
+      pM = qM;
+      pX = qX;
+      pY = qY;
+    }
+    if (s + 1 < nstrips) {
+      map_pair(64 * (s + 1) + lane, pn, okan, okbn, fbn, xi);
+      xnA = P.xtab[xi];
+      xnB = P.xtab[okbn ? xi + 1 : xi];
+    }
+    const int tend = s < nstrips ? min(Ws + Lys, T) : 0;
+    int t = Ws + 64;
+    for (; t + 1 < tend; t += 2) {
+      interior(t - Ws + 1, pM, pX, pY, qM, qX, qY);
+      interior(t - Ws + 2, qM, qX, qY, pM, pX, pY);
+    }
+    if (t < tend) {
+      interior(t - Ws + 1, pM, pX, pY, qM, qX, qY);
+      pM = qM;
+      pX = qX;
+      pY = qY;
+    }
+  }
+  // the rows still held
+  if (okA) {
+    const double h = accA + (okB ? accB : 0.0);
+    __hip_atomic_fetch_add(&ksum[p], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Pairs dealt one per wave: each wave stages its own y columns.
 template <bool SW, bool BP>
 __global__ void __launch_bounds__(256) sk_bpla_fast_kernel(BplaLaunch P) {
@@ -592,7 +805,8 @@ __global__ void __launch_bounds__(256) sk_bpla_fast_kernel(BplaLaunch P) {
 #define SK_BPLA_ITEMS_ATTR
 #endif
 template <bool SW, bool BP>
-__global__ void __launch_bounds__(1024) SK_BPLA_ITEMS_ATTR sk_bpla_fast_items_kernel(BplaLaunch P) {
+__global__ void __launch_bounds__(64 * kBplaItemsWavesMax) SK_BPLA_ITEMS_ATTR
+    sk_bpla_fast_items_kernel(BplaLaunch P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -646,7 +860,7 @@ __global__ void __launch_bounds__(1024) SK_BPLA_ITEMS_ATTR sk_bpla_fast_items_ke
       int start = 0;
       for (int q = 0; q < np - 1; ++q) {
         const int lq = __shfl(len, q, 64);
-        start += lane > q ? lq : 0;
+        start += lane > q ? (SW ? lq : lq + (lq & 1)) : 0;  // the exp path pads pairs to even rows
       }
       if (lane < np) ci[lane] = make_int4(pb, len, start, 0);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

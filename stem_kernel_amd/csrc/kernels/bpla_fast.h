@@ -38,26 +38,28 @@ __device__ __forceinline__ float f32_madd(float n, float a, float b) {
   return n + a * b;
 }
 
-// exp(x), |x| << 700: x = (64m + j) ln2/64 + r, |r| <= ln2/128, e^r by its
-// Taylor series to degree 5 (truncation < 4e-17 relative), times 2^(j/64)
-// from an LDS table, times 2^m.
-__device__ __forceinline__ double fast_exp(double x, const double* etab, const double (&ec)[4]) {
-  const double k = __builtin_rint(x * 92.332482616893657);  // 64 / ln2
-  const int ki = (int)k;
-  double r = __builtin_fma(-k, 1.0830424693267560e-02, x);  // ln2/64, high part (exact k*hi)
-  r = __builtin_fma(-k, 2.9815858269852933e-12, r);         // ln2/64, low part
-  double p = ec[0];
-  p = __builtin_fma(p, r, ec[1]);
-  p = __builtin_fma(p, r, ec[2]);
-  p = __builtin_fma(p, r, ec[3]);
+// exp(x) for |x| < 2^40 (overflow to inf past ~709, underflow to 0):
+// x = (1024 m + j) ln2/1024 + r, |r| <= ln2/2048; k = 1024 m + j rounded by
+// the 1.5 * 2^52 shifter (its low word is k), r by a two-part ln2/1024 (the
+// high part has 32 significant bits, so k * hi is exact), e^r by its Taylor
+// series to degree 3 (truncation < 6e-16 relative), times 2^(j/1024) from
+// the workgroup's LDS table, times 2^m.  11 VALU and one LDS read (the
+// degree-5 form over a 64-entry table took 16).
+__device__ __forceinline__ double fast_exp(double x, const double* etab) {
+  const double t = __builtin_fma(x, 1477.3197218702985, 6755399441055744.0);  // 1024/ln2, 1.5*2^52
+  const int ki = __double2loint(t);
+  const double k = t - 6755399441055744.0;
+  double r = __builtin_fma(-k, 6.769015435565962e-04, x);  // ln2/1024, high part
+  r = __builtin_fma(-k, -4.1024561256651217e-14, r);       // ln2/1024, low part
+  double p = __builtin_fma(r, 0.16666666666666666, 0.5);
   p = __builtin_fma(p, r, 1.0);
   p = __builtin_fma(p, r, 1.0);
-  return __builtin_amdgcn_ldexp(etab[ki & 63] * p, ki >> 6);
+  return __builtin_amdgcn_ldexp(etab[ki & 1023] * p, ki >> 10);
 }
 
-// 2^(j/64), j < 64, into the workgroup's exp table (first kBplaExpLds bytes)
+// 2^(j/1024), j < 1024, into the workgroup's exp table (first kBplaExpLds bytes)
 __device__ __forceinline__ void fill_exp_table(double* etab) {
-  if (threadIdx.x < 64) etab[threadIdx.x] = exp2((double)threadIdx.x / 64.0);
+  for (int j = threadIdx.x; j < 1024; j += blockDim.x) etab[j] = exp2((double)j / 1024.0);
   __syncthreads();
 }
 

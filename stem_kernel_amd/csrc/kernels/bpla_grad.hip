@@ -353,7 +353,7 @@ __device__ void bpla_grad_wave_pair(const BplaGradLaunch& P, int x, int y, const
         const BplaPos yc = ycol[b - 1];
         double wp;
         const double sc = score(xr, yc, wp);
-        Pn = fast_exp(beta * sc, etab, P.ec) * M;
+        Pn = fast_exp(beta * sc, etab) * M;
         BM[(int64_t)t * 64 + lane] = M;
         BX[(int64_t)t * 64 + lane] = X;
         BY[(int64_t)t * 64 + lane] = Y;
@@ -398,7 +398,7 @@ __device__ void bpla_grad_wave_pair(const BplaGradLaunch& P, int x, int y, const
       const BplaPos yc = ycol[j - 1];
       double wp;
       const double sc = score(xr, yc, wp);
-      const double bs = fast_exp(beta * sc, etab, P.ec);
+      const double bs = fast_exp(beta * sc, etab);
       const bool c1 = j == 1;
       // diagonal F_M + F_IX + F_IY + F_LX + F_LY at (i-1, j-1)
       const double extra = i == 1 ? (c1 ? 3.0 : 1.0) : (double)j;

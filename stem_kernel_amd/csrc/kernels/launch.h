@@ -142,9 +142,6 @@ struct BplaLaunch {
   // fast kernel, grouped by y: items {first pair, count} of pairs sharing y
   const int2* items = nullptr;
   int32_t n_items = 0;
-  // fast kernel's exp: Taylor coefficients 1/5!, 1/4!, 1/3!, 1/2! (kernel
-  // arguments, so they sit in SGPRs as FMA addends)
-  double ec[4] = {8.3333333333333332e-03, 4.1666666666666664e-02, 1.6666666666666666e-01, 0.5};
   const double* table = nullptr;  // 16: score table (x residue major)
   double alpha = 0.0, beta = 0.0, gap = 0.0, ext = 0.0;
   double beta_gap = 0.0, beta_ext = 0.0;  // exp(beta*gap), exp(beta*ext)
@@ -177,7 +174,6 @@ struct BplaGradLaunch {
   // sk_bpla_tab_kernel, pairs pulled by waves, result of pair k at oidx[k]
   const BplaPos* xtab = nullptr;
   const BplaPos* ytab = nullptr;
-  double ec[4] = {8.3333333333333332e-03, 4.1666666666666664e-02, 1.6666666666666666e-01, 0.5};
   unsigned long long* pair_counter = nullptr;
   const int64_t* oidx = nullptr;
   int32_t lds_max_len = 0;  // even, >= 64
@@ -293,11 +289,17 @@ int stem_maxk(int max_nl);
 size_t str_lds_bytes(const StrLaunch& P, int nwaves);
 hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st);
 
-// fast kernels: a workgroup's LDS starts with the exp table 2^(j/64), j < 64
-constexpr size_t kBplaExpLds = 64 * 8;
+// fast kernels: a workgroup's LDS starts with the exp table 2^(j/1024), j < 1024
+constexpr size_t kBplaExpLds = 1024 * 8;
 // a wave's chunk of pairs streamed back to back: per pair {xtab base,
 // length, first row, -} and its K sum
 constexpr int kBplaChunkMax = 8;
+// y-grouped fast kernel: at most 12 waves per workgroup, 3 per SIMD (the
+// two-row exp path holds two rows' operands and state: up to 168 VGPRs)
+#ifndef SK_BPLA_ITEMS_WAVES
+#define SK_BPLA_ITEMS_WAVES 12
+#endif
+constexpr int kBplaItemsWavesMax = SK_BPLA_ITEMS_WAVES;
 constexpr size_t kBplaChunkLds = kBplaChunkMax * (16 + 8);
 // grouped fast kernel: exp table | shared y columns | per wave boundary row
 // and chunk
@@ -308,8 +310,10 @@ __host__ __device__ inline size_t bpla_items_lds_bytes(int maxlen, int nwaves) {
 size_t bpla_lds_bytes(const BplaLaunch& P, int nwaves);
 hipError_t launch_bpla(const BplaLaunch& P, int grid, int nwaves, hipStream_t st);
 // dyadic-profile fast path: per-call operand tables, then the DP
+// xscale multiplies the x-role factors v[l] (beta for the exp path, whose
+// exponent is then formed without a multiply; 1 elsewhere)
 hipError_t launch_bpla_tab(const float4* prof, const float4* lru, int64_t n, const double* table,
-                           BplaPos* xrole, BplaPos* yrole, hipStream_t st);
+                           double xscale, BplaPos* xrole, BplaPos* yrole, hipStream_t st);
 // per-wave LDS of the fast kernel: y columns (BplaPos, maxlen) | boundary
 // row {M, X, Y} [maxlen + 2] | chunk
 __host__ __device__ inline size_t bpla_fast_wave_lds_bytes(int maxlen) {

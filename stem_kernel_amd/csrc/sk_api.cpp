@@ -1167,11 +1167,13 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
     // x-role table of the x set, y-role table of the y set
     sk::BplaPos* tx = d_tab;           // [npx] x role | [npx] y role
     sk::BplaPos* ty = d_tab + npx;
-    SK_HIP(ctx, sk::launch_bpla_tab(xs_->dev.pos_prof, xs_->dev.pos_lru, (int64_t)npx, d_tb, tx,
+    // the exp path's x operands carry beta (bpla_fast_chunk2)
+    const double xscale = sw ? 1.0 : kp->beta;
+    SK_HIP(ctx, sk::launch_bpla_tab(xs_->dev.pos_prof, xs_->dev.pos_lru, (int64_t)npx, d_tb, xscale, tx,
                                     d_tab + npx, S));
     if (npy) {
       ty = d_tab + 2 * npx + npy;      // [npy] x role (unused) | [npy] y role
-      SK_HIP(ctx, sk::launch_bpla_tab(ys_->dev.pos_prof, ys_->dev.pos_lru, (int64_t)npy, d_tb,
+      SK_HIP(ctx, sk::launch_bpla_tab(ys_->dev.pos_prof, ys_->dev.pos_lru, (int64_t)npy, d_tb, xscale,
                                       d_tab + 2 * npx, ty, S));
     }
     sk::BplaLaunch F = T;
@@ -1199,13 +1201,14 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
       // per launch for two 8-wave ones: the y columns staged once for 16
       // waves), halved while its LDS does not fit, the CU's 16 waves then
       // made up by more workgroups.
-      static const int iw = std::getenv("SK_BPLA_IWAVES") ? std::atoi(std::getenv("SK_BPLA_IWAVES")) : 16;
+      static const int iw =
+          std::getenv("SK_BPLA_IWAVES") ? std::atoi(std::getenv("SK_BPLA_IWAVES")) : sk::kBplaItemsWavesMax;
       static const int iwg = std::getenv("SK_BPLA_IWG") ? std::atoi(std::getenv("SK_BPLA_IWG")) : 0;
-      w = std::min(std::max(iw, 1), 16);
+      w = std::min(std::max(iw, 1), sk::kBplaItemsWavesMax);
       while (w > 1 && sk::bpla_items_lds_bytes(F.lds_max_len, w) > 163840) w /= 2;
       const size_t l = sk::bpla_items_lds_bytes(F.lds_max_len, w);
       if (l > 163840) return fail(ctx, SK_ERR_UNSUPPORTED, "sequence too long for BPLA kernel LDS");
-      per_cu = std::max(1, std::min<int>((int)(163840 / l), iwg > 0 ? iwg : std::max(1, 16 / w)));
+      per_cu = std::max(1, std::min<int>((int)(163840 / l), iwg > 0 ? iwg : std::max(1, sk::kBplaItemsWavesMax / w)));
       units = F.n_items;
     } else {
       const size_t wl = sk::bpla_fast_wave_lds_bytes(F.lds_max_len);
@@ -2258,11 +2261,11 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
     sk::BplaPos* tabs = static_cast<sk::BplaPos*>(tab_buf.p);
     sk::BplaPos* tx = tabs;  // [npx] x role | [npx] y role (| [npy] x role | [npy] y role)
     sk::BplaPos* ty = tabs + npx;
-    SK_HIP(ctx, sk::launch_bpla_tab(xs_->dev.pos_prof, xs_->dev.pos_lru, (int64_t)npx, d_tb, tx,
+    SK_HIP(ctx, sk::launch_bpla_tab(xs_->dev.pos_prof, xs_->dev.pos_lru, (int64_t)npx, d_tb, 1.0, tx,
                                     tabs + npx, S));
     if (npy) {
       ty = tabs + 2 * npx + npy;
-      SK_HIP(ctx, sk::launch_bpla_tab(ys_->dev.pos_prof, ys_->dev.pos_lru, (int64_t)npy, d_tb,
+      SK_HIP(ctx, sk::launch_bpla_tab(ys_->dev.pos_prof, ys_->dev.pos_lru, (int64_t)npy, d_tb, 1.0,
                                       tabs + 2 * npx, ty, S));
     }
     rc = ensure_scratch(ctx, (size_t)grid * wpb * (size_t)bt * 8 + 64);
