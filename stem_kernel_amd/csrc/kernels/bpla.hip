@@ -17,6 +17,8 @@
 // FP64 throughout; one exp per cell is the bound.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "bpla_fast.h"
 #include "device_set.h"
 #include "launch.h"
@@ -304,7 +306,7 @@ hipError_t launch_bpla_tab(const float4* prof, const float4* lru, int64_t n, con
   return hipGetLastError();
 }
 
-template <bool BP>
+template <bool BP, bool FULL>
 __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, const int4* ci, double* ksum,
                                                  int Ly, const BplaPos* ycol, double* bnd, const double* etab,
                                                  int lane);
@@ -332,7 +334,10 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
                                                 double* ksum, int Ly, const BplaPos* ycol,
                                                 double* bnd, const double* etab, int lane) {
   if (!SW) {  // the exp path runs two rows per lane
-    bpla_fast_chunk2<BP>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
+    if (Ly >= 64)
+      bpla_fast_chunk2<BP, true>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
+    else
+      bpla_fast_chunk2<BP, false>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
     return;
   }
   const double alpha = P.alpha, beta = P.beta, gap = P.gap, ext = P.ext;
@@ -567,7 +572,7 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
 // (okA / okB), as in the one-row schedule.  xtab holds the x operands with
 // beta folded in (v[l] * beta), so the exponent is
 // fma(uu, s, alpha * beta * pp) (BP) or s (LA).
-template <bool BP>
+template <bool BP, bool FULL>
 __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, const int4* ci, double* ksum,
                                                  int Ly, const BplaPos* ycol, double* bnd, const double* etab,
                                                  int lane) {
@@ -627,16 +632,18 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
     }
     return fast_exp(s, etab);
   };
-  // both cells of a step: d = row above at (j-1), u = row above at j (lane
-  // l-1's row B); c1: column 1 (left is column 0: zero)
-  auto cells = [&](const BplaPos& yc, double dM, double dX, double dY, double uM, double uX, bool c1)
-                   __attribute__((always_inline)) {
+  // both cells of a step: dS = M + X + Y of the row above at (j-1) (lane
+  // l-1 sends its row B's sum, bS), u = row above at j (lane l-1's row B);
+  // c1: column 1 (left is column 0: zero).  A row's left sum M + X is
+  // shared by its Y recurrence and the diagonal sum it hands on.
+  auto cells = [&](const BplaPos& yc, double dS, double uM, double uX, bool c1) __attribute__((always_inline)) {
     const double eA = expo(xA, yc);
     const double eB = expo(xB, yc);
-    const double nMA = eA * __builtin_fma(fb, dX + dY + dM, 1.0);
+    const double sA = aM + aX;
+    const double nMA = eA * __builtin_fma(fb, dS, 1.0);
     const double nXA = cbg * uM + cbe * uX;
-    const double nYA = c1 ? 0.0 : bg * (aM + aX) + be * aY;
-    const double nMB = eB * (1.0 + (aX + aY + aM));  // diagonal: row A at j-1
+    const double nYA = c1 ? 0.0 : bg * sA + be * aY;
+    const double nMB = __builtin_fma(eB, sA + aY, eB);  // diagonal: row A at j-1
     const double nXB = bg * nMA + be * nXA;
     const double nYB = c1 ? 0.0 : bg * (bM + bX) + be * bY;
     aM = nMA;
@@ -650,19 +657,22 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
   };
 
   // interior step: lane 0's column jb, every lane active
-  auto interior = [&](int jb, double& dM, double& dX, double& dY, double& uM, double& uX, double& uY)
+  // (the boundary row holds {M, X, M + X + Y} of row B per column)
+  auto interior = [&](int jb, double& dM, double& dX, double& dS, double& uM, double& uX, double& uS)
                       __attribute__((always_inline)) {
+    (void)dM;
+    (void)dX;
     const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
     const double* bj = bnd + 3 * jb;
     uM = wave_shr1(bM, bj[0]);
     uX = wave_shr1(bX, bj[1]);
-    uY = wave_shr1(bY, bj[2]);
-    cells(yc, dM, dX, dY, uM, uX, false);
+    uS = wave_shr1((bM + bX) + bY, bj[2]);
+    cells(yc, dS, uM, uX, false);
     if (lane == 63) {  // lane 63's column is jb - 63
       double* bw = bnd + 3 * (jb - 63);
       bw[0] = bM;
       bw[1] = bX;
-      bw[2] = bY;
+      bw[2] = (bM + bX) + bY;
     }
     yofs += (unsigned)sizeof(BplaPos);
   };
@@ -671,8 +681,18 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
   // handing its finished rows' sums to their pair (rows that exist only);
   // lanes below are at column w - lane + 1 of strip s, lanes above at column
   // Lys + w - lane + 1 of strip s-1
-  auto window = [&](int s, int w, double& dM, double& dX, double& dY, double& uM, double& uX, double& uY)
+  // FULL (Ly >= 64, so Lys = Ly): every lane computes every window step.
+  // The cells of lanes that have not started strip 0 yet are garbage that
+  // their wrap discards (sums and left / diagonal values reset, row B's left
+  // masked at column 1), and those of lanes past the last strip belong to
+  // rows that do not exist (dropped at the hand-off); lane 63's stray
+  // boundary writes in strip 0 land on columns it overwrites with the real
+  // values before lane 0 of strip 1 reads them.  Otherwise (Ly < 64: columns
+  // past Ly in every strip) the cells of columns past Ly are skipped.
+  auto window = [&](int s, int w, double& dM, double& dX, double& dS, double& uM, double& uX, double& uS)
                     __attribute__((always_inline)) {
+    (void)dM;
+    (void)dX;
     const bool wrap = lane == w;
     if (wrap) {
       const double h = (okA ? accA : 0.0) + (okB ? accB : 0.0);
@@ -687,24 +707,37 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
       cbg = bg * fbn;
       cbe = be * fbn;
       yofs = 0;
-      dM = dX = dY = 0.0;
+      dS = 0.0;
       aM = aX = aY = 0.0;  // row A's column 0 (row B's diagonal at column 1)
     }
-    const int jl = lane <= w ? w - lane + 1 : Lys + w - lane + 1;
-    const bool on = jl <= Ly && (lane <= w ? s < nstrips : s > 0);
     const int jb = w + 1;  // lane 0's column (strip s)
     const double* bj = bnd + 3 * (jb <= Ly ? jb : 0);
     uM = wave_shr1(bM, bj[0]);
     uX = wave_shr1(bX, bj[1]);
-    uY = wave_shr1(bY, bj[2]);
-    if (on) {
+    uS = wave_shr1((bM + bX) + bY, bj[2]);
+    if (FULL) {
       const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
-      cells(yc, dM, dX, dY, uM, uX, wrap);
+      cells(yc, dS, uM, uX, wrap);
+      // lane 63's column: w - 62 once it wrapped (w = 63), else Lys + w - 62
+      const int j63 = w == 63 ? 1 : Lys + w - 62;
       if (lane == 63) {
-        double* bw = bnd + 3 * jl;
+        double* bw = bnd + 3 * j63;
         bw[0] = bM;
         bw[1] = bX;
-        bw[2] = bY;
+        bw[2] = (bM + bX) + bY;
+      }
+    } else {
+      const int jl = lane <= w ? w - lane + 1 : Lys + w - lane + 1;
+      const bool on = jl <= Ly && (lane <= w ? s < nstrips : s > 0);
+      if (on) {
+        const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+        cells(yc, dS, uM, uX, wrap);
+        if (lane == 63) {
+          double* bw = bnd + 3 * jl;
+          bw[0] = bM;
+          bw[1] = bX;
+          bw[2] = (bM + bX) + bY;
+        }
       }
     }
     yofs += (unsigned)sizeof(BplaPos);
@@ -732,6 +765,10 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
       map_pair(64 * (s + 1) + lane, pn, okan, okbn, fbn, xi);
       xnA = P.xtab[xi];
       xnB = P.xtab[okbn ? xi + 1 : xi];
+    } else {
+      // the drain: a lane that wraps past the last strip holds no rows (its
+      // cells there are computed, FULL, and must not be handed on)
+      okan = okbn = false;
     }
     const int tend = s < nstrips ? min(Ws + Lys, T) : 0;
     int t = Ws + 64;

@@ -128,7 +128,7 @@ hipError_t launch_str_fast(const StrFastLaunch& P, int grid, int nwaves, hipStre
 // (dyadic profile columns only, see bpla.hip): x role v = u_l / xs with
 // u_l = sum_k table[k][l] x_k, y role v = y_l / ys, so LAScore = sum_l
 // v_x[l] v_y[l]; pr, pl, pu: sqrt p_right, p_left, p_unpair.
-struct BplaPos {
+struct alignas(16) BplaPos {  // 16-B aligned: three ds_read_b128 with immediate offsets
   double v[4];
   float pr, pl, pu, dyadic;
 };
@@ -293,7 +293,7 @@ hipError_t launch_str(const StrLaunch& P, int grid, int nwaves, hipStream_t st);
 constexpr size_t kBplaExpLds = 1024 * 8;
 // a wave's chunk of pairs streamed back to back: per pair {xtab base,
 // length, first row, -} and its K sum
-constexpr int kBplaChunkMax = 8;
+constexpr int kBplaChunkMax = 16;
 // y-grouped fast kernel: at most 12 waves per workgroup, 3 per SIMD (the
 // two-row exp path holds two rows' operands and state: up to 168 VGPRs)
 #ifndef SK_BPLA_ITEMS_WAVES
