@@ -658,15 +658,28 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
 
   // interior step: lane 0's column jb, every lane active
   // (the boundary row holds {M, X, M + X + Y} of row B per column)
-  auto interior = [&](int jb, double& dM, double& dX, double& dS, double& uM, double& uX, double& uS)
-                      __attribute__((always_inline)) {
-    (void)dM;
-    (void)dX;
-    const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+  // Interior operands are read a step ahead (the y column and lane 0's
+  // boundary values of the next step land during this step's arithmetic):
+  // (yc, b*) this step's, (ycn, n*) the next step's.
+  auto iload = [&](int jb, BplaPos& yc, double& b0, double& b1, double& b2) __attribute__((always_inline)) {
+    yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
     const double* bj = bnd + 3 * jb;
-    uM = wave_shr1(bM, bj[0]);
-    uX = wave_shr1(bX, bj[1]);
-    uS = wave_shr1((bM + bX) + bY, bj[2]);
+    b0 = bj[0];
+    b1 = bj[1];
+    b2 = bj[2];
+  };
+  auto interior = [&](int jb, double& dS, double& uS, const BplaPos& yc, double b0, double b1, double b2,
+                      BplaPos& ycn, double& n0, double& n1, double& n2) __attribute__((always_inline)) {
+    ycn = *reinterpret_cast<const BplaPos*>(ybase + yofs + (unsigned)sizeof(BplaPos));
+    {
+      const double* bj = bnd + 3 * (jb + 1);
+      n0 = bj[0];
+      n1 = bj[1];
+      n2 = bj[2];
+    }
+    const double uM = wave_shr1(bM, b0);
+    const double uX = wave_shr1(bX, b1);
+    uS = wave_shr1((bM + bX) + bY, b2);
     cells(yc, dS, uM, uX, false);
     if (lane == 63) {  // lane 63's column is jb - 63
       double* bw = bnd + 3 * (jb - 63);
@@ -695,9 +708,13 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
     (void)dX;
     const bool wrap = lane == w;
     if (wrap) {
-      const double h = (okA ? accA : 0.0) + (okB ? accB : 0.0);
-      if (okA) ksum[p] += h;
-      accA = accB = 0.0;
+      // the finished rows' sums stay in the lane while its next rows belong
+      // to the same pair; they go to the pair's sum when the pair changes
+      const double h = accA + (okB ? accB : 0.0);
+      const bool cont = okA && okan && pn == p;
+      if (okA && !cont) ksum[p] += h;
+      accA = cont ? h : 0.0;
+      accB = 0.0;
       xA = xnA;
       xB = xnB;
       p = pn;
@@ -772,15 +789,18 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
     }
     const int tend = s < nstrips ? min(Ws + Lys, T) : 0;
     int t = Ws + 64;
-    for (; t + 1 < tend; t += 2) {
-      interior(t - Ws + 1, pM, pX, pY, qM, qX, qY);
-      interior(t - Ws + 2, qM, qX, qY, pM, pX, pY);
-    }
     if (t < tend) {
-      interior(t - Ws + 1, pM, pX, pY, qM, qX, qY);
-      pM = qM;
-      pX = qX;
-      pY = qY;
+      BplaPos yc0, yc1;
+      double a0, a1, a2, c0, c1, c2;
+      iload(t - Ws + 1, yc0, a0, a1, a2);
+      for (; t + 1 < tend; t += 2) {
+        interior(t - Ws + 1, pY, qY, yc0, a0, a1, a2, yc1, c0, c1, c2);
+        interior(t - Ws + 2, qY, pY, yc1, c0, c1, c2, yc0, a0, a1, a2);
+      }
+      if (t < tend) {
+        interior(t - Ws + 1, pY, qY, yc0, a0, a1, a2, yc1, c0, c1, c2);
+        pY = qY;
+      }
     }
   }
   // the rows still held
