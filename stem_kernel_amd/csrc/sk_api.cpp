@@ -1076,7 +1076,11 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   for (int64_t k = 0; k < n; ++k) n_fast += is_fast(k);
   // fast pairs grouped by y (a workgroup stages one y for all its waves)
   // when the y's repeat enough; else one pair per wave
+  // items: runs of one y of at most SK_BPLA_ITEM pairs (default 16 per wave
+  // of a full workgroup)
   constexpr int kItemWaves = 8;
+  static const int item_max = std::getenv("SK_BPLA_ITEM") ? std::max(1, std::atoi(std::getenv("SK_BPLA_ITEM")))
+                                                          : 16 * sk::kBplaItemsWavesMax;
   std::vector<int2> items;
   {
     std::vector<int32_t> ycnt;
@@ -1113,10 +1117,10 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
           py.push_back(y[k]);
           oidx.push_back(k);
         }
-      if (group)  // runs of one y, at most 16 pairs per wave
+      if (group)  // runs of one y
         for (int64_t a = 0; a < n_fast;) {
           int64_t b = a;
-          while (b < n_fast && py[b] == py[a] && b - a < 16 * kItemWaves) ++b;
+          while (b < n_fast && py[b] == py[a] && b - a < item_max) ++b;
           items.push_back(make_int2((int)a, (int)(b - a)));
           a = b;
         }
@@ -1191,7 +1195,7 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
       F.n_items = (int32_t)items.size();
       // pairs a wave streams back to back (SK_BPLA_CHUNK: 1..kBplaChunkMax)
       // (0: per item, as many as give each wave one chunk)
-      F.chunk = 4;
+      F.chunk = 8;  // C4, items of 192 pairs: 7.99 ms per launch against 8.58 (4) and 8.97 (16)
       if (const char* e = std::getenv("SK_BPLA_CHUNK")) F.chunk = std::atoi(e);
       F.chunk = std::min(std::max(F.chunk, 0), sk::kBplaChunkMax);
       // waves per workgroup and workgroups per CU (SK_BPLA_IWAVES /
