@@ -174,6 +174,9 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_SEGSUM  // MATCH: same-parent runs summed per quad before the atomic (0 = off)
 #define SK_SEGSUM 1
 #endif
+#ifndef SK_SEGSUM_MAXK  // the widest class that sums runs per quad
+#define SK_SEGSUM_MAXK 20
+#endif
 #ifndef SK_SKIP_LOOPS  // cost experiment only (wrong results): loop rows (1) / rows with only gamma children (2) skip MATCH and the sweep
 #define SK_SKIP_LOOPS 0
 #endif
@@ -238,19 +241,33 @@ __device__ __forceinline__ double row_ld(__amdgpu_buffer_rsrc_t r, int lane, int
 // S[k] += eg0 * r0[lane + 64k] + eg1 * r1[lane + 64k]: every load of both rows
 // is issued before the first is consumed (one memory round trip, not one per
 // slot).
+// The widest classes (MAXK > SK_HALF_A) load the two rows in two halves of
+// slots: half the peak registers of phase A (which otherwise holds S and
+// both rows at once) for a second memory round trip.
+#ifndef SK_HALF_A
+#define SK_HALF_A 64  // off: C5 90.7k against 89.5k pairs/s halved (tools/ab.sh, r03l)
+#endif
+#ifndef SK_HALF_D  // phase D likewise
+#define SK_HALF_D 64
+#endif
 template <int MAXK>
 __device__ __forceinline__ void add_rows2(double (&S)[MAXK], __amdgpu_buffer_rsrc_t r0,
                                           __amdgpu_buffer_rsrc_t r1, double eg0, double eg1,
                                           int lane) {
-  double a[MAXK], b[MAXK];
+  constexpr int H = MAXK > SK_HALF_A ? MAXK / 2 : MAXK;
 #pragma unroll
-  for (int k = 0; k < MAXK; ++k) {
-    a[k] = row_ld(r0, lane, k);
-    b[k] = row_ld(r1, lane, k);
+  for (int h0 = 0; h0 < MAXK; h0 += H) {
+    double a[H], b[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      a[k] = h0 + k < MAXK ? row_ld(r0, lane, h0 + k) : 0.0;
+      b[k] = h0 + k < MAXK ? row_ld(r1, lane, h0 + k) : 0.0;
+    }
+    SCHED_FENCE();
+#pragma unroll
+    for (int k = 0; k < H; ++k)
+      if (h0 + k < MAXK) S[h0 + k] += eg0 * a[k] + eg1 * b[k];
   }
-  SCHED_FENCE();
-#pragma unroll
-  for (int k = 0; k < MAXK; ++k) S[k] += eg0 * a[k] + eg1 * b[k];
 }
 
 // One (x,y) pair on one wavefront.
@@ -614,7 +631,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
               // this round's reads into a branch)
               const double w = g[u] * rv[u] * (ok ? 1.0 : 0.0);
               const int h = ok ? (int)((e[u] >> 11) & 0x7ff) - q0 : lane;
-              if constexpr (SK_SEGSUM && MAXK <= 20) {
+              if constexpr (SK_SEGSUM && MAXK <= SK_SEGSUM_MAXK) {
                 // Node-major edges put a parent's edges in adjacent lanes:
                 // each run is summed within its quad (DPP quad_perm,
                 // Hillis-Steele on contiguous keys) and only the run's last
@@ -777,45 +794,43 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // element q of this row is by the same lane (q = lane + 64k), so
     // per-thread program order makes it visible: no fence.  A row nobody
     // reads (a root) is not stored; it is no child of the next row either.
+    // (the widest classes read G1 back in two halves: fewer live registers)
+    constexpr int HD = MAXK > SK_HALF_D ? MAXK / 2 : MAXK;
     if (pslot == 0xffffu) {
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) S[k] = egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
     } else if (pslot == 0xfffeu) {
       // read only by the next row, from registers: not stored
       const double cw = combo ? 1.0 : xwg;
-      double g1[MAXK];
-      if (combo) {
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) g1[k] = 0.0;
-      } else {
+      for (int h0 = 0; h0 < MAXK; h0 += HD) {
+        double g1[HD];
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) g1[k] = R[lane + 64 * k];
+        for (int k = 0; k < HD; ++k) g1[k] = combo ? 0.0 : R[lane + 64 * (h0 + k)];
+        SCHED_FENCE();
+#pragma unroll
+        for (int k = 0; k < HD; ++k)
+          S[h0 + k] = egd * (g1[k] + cw * S[h0 + k]) + egt0 * T0[h0 + k] + (NPF >= 2 ? egt1 * T1[h0 + k] : 0.0);
       }
-      SCHED_FENCE();
-#pragma unroll
-      for (int k = 0; k < MAXK; ++k)
-        S[k] = egd * (g1[k] + cw * S[k]) + egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
     } else {
       double* __restrict__ orow = slab + (size_t)pslot * stride + lane;
       // all R reads issued before the first store (one LDS round trip)
-      double g1[MAXK];
       const double cw = combo ? 1.0 : xwg;
-      if (combo) {
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) g1[k] = 0.0;
-      } else {
+      for (int h0 = 0; h0 < MAXK; h0 += HD) {
+        double g1[HD];
 #pragma unroll
-        for (int k = 0; k < MAXK; ++k) g1[k] = R[lane + 64 * k];
-      }
-      SCHED_FENCE();
+        for (int k = 0; k < HD; ++k) g1[k] = combo ? 0.0 : R[lane + 64 * (h0 + k)];
+        SCHED_FENCE();
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k) {
-        const double o = g1[k] + cw * S[k];
+        for (int k = 0; k < HD; ++k) {
+          const double o = g1[k] + cw * S[h0 + k];
 #ifndef SK_XNOSTORE
-        orow[64 * k] = o;
+          orow[64 * (h0 + k)] = o;
 #endif
-        // the next row's partial sum: itself (distance-1) + prefetched rows
-        S[k] = egd * o + egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
+          // the next row's partial sum: itself (distance-1) + prefetched rows
+          S[h0 + k] = egd * o + egt0 * T0[h0 + k] + (NPF >= 2 ? egt1 * T1[h0 + k] : 0.0);
+        }
       }
     }
     done = nxt_done;
