@@ -37,9 +37,10 @@ Ranks: under torchrun (RANK set) each process is one rank; ``--gpus N``
 without a launcher starts its own N worker processes (spawn_ranks) before any
 GPU call, so ``python3 bench.py --gpus 8`` runs as-is.
 
-Roofline: see roofline() -- measured HBM bytes (profiles/<kind>_traffic.json,
+Roofline: see roofline() -- measured HBM bytes (profiles/<config>_traffic.json,
 stamped with the kernel source hash; stale profiles are not used) over the
-launches' span for the HBM-bound kernels, the survey model beside it.
+launches' span for the HBM-bound kernels, the survey model beside it
+(profiles/<config>_traffic.json, stamped with the kernel source hash).
 """
 from __future__ import annotations
 
@@ -156,11 +157,11 @@ def algorithmic(kind, shapes, x, y):
         24.0 * float(np.sum(lens[x].astype(np.float64) * lens[y]))
 
 
-def load_profile(kind, length, path=None):
-    """profiles/<kind>_traffic.json (tools/measure.sh -> tools/profile_summary.py)
+def load_profile(config, kind, length, path=None):
+    """profiles/<config>_traffic.json (tools/measure.sh -> tools/profile_summary.py)
     and whether it was measured on these kernel sources (provenance hash)."""
     from stem_kernel_amd import provenance
-    path = path or os.path.join(ROOT, "profiles", f"{kind}_traffic.json")
+    path = path or os.path.join(ROOT, "profiles", f"{config}_traffic.json")
     try:
         with open(path) as f:
             pm = json.load(f)
@@ -171,7 +172,7 @@ def load_profile(kind, length, path=None):
     return pm, pm.get("source_hash") == provenance.source_hash(), path
 
 
-def roofline(kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, cells, pmc_json=None):
+def roofline(config, kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, cells, pmc_json=None):
     """The dominant kernel's roofline.
 
     HBM-bound kernels (DAG stem, 4-D stem): the headline `achieved` is the
@@ -190,7 +191,7 @@ def roofline(kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, cells, pmc
     eff_s = span_ms / n_launch * 1e-3
     alg_pl = alg / n_launch
     scale = 1e9 if unit == "GB/s" else 1e12
-    pm, fresh, path = load_profile(kind, length, pmc_json)
+    pm, fresh, path = load_profile(config, kind, length, pmc_json)
     rel = os.path.relpath(path, ROOT)
     traffic = None
     if pm is not None and pm.get("hbm_bytes_per_cell"):
@@ -603,7 +604,7 @@ def main():
         # by sk_last_timing
         rf = None
         if not a.cpu_stub:
-            rf = roofline(kind, a.length, shapes, xs, ys, float(np.sum(k_ms)), float(np.sum(l_ms)),
+            rf = roofline(a.config, kind, a.length, shapes, xs, ys, float(np.sum(k_ms)), float(np.sum(l_ms)),
                           int(np.sum(launches)), cells, a.pmc_json)
             rf["kernel"] = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
                             "stem4d": "sk_stem4d_kernel", "bpla": "sk_bpla_fast_kernel"}[kind]

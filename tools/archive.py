@@ -40,8 +40,9 @@ def main():
         for f in glob.glob(os.path.join(run, name, "**", "*counter_collection.csv"), recursive=True):
             rows(f, os.path.join(prof, f"{tag}_pmc_{name.lower()}.csv"), sk)
     for f in glob.glob(os.path.join(run, "*_traffic.json")):
-        shutil.copy(f, os.path.join(prof, os.path.basename(f)))
-        shutil.copy(f, os.path.join(prof, f"{tag}_{os.path.basename(f)}"))
+        cfg = json.load(open(f))["config"]
+        shutil.copy(f, os.path.join(prof, f"{cfg}_traffic.json"))
+        shutil.copy(f, os.path.join(prof, f"{tag}_traffic.json"))
     print("archived", tag)
 
 

@@ -2,7 +2,7 @@
 # One measurement round trip on the GPU box (run from the repo root through
 # gpurun):  [GPU parity suite + smoke], rocprofv3 kernel trace + stats of the
 # bench, FETCH_SIZE / WRITE_SIZE / LDS counter passes (one rocprofv3 run
-# each), tools/profile_summary.py -> profiles/<kind>_traffic.json (stamped
+# each), tools/profile_summary.py -> profiles/<config>_traffic.json (stamped
 # with the source hash), then the plain bench line, which reads that file.
 # Usage: tools/measure.sh CONFIG TAG [--tests]
 set -o pipefail
@@ -35,8 +35,8 @@ run_pmc() {  # name counters...
 run_pmc FETCH_SIZE FETCH_SIZE || exit 1
 run_pmc WRITE_SIZE WRITE_SIZE || exit 1
 run_pmc LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE || exit 1
-python3 tools/profile_summary.py $OUT $CFG $KSUB $OUT/${KIND}_traffic.json > $OUT/summary.log 2>&1 || { tail -20 $OUT/summary.log; exit 1; }
-cp $OUT/${KIND}_traffic.json profiles/${KIND}_traffic.json
+python3 tools/profile_summary.py $OUT $CFG $KSUB $OUT/${CFG}_traffic.json > $OUT/summary.log 2>&1 || { tail -20 $OUT/summary.log; exit 1; }
+cp $OUT/${CFG}_traffic.json profiles/${CFG}_traffic.json
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 timeout -k 10 500 python3 -u bench.py --config $CFG > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log | cut -c1-300

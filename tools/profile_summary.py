@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Fold one tools/measure.sh run into profiles/<kind>_traffic.json.
+"""Fold one tools/measure.sh run into profiles/<config>_traffic.json.
 
 Inputs (OUTDIR from tools/measure.sh):
   prof/         rocprofv3 --kernel-trace --stats of bench.py (default steps)
