@@ -1051,76 +1051,86 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
              const int32_t* x, const int32_t* y, int64_t n, double* out_dev) {
   const bool bp = kp->kind == SK_BPLA || kp->kind == SK_BPLA_SW;
   const bool sw = kp->kind == SK_BPLA_SW || kp->kind == SK_LA_SW;
-  double cells = 0.0;
-  for (int64_t k = 0; k < n; ++k) {
-    const Example& ex = xs_->ex[x[k]];
-    const Example& ey = ys_->ex[y[k]];
-    // BPLAScore reads p_left/p_right/p_unpair, which MData(ma) leaves empty
-    if (bp && (!ex.has_bp || !ey.has_bp))
-      return fail(ctx, SK_ERR_INVALID, "BPLA with base pairs needs examples built with use_bp");
-    cells += (double)ex.len * (double)ey.len;
-  }
-  ctx->last_cells = cells;
+  // SK_HOST_STATS: host time per phase (diagnostic)
+  static const bool host_stats = std::getenv("SK_HOST_STATS") != nullptr;
+  auto now_ms = [] {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  const double tb0 = host_stats ? now_ms() : 0.0;
+  double tb1 = tb0, tb2 = tb0;
   const HostPack& PX = xs_->pack;
   const HostPack& PY = ys_->pack;
-  // pairs whose profiles are all dyadic take the fast kernel (tabulated
-  // LAScore factors); the rest the general one.  Fast pairs first, the
-  // permutation undone through oidx.
+  // per-example lengths and flags once (the pair loops below touch only
+  // these small arrays, not the examples)
+  const bool general_only = std::getenv("SK_BPLA_GENERAL") != nullptr;  // A/B switch
+  auto ex_info = [&](const sk_dataset* d, const HostPack& H, std::vector<int32_t>& len,
+                     std::vector<uint8_t>& ok, std::vector<uint8_t>& dy) {
+    const size_t m = d->ex.size();
+    len.resize(m);
+    ok.resize(m);
+    dy.resize(m);
+    for (size_t i = 0; i < m; ++i) {
+      len[i] = d->ex[i].len;
+      ok[i] = !bp || d->ex[i].has_bp;  // BPLAScore reads p_left/p_right/p_unpair
+      dy[i] = !general_only && H.ex_dyadic[i];
+    }
+  };
+  std::vector<int32_t> lx, ly;
+  std::vector<uint8_t> okx, oky, dyx, dyy;
+  ex_info(xs_, PX, lx, okx, dyx);
+  ex_info(ys_, PY, ly, oky, dyy);
+  // one pass: cells, validity, fast flags, per-y counts of the fast pairs
+  // (fast: both profiles dyadic -- the fast kernel with tabulated LAScore
+  // factors; the rest the general one)
+  std::vector<uint8_t> fastk((size_t)n);
+  std::vector<int32_t> ycnt(ys_->ex.size(), 0);
+  double cells = 0.0;
+  int64_t n_fast = 0, distinct = 0;
+  for (int64_t k = 0; k < n; ++k) {
+    const int32_t a = x[k], b = y[k];
+    if (!okx[a] || !oky[b])
+      return fail(ctx, SK_ERR_INVALID, "BPLA with base pairs needs examples built with use_bp");
+    cells += (double)lx[a] * (double)ly[b];
+    const uint8_t f = dyx[a] & dyy[b];
+    fastk[(size_t)k] = f;
+    n_fast += f;
+    if (f && ycnt[b]++ == 0) ++distinct;
+  }
+  ctx->last_cells = cells;
+  // Fast pairs first, the permutation undone through oidx; fast pairs
+  // grouped by y (a workgroup stages one y for all its waves) when the y's
+  // repeat enough, else one pair per wave.  Items: runs of one y of at most
+  // SK_BPLA_ITEM pairs (default 16 per wave of a full workgroup).
   std::vector<int32_t> px, py;
   std::vector<int64_t> oidx;
-  int64_t n_fast = 0;
-  const bool general_only = std::getenv("SK_BPLA_GENERAL") != nullptr;  // A/B switch
-  auto is_fast = [&](int64_t k) {
-    return !general_only && PX.ex_dyadic[x[k]] && PY.ex_dyadic[y[k]];
-  };
-  for (int64_t k = 0; k < n; ++k) n_fast += is_fast(k);
-  // fast pairs grouped by y (a workgroup stages one y for all its waves)
-  // when the y's repeat enough; else one pair per wave
-  // items: runs of one y of at most SK_BPLA_ITEM pairs (default 16 per wave
-  // of a full workgroup)
   constexpr int kItemWaves = 8;
   static const int item_max = std::getenv("SK_BPLA_ITEM") ? std::max(1, std::atoi(std::getenv("SK_BPLA_ITEM")))
                                                           : 16 * sk::kBplaItemsWavesMax;
   std::vector<int2> items;
   {
-    std::vector<int32_t> ycnt;
-    int64_t distinct = 0;
-    ycnt.assign(ys_->ex.size(), 0);
-    for (int64_t k = 0; k < n; ++k)
-      if (is_fast(k) && ycnt[y[k]]++ == 0) ++distinct;
     const bool group = n_fast >= 4 * kItemWaves * std::max<int64_t>(distinct, 1) &&
                        !std::getenv("SK_BPLA_NO_ITEMS");
     const bool permute = n_fast != n || group;
     if (permute && n_fast) {
-      px.reserve(n);
-      py.reserve(n);
-      oidx.reserve(n);
-      std::vector<int64_t> fast(n_fast);
-      if (group) {  // stable counting sort by y (ycnt holds the per-y counts)
-        std::vector<int64_t> pos(ys_->ex.size() + 1, 0);
+      px.resize((size_t)n);
+      py.resize((size_t)n);
+      oidx.resize((size_t)n);
+      // fast pairs in y order (stable counting sort) or in call order, then
+      // the general ones
+      std::vector<int64_t> pos(ys_->ex.size() + 1, 0);
+      if (group)
         for (size_t j = 0; j < ys_->ex.size(); ++j) pos[j + 1] = pos[j] + ycnt[j];
-        for (int64_t k = 0; k < n; ++k)
-          if (is_fast(k)) fast[pos[y[k]]++] = k;
-      } else {
-        int64_t f = 0;
-        for (int64_t k = 0; k < n; ++k)
-          if (is_fast(k)) fast[f++] = k;
+      int64_t f = 0, g = n_fast;
+      for (int64_t k = 0; k < n; ++k) {
+        const int64_t d = fastk[(size_t)k] ? (group ? pos[y[k]]++ : f++) : g++;
+        px[(size_t)d] = x[k];
+        py[(size_t)d] = y[k];
+        oidx[(size_t)d] = k;
       }
-      for (int64_t k : fast) {
-        px.push_back(x[k]);
-        py.push_back(y[k]);
-        oidx.push_back(k);
-      }
-      for (int64_t k = 0; k < n; ++k)
-        if (!is_fast(k)) {
-          px.push_back(x[k]);
-          py.push_back(y[k]);
-          oidx.push_back(k);
-        }
       if (group)  // runs of one y
         for (int64_t a = 0; a < n_fast;) {
           int64_t b = a;
-          while (b < n_fast && py[b] == py[a] && b - a < item_max) ++b;
+          while (b < n_fast && py[(size_t)b] == py[(size_t)a] && b - a < item_max) ++b;
           items.push_back(make_int2((int)a, (int)(b - a)));
           a = b;
         }
@@ -1128,6 +1138,7 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
       y = py.data();
     }
   }
+  if (host_stats) tb1 = now_ms();
   const bool permute = !oidx.empty();
   const size_t nb = (size_t)n;
   const size_t npx = PX.pos_prof.size(), npy = ys_ == xs_ ? 0 : PY.pos_prof.size();
@@ -1166,6 +1177,7 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   T.bp = bp ? 1 : 0;
   T.oidx = d_oidx;
   T.out = out_dev;
+  if (host_stats) tb2 = now_ms();
   SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
   if (n_fast) {
     // x-role table of the x set, y-role table of the y set
@@ -1250,12 +1262,16 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
     SK_HIP(ctx, sk::lev_mark(ctx, S));
   }
   SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
+  const double tb3 = host_stats ? now_ms() : 0.0;
   SK_HIP(ctx, hipStreamSynchronize(S));
   SK_HIP(ctx, sk::lev_collect(ctx));
   float ms = 0.f;
   SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_stem_ms = ms;
   ctx->last_launches = (n_fast ? 1 : 0) + (n_fast < n ? 1 : 0);
+  if (host_stats)
+    fprintf(stderr, "[sk bpla host] plan %.3f ms, uploads %.3f ms, launches %.3f ms, wait %.3f ms (GPU %.3f ms)\n",
+            tb1 - tb0, tb2 - tb1, tb3 - tb2, now_ms() - tb3, (double)ms);
   return SK_OK;
 }
 
