@@ -1,0 +1,47 @@
+// Calibration of rocprofv3's FETCH_SIZE / WRITE_SIZE for the access widths
+// the engine's kernels use (MI355X_MICROARCH.md: FETCH_SIZE counts half the
+// bytes of a 16-B-per-lane streaming read; other widths uncalibrated).
+// Reads (or writes) a 1 GiB buffer -- four times the 256 MiB Infinity Cache --
+// once, coalesced, with 8 or 16 bytes per lane; the counters of each launch
+// are compared with the 1 GiB it moves (tools/calib/run.sh).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+__global__ void read8(const double* __restrict__ a, size_t n, double* out) {
+  double s = 0.0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    s += a[i];
+  if (s == 12345.678) out[0] = s;  // keeps the loads
+}
+
+__global__ void read16(const double2* __restrict__ a, size_t n, double* out) {
+  double s = 0.0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const double2 v = a[i];
+    s += v.x + v.y;
+  }
+  if (s == 12345.678) out[0] = s;
+}
+
+__global__ void write8(double* __restrict__ a, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    a[i] = (double)i;
+}
+
+int main() {
+  const size_t bytes = (size_t)1 << 30;
+  double* a = nullptr;
+  double* out = nullptr;
+  if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
+  const size_t n8 = bytes / 8;
+  hipLaunchKernelGGL(write8, dim3(4096), dim3(256), 0, 0, a, n8);
+  hipLaunchKernelGGL(read8, dim3(4096), dim3(256), 0, 0, a, n8, out);
+  hipLaunchKernelGGL(read16, dim3(4096), dim3(256), 0, 0, reinterpret_cast<const double2*>(a), n8 / 2, out);
+  if (hipDeviceSynchronize() != hipSuccess) return 2;
+  std::printf("moved %zu bytes per launch (write8, read8, read16)\n", bytes);
+  (void)hipFree(a);
+  (void)hipFree(out);
+  return 0;
+}

@@ -1,0 +1,17 @@
+#!/bin/bash
+# FETCH_SIZE / WRITE_SIZE calibration on the GPU box (see fetch_calib.hip).
+set -o pipefail
+OUT=gpurun_out/calib; mkdir -p $OUT; export TMPDIR=/tmp
+ROOT=$(pwd)
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 60 rocprofv3 --pmc $c -d $ROOT/$OUT/$c -o run --output-format csv -- $ROOT/tools/calib/fetch_calib > $OUT/$c.log 2>&1 || { tail -5 $OUT/$c.log; exit 1; }
+done
+python3 - <<'PY'
+import csv, glob
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    for f in glob.glob(f"gpurun_out/calib/{c}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == c:
+                kb = float(r["Counter_Value"])
+                print(c, r["Kernel_Name"].split("(")[0], "KiB", kb, "ratio to 1 GiB", kb * 1024 / 2**30)
+PY
