@@ -233,6 +233,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* base, i
                                            0x00020000);
 }
 
+typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+
 // element lane + 64k of a row
 __device__ __forceinline__ double row_ld(__amdgpu_buffer_rsrc_t r, int lane, int k) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8, k * 512, 0));
@@ -813,7 +815,13 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
           S[h0 + k] = egd * (g1[k] + cw * S[h0 + k]) + egt0 * T0[h0 + k] + (NPF >= 2 ? egt1 * T1[h0 + k] : 0.0);
       }
     } else {
+#ifdef SK_FULL_STORE
       double* __restrict__ orow = slab + (size_t)pslot * stride + lane;
+#else
+      // stores through the slot's buffer resource: the padded tail (q >=
+      // NLy, never read) is dropped by the range check, not written
+      const __amdgpu_buffer_rsrc_t orsrc = row_rsrc(slab + (size_t)pslot * stride, NLy);
+#endif
       // all R reads issued before the first store (one LDS round trip)
       const double cw = combo ? 1.0 : xwg;
 #pragma unroll
@@ -826,7 +834,12 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
         for (int k = 0; k < HD; ++k) {
           const double o = g1[k] + cw * S[h0 + k];
 #ifndef SK_XNOSTORE
+#ifdef SK_FULL_STORE
           orow[64 * (h0 + k)] = o;
+#else
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), orsrc, lane * 8,
+                                                (h0 + k) * 512, 0);
+#endif
 #endif
           // the next row's partial sum: itself (distance-1) + prefetched rows
           S[h0 + k] = egd * o + egt0 * T0[h0 + k] + (NPF >= 2 ? egt1 * T1[h0 + k] : 0.0);
@@ -980,7 +993,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
         c0 = __builtin_amdgcn_readfirstlane(c0);
         if (c0 < Y.nch) iy_sweep(Y, R, c0, lane);
         double* grow = gamtab + (size_t)g * (64 * MAXK);
-        for (int k = 0; k < MAXK; ++k) grow[lane + 64 * k] = R[lane + 64 * k];
+        for (int k = 0; k < MAXK; ++k)
+          if (lane + 64 * k < Y.nl) grow[lane + 64 * k] = R[lane + 64 * k];  // (the tail is never read)
         wave_sync();
       }
       __syncthreads();  // the table and kappa, for every wave's pairs
@@ -1062,7 +1076,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
           if (c0 < Y.nch) iy_sweep(Y, R, c0, lane);
           double* prow = phitab + (size_t)idx * (64 * MAXK);
 #pragma unroll
-          for (int k = 0; k < MAXK; ++k) prow[lane + 64 * k] = R[lane + 64 * k];
+          for (int k = 0; k < MAXK; ++k)
+            if (lane + 64 * k < Y.nl) prow[lane + 64 * k] = R[lane + 64 * k];
           wave_sync();
         }
         __syncthreads();

@@ -891,11 +891,35 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
           P.ex_phi_bits[base + P.phk_idx[j] / 64] |= 1ull << (P.phk_idx[j] % 64);
       }
       if (std::getenv("SK_PACK_STATS")) {  // diagnostic: rows, unstored rows, slots
-        static long s_rows = 0, s_nost = 0, s_slots = 0;
+        static long s_rows = 0, s_nost = 0, s_slots = 0, s_nodes = 0, s_st = 0, s_slab = 0, s_gam = 0,
+                    s_phi = 0, s_reg = 0;
         s_rows += nlxg;
+        s_nodes += nn;
         for (int v = 0; v < nn; ++v) s_nost += nostore[v];
         s_slots += gslots;
-        if (e + 1 == n) fprintf(stderr, "[sk pack] gamma schedule: %ld rows, %ld unstored, %ld slots\n", s_rows, s_nost, s_slots);
+        // row reads the kernel issues: slab / Gamma / Phi child records, minus
+        // the previous row (taken from registers); stored rows
+        {
+          uint32_t prev = 0xffffu;
+          size_t k = (size_t)P.ex_xgch_base.back();
+          for (size_t r = (size_t)P.ex_xg_base.back(); r < P.xgrow.size(); ++r) {
+            const int ne = P.xgrow[r].a & 0xff;
+            for (int t = 0; t < ne; ++t, ++k) {
+              const uint32_t c = P.xg_ch[k] & 0xffffu;
+              if (c == prev) ++s_reg;
+              else if (c & 0x8000u) ++s_gam;
+              else if (c & 0x4000u) ++s_phi;
+              else ++s_slab;
+            }
+            prev = P.xgrow[r].b >> 16;
+            s_st += prev < 0x4000u;
+          }
+        }
+        if (e + 1 == n)
+          fprintf(stderr,
+                  "[sk pack] gamma schedule: %ld nodes, %ld rows, %ld unstored, %ld slots; stored %ld, reads: "
+                  "slab %ld gamma %ld phi %ld, from registers %ld\n",
+                  s_nodes, s_rows, s_nost, s_slots, s_st, s_slab, s_gam, s_phi, s_reg);
       }
       if (gslots >= 0x4000) {  // slot ids share the record with the gamma / phi flags
         err = "too many live DAG rows";
