@@ -122,8 +122,13 @@ typedef __attribute__((address_space(3))) int32_t lds_i32;
 struct YView {  // the y example (staged in LDS unless noted)
   const uint4* __restrict__ nrg;  // node records {a, c, w, p0} (HBM, L2-resident)
   const lds_u32* sc;   // sweep schedule: (nch + 2) chunks of 64 child:11 | parent:11 | gaps:10
-  const lds_f64* ew;   // their weights gap^2 w(parent) g^gaps (0 for dummies)
+  const lds_f64* ew;   // their weights gap^2 w(parent) g^gaps (0 for dummies), or
+                       // (node_weights<MAXK>) per node gap^2 w(q), or
+  const lds_f32* ewf;  // (node_weights_f32<MAXK>) per node w(q): gap^2 w(q) g^gaps in the sweep
+  const lds_f64* gp;   // g^k
+  double gap2;
   const lds_u32* ed2;  // edges node-major (sorted ids)
+  const uint32_t* __restrict__ ed2g;  // the same in HBM (L2-resident; edges_global<MAXK>)
   const lds_i32* lfirst;  // length v -> first node (nodes sorted by length), v <= lmax+1
   const lds_i32* ycs;     // length v -> first sweep chunk reaching v, v <= lmax+1
   int lmax;               // largest node length of the example
@@ -186,6 +191,46 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
 #define SK_MU 3
 #endif
+#ifndef SK_NODEW_MIN  // the narrowest class whose sweep weights are per node (LDS for waves)
+#define SK_NODEW_MIN 20
+#endif
+// Sweep weights per y node (gap^2 w(q), 8 B per node; the widest classes
+// w(q) itself, the float, 4 B) instead of per schedule slot (8 B per slot of
+// (nch + 2) x 64): a third of the schedule's LDS, for one more LDS read per
+// slot (g^gaps) and the product(s) the staging formed (same operands, same
+// order: the same double).  The wide classes are LDS-bound in
+// waves per CU (C5's MAXK 24: 5 waves with slot weights, 7 without), so they
+// trade; MAXK 16 holds 8 waves either way (VGPRs).
+template <int MAXK>
+constexpr bool node_weights() {
+  return MAXK >= SK_NODEW_MIN;
+}
+#ifndef SK_NODEF_MIN  // the narrowest class whose node weights are the floats w(q)
+#define SK_NODEF_MIN 24
+#endif
+template <int MAXK>
+constexpr bool node_weights_f32() {
+  return node_weights<MAXK>() && MAXK >= SK_NODEF_MIN;
+}
+#ifndef SK_PW2_MIN  // the narrowest class whose MATCH passes are 128 nodes (LDS for waves)
+#define SK_PW2_MIN 24
+#endif
+// MATCH pass width in 64-node groups: SK_PW, 2 in the widest classes (the
+// per-wave accumulator is 64 * PW doubles of LDS)
+template <int MAXK>
+constexpr int pass_width() {
+  return MAXK >= SK_PW2_MIN ? 2 : SK_PW;
+}
+#ifndef SK_EDG_MIN  // the narrowest class whose MATCH reads the node-major edges from L2, not LDS
+#define SK_EDG_MIN 64  // off: C5 100.7k against 102.3k pairs/s (r03 A/B; MATCH 14.4k against 9.9k cycles per row)
+#endif
+// The node-major edges (4 B per edge) read by MATCH from HBM / L2 instead of
+// LDS: one more wave per CU in the widest classes, for an L2 round trip per
+// MATCH round (issued a round ahead).
+template <int MAXK>
+constexpr bool edges_global() {
+  return MAXK >= SK_EDG_MIN;
+}
 
 #ifdef SK_STAMPS
 #define STAMP(i)                                                  \
@@ -233,11 +278,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* base, i
                                            0x00020000);
 }
 
+// cache policy bits of the G0 row loads / stores (experiments: 2 = nt)
+#ifndef SK_ROW_LD_POL
+#define SK_ROW_LD_POL 0
+#endif
+#ifndef SK_ROW_ST_POL
+#define SK_ROW_ST_POL 0
+#endif
 typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
 
 // element lane + 64k of a row
 __device__ __forceinline__ double row_ld(__amdgpu_buffer_rsrc_t r, int lane, int k) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8, k * 512, 0));
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8, k * 512, SK_ROW_LD_POL));
 }
 
 // S[k] += eg0 * r0[lane + 64k] + eg1 * r1[lane + 64k]: every load of both rows
@@ -302,9 +354,17 @@ __device__ __forceinline__ void add_rows2(double (&S)[MAXK], __amdgpu_buffer_rsr
 // order, so nothing drains between chunks: only the data a lane consumes is
 // waited for.  Records are read two chunks ahead, weights one; dummy records
 // (weight 0) pad the chunks.  Ends with a wave barrier.
+template <bool NW, bool NWF>
 __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int lane) {
   const lds_u32* rp = Y.sc + c0 * 64 + lane;
-  const lds_f64* wp = Y.ew + c0 * 64 + lane;
+  const lds_f64* wp = Y.ew + (NW ? 0 : c0 * 64 + lane);
+  // NW: the slot's weight from its parent's node weight and g^gaps; a dummy
+  // (child == parent) weighs 0
+  auto nweight = [&](uint32_t rec) __attribute__((always_inline)) -> double {
+    const uint32_t pa = (rec >> 11) & 0x7ff;
+    const double w = (NWF ? Y.gap2 * (double)Y.ewf[pa] : Y.ew[pa]) * Y.gp[rec >> 22];
+    return ((rec ^ (rec >> 11)) & 0x7ff) == 0u ? 0.0 : w;
+  };
   // three chunk slots in rotation (the loop is unrolled by three, so no
   // loaded register is ever copied, which would force a wait for it)
   struct Ck {
@@ -313,8 +373,8 @@ __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int
   };
   Ck A, B, C;
   A.rec = rp[0];
-  A.w = wp[0];
   B.rec = rp[64];
+  A.w = NW ? nweight(A.rec) : wp[0];
   B.w = 0.0;
   C.rec = 0u;
   C.w = C.rv = B.rv = 0.0;
@@ -324,7 +384,7 @@ __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int
   // chunk X now, Y next, Z after: false after the last chunk
   auto step = [&](Ck& X, Ck& Yc, Ck& Z) __attribute__((always_inline)) -> bool {
     Z.rec = rp[128];
-    Yc.w = wp[64];
+    Yc.w = NW ? nweight(Yc.rec) : wp[64];
     __hip_atomic_fetch_add(&R[(X.rec >> 11) & 0x7ff], X.rv * X.w, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WAVEFRONT);
     Yc.rv = R[Yc.rec & 0x7ff];
@@ -356,6 +416,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
                             const lds_f64* kap, const double* __restrict__ phitab,
                             const double* __restrict__ phikap) {
   constexpr int stride = 64 * MAXK;
+  constexpr int PW = pass_width<MAXK>();
   const DevSet& s = P.xset;
   const DevSet& ys = P.yset;
   const double* __restrict__ yPg = ys.yn_P + Y.nb;  // path counts of y (HBM, L2-resident)
@@ -460,17 +521,17 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     }
     qa = __builtin_amdgcn_readfirstlane(qa);
     qb = __builtin_amdgcn_readfirstlane(qb);
-    uint4 nd_first[SK_PW];
-    double Pq_first[SK_PW];
+    uint4 nd_first[PW];
+    double Pq_first[PW];
 #pragma unroll
-    for (int j = 0; j < SK_PW; ++j) {
+    for (int j = 0; j < PW; ++j) {
       nd_first[j] = make_uint4(0u, 0u, 0u, 0u);
       Pq_first[j] = 0.0;
     }
     if (qa < qb) {
 #pragma unroll
-      for (int j = 0; j < SK_PW; ++j) {
-        const int qf = min(max(qb - 64 * SK_PW, qa) + 64 * j + lane, qb - 1);
+      for (int j = 0; j < PW; ++j) {
+        const int qf = min(max(qb - 64 * PW, qa) + 64 * j + lane, qb - 1);
         nd_first[j] = Y.nrg[qf];
         Pq_first[j] = yPg[qf];
       }
@@ -565,43 +626,43 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     if (!combo && qa < qb && !(SK_SKIP_LOOPS && skipr)) {
       // node records and path counts come from HBM (L2-resident per y),
       // the first pass's issued before A, each later pass's during the
-      // pass before.  A pass covers NW = 64*SK_PW nodes [q0, top], lane l
+      // pass before.  A pass covers NW = 64*PW nodes [q0, top], lane l
       // scoring nodes q0 + 64j + l.
-      constexpr int NW = 64 * SK_PW;
+      constexpr int NW = 64 * PW;
       int top = qb - 1, q0 = max(top - NW + 1, qa);
-      uint4 nd_n[SK_PW];
-      double Pq_n[SK_PW];
+      uint4 nd_n[PW];
+      double Pq_n[PW];
 #pragma unroll
-      for (int j = 0; j < SK_PW; ++j) {
+      for (int j = 0; j < PW; ++j) {
         nd_n[j] = nd_first[j];
         Pq_n[j] = Pq_first[j];
       }
       for (;;) {
-        uint4 nd[SK_PW];
-        double Pq[SK_PW];
+        uint4 nd[PW];
+        double Pq[PW];
 #pragma unroll
-        for (int j = 0; j < SK_PW; ++j) {
+        for (int j = 0; j < PW; ++j) {
           nd[j] = nd_n[j];
           Pq[j] = Pq_n[j];
         }
         const int ntop = top - NW, nq0 = max(ntop - NW + 1, qa);
         if (ntop >= qa) {
 #pragma unroll
-          for (int j = 0; j < SK_PW; ++j) {
+          for (int j = 0; j < PW; ++j) {
             nd_n[j] = Y.nrg[min(nq0 + 64 * j + lane, ntop)];
             Pq_n[j] = yPg[min(nq0 + 64 * j + lane, ntop)];
           }
         }
         // node-score operands, requested ahead of the child sums
-        double co_v[SK_PW], gl_v[SK_PW];
+        double co_v[PW], gl_v[PW];
 #pragma unroll
-        for (int j = 0; j < SK_PW; ++j) {
+        for (int j = 0; j < PW; ++j) {
           co_v[j] = co[xcode + ((nd[j].y >> 16) & 0xf)];
           gl_v[j] = gp[nd[j].y & 0xffff];
         }
-        double Hq[SK_PW];  // x leaf child against a y stem: G0[leaf][*] = 0
+        double Hq[PW];  // x leaf child against a y stem: G0[leaf][*] = 0
 #pragma unroll
-        for (int j = 0; j < SK_PW; ++j) Hq[j] = 0.0;
+        for (int j = 0; j < PW; ++j) Hq[j] = 0.0;
         if (!xloop) {
           // edge range of nodes [q0, top]: E(q0) .. E(top) + n_edges(top),
           // 64*SK_MU edges per round: all reads of a round are issued
@@ -611,13 +672,27 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
           const int jt = (top - q0) >> 6;
           uint32_t ndt = nd[0].x;
 #pragma unroll
-          for (int j = 1; j < SK_PW; ++j) ndt = jt == j ? nd[j].x : ndt;
+          for (int j = 1; j < PW; ++j) ndt = jt == j ? nd[j].x : ndt;
           const uint32_t at = __builtin_amdgcn_readlane(ndt, (top - q0) & 63);
           const int eb = (int)((at & 0xffff) + ((at >> 16) & 0xff));
+          constexpr bool EG = edges_global<MAXK>();
+          uint32_t en[SK_MU];  // (EG) the round's edges, loaded a round ahead
+          if constexpr (EG) {
+#pragma unroll
+            for (int u = 0; u < SK_MU; ++u) en[u] = Y.ed2g[min(ea + 64 * u + lane, eb - 1)];
+          }
           for (int f0 = ea; f0 < eb; f0 += 64 * SK_MU) {
             uint32_t e[SK_MU];
+            if constexpr (EG) {
 #pragma unroll
-            for (int u = 0; u < SK_MU; ++u) e[u] = Y.ed2[min(f0 + 64 * u + lane, eb - 1)];
+              for (int u = 0; u < SK_MU; ++u) {
+                e[u] = en[u];
+                en[u] = Y.ed2g[min(f0 + 64 * (SK_MU + u) + lane, eb - 1)];
+              }
+            } else {
+#pragma unroll
+              for (int u = 0; u < SK_MU; ++u) e[u] = Y.ed2[min(f0 + 64 * u + lane, eb - 1)];
+            }
             // unconditional accumulates (lanes past the range add 0 to their
             // own slot), so no read is sunk into a branch
             double g[SK_MU], rv[SK_MU];
@@ -666,13 +741,13 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
             }
           }
 #pragma unroll
-          for (int j = 0; j < SK_PW; ++j) {
+          for (int j = 0; j < PW; ++j) {
             Hq[j] = hb[64 * j + lane];
             hb[64 * j + lane] = 0.0;
           }
         }
 #pragma unroll
-        for (int j = 0; j < SK_PW; ++j) {
+        for (int j = 0; j < PW; ++j) {
           const int q = q0 + 64 * j + lane;
           const bool on = q <= top;
           const uint32_t nda = nd[j].x, ndc = nd[j].y;
@@ -787,7 +862,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // a row nobody reads (a root: pslot 0xffff) needs only its MATCH terms
     // (K is the path sum of M), so it skips the sweep and the store
     if (!combo && c0 < Y.nch && pslot != 0xffffu && !(SK_SKIP_LOOPS && skipr)) {
-      iy_sweep(Y, R, c0, lane);
+      iy_sweep<node_weights<MAXK>(), node_weights_f32<MAXK>()>(Y, R, c0, lane);
       wave_sync();
     }
     STAMP(5);
@@ -838,7 +913,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
           orow[64 * (h0 + k)] = o;
 #else
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), orsrc, lane * 8,
-                                                (h0 + k) * 512, 0);
+                                                (h0 + k) * 512, SK_ROW_ST_POL);
 #endif
 #endif
           // the next row's partial sum: itself (distance-1) + prefetched rows
@@ -875,16 +950,19 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
   const int maxnl = P.lds_max_nl;  // multiple of 64
+  constexpr int PW = pass_width<MAXK>();
 
   // LDS carve (every region a multiple of 16 bytes)
   lds_f64* co = (lds_f64*)(smem);                             // 256
   lds_f64* gp = co + 256;                                     // n_gpow_pad
   lds_f64* Rall = gp + P.n_gpow_pad;                          // nwaves*maxnl
-  lds_f64* hball = Rall + (size_t)nwaves * maxnl;             // nwaves*64*SK_PW (MATCH sums)
-  lds_f64* yew = hball + (size_t)nwaves * 64 * SK_PW;         // lds_max_nch*64 weights
-  lds_u32* ysc = (lds_u32*)(yew + (size_t)P.lds_max_nch * 64);  // lds_max_nch*64 records
+  lds_f64* hball = Rall + (size_t)nwaves * maxnl;             // nwaves*64*PW (MATCH sums)
+  constexpr bool NW = node_weights<MAXK>();
+  lds_f64* yew = hball + (size_t)nwaves * 64 * PW;         // lds_max_nch*64 weights (NW: maxnl)
+  lds_u32* ysc = (lds_u32*)(yew + (node_weights_f32<MAXK>() ? (size_t)maxnl / 2
+                                   : NW ? (size_t)maxnl : (size_t)P.lds_max_nch * 64));  // lds_max_nch*64 records
   lds_u32* yed2 = ysc + (size_t)P.lds_max_nch * 64;           // lds_max_edges (mult. of 4)
-  lds_i32* ylf = (lds_i32*)(yed2 + P.lds_max_edges);          // lds_max_len_pad
+  lds_i32* ylf = (lds_i32*)(yed2 + (edges_global<MAXK>() ? 0 : P.lds_max_edges));  // lds_max_len_pad
   lds_i32* ycs = ylf + P.lds_max_len_pad;                     // lds_max_len_pad
   lds_i32* ctl = ycs + P.lds_max_len_pad;                     // 4 ints
   lds_f64* kap = (lds_f64*)(ctl + 4);                         // xset.n_gam (gam_on)
@@ -893,8 +971,8 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
   for (int k = threadIdx.x; k < P.n_gpow; k += blockDim.x) gp[k] = P.gpow[k];
 
   lds_f64* R = Rall + (size_t)wave * maxnl;
-  lds_f64* hb = hball + (size_t)wave * 64 * SK_PW;
-  for (int j = 0; j < SK_PW; ++j) hb[64 * j + lane] = 0.0;  // kept zero between MATCH passes
+  lds_f64* hb = hball + (size_t)wave * 64 * PW;
+  for (int j = 0; j < PW; ++j) hb[64 * j + lane] = 0.0;  // kept zero between MATCH passes
   double* slab = P.scratch + (size_t)(blockIdx.x * nwaves + wave) * P.slab_doubles;
   double* gamtab = P.gam_on ? P.gam + (size_t)blockIdx.x * P.gam_doubles : nullptr;
   // the workgroup's Phi table: n_phi rows of 64*MAXK, then their sums kappa
@@ -930,14 +1008,21 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
         const uint32_t r = k < nrec ? s.ysc[sb + k] : (d | (d << 11));
         const uint32_t ch = r & 0x7ff, pa = (r >> 11) & 0x7ff;
         ysc[k] = r;
-        yew[k] = ch == pa ? 0.0 : gap2 * (double)s.yn_w[nb + pa] * gp[r >> 22];
+        if (!NW) yew[k] = ch == pa ? 0.0 : gap2 * (double)s.yn_w[nb + pa] * gp[r >> 22];
       }
-      for (int k = threadIdx.x; k < ne; k += blockDim.x) yed2[k] = s.ye2[eb + k];
+      if (node_weights_f32<MAXK>())
+        for (int q = threadIdx.x; q < maxnl; q += blockDim.x) ((lds_f32*)yew)[q] = q < Y.nl ? s.yn_w[nb + q] : 0.0f;
+      else if (NW)  // (gap2 w) gp: the slot weights' rounding
+        for (int q = threadIdx.x; q < maxnl; q += blockDim.x) yew[q] = q < Y.nl ? gap2 * (double)s.yn_w[nb + q] : 0.0;
+      if (!edges_global<MAXK>())
+        for (int k = threadIdx.x; k < ne; k += blockDim.x) yed2[k] = s.ye2[eb + k];
       const int cb = s.ex_ycs_base[y];
       for (int v = threadIdx.x; v <= Y.lmax + 1; v += blockDim.x) ycs[v] = s.ycs[cb + v];
     }
     Y.nrg = s.yrec + nb;
-    Y.sc = ysc; Y.ew = yew; Y.ed2 = yed2; Y.lfirst = ylf; Y.ycs = ycs;
+    Y.sc = ysc; Y.ew = yew; Y.ed2 = yed2; Y.lfirst = ylf; Y.ycs = ycs; Y.gp = gp;
+    Y.ewf = (const lds_f32*)yew; Y.gap2 = gap2;
+    Y.ed2g = s.ye2 + eb;
     Y.nb = nb; Y.bb = bb;
     __syncthreads();
     // length -> first node index (nodes are sorted by length)
@@ -991,7 +1076,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
         int c0 = 0;
         if (band > 0) c0 = Y.ycs[min(max(glen - band, 0), Y.lmax + 1)];
         c0 = __builtin_amdgcn_readfirstlane(c0);
-        if (c0 < Y.nch) iy_sweep(Y, R, c0, lane);
+        if (c0 < Y.nch) iy_sweep<node_weights<MAXK>(), node_weights_f32<MAXK>()>(Y, R, c0, lane);
         double* grow = gamtab + (size_t)g * (64 * MAXK);
         for (int k = 0; k < MAXK; ++k)
           if (lane + 64 * k < Y.nl) grow[lane + 64 * k] = R[lane + 64 * k];  // (the tail is never read)
@@ -1033,7 +1118,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
                 const uint32_t na = Y.nrg[q].x;
                 const int ne = (int)((na >> 16) & 0xff), e0 = (int)(na & 0xffff);
                 for (int e = 0; e < ne; ++e) {
-                  const uint32_t rec = Y.ed2[e0 + e];
+                  const uint32_t rec = edges_global<MAXK>() ? Y.ed2g[e0 + e] : Y.ed2[e0 + e];
                   H += gp[rec >> 22] * R[rec & 0x7ff];
                 }
               }
@@ -1073,7 +1158,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
           int c0 = 0;
           if (band > 0) c0 = Y.ycs[min(max(alen - band, 0), Y.lmax + 1)];
           c0 = __builtin_amdgcn_readfirstlane(c0);
-          if (c0 < Y.nch) iy_sweep(Y, R, c0, lane);
+          if (c0 < Y.nch) iy_sweep<node_weights<MAXK>(), node_weights_f32<MAXK>()>(Y, R, c0, lane);
           double* prow = phitab + (size_t)idx * (64 * MAXK);
 #pragma unroll
           for (int k = 0; k < MAXK; ++k)
@@ -1116,9 +1201,13 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += 256 * 8;
   b += (size_t)P.n_gpow_pad * 8;
   b += (size_t)nwaves * P.lds_max_nl * 8;          // one row per wave
-  b += (size_t)nwaves * 64 * SK_PW * 8;            // MATCH accumulators
-  b += (size_t)P.lds_max_nch * 64 * 12;            // sweep schedule: weights + records
-  b += (size_t)P.lds_max_edges * 4;                // node-major edges
+  b += (size_t)nwaves * 64 * (stem_maxk(P.lds_max_nl) >= SK_PW2_MIN ? 2 : SK_PW) * 8;  // MATCH accumulators
+  const int maxk = stem_maxk(P.lds_max_nl);
+  if (maxk >= SK_NODEW_MIN)                        // sweep schedule: records, node weights
+    b += (size_t)P.lds_max_nch * 64 * 4 + (size_t)P.lds_max_nl * (maxk >= SK_NODEF_MIN ? 4 : 8);
+  else                                             // sweep schedule: weights + records
+    b += (size_t)P.lds_max_nch * 64 * 12;
+  if (stem_maxk(P.lds_max_nl) < SK_EDG_MIN) b += (size_t)P.lds_max_edges * 4;  // node-major edges
   b += (size_t)P.lds_max_len_pad * 4 * 2 + 16;     // length tables, control
   if (P.gam_on) b += (size_t)P.xset.n_gam * 8;     // Gamma sums kappa
   return b;

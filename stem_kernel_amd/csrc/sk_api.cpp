@@ -2110,8 +2110,8 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       std::fprintf(stderr, "\n[stamps] per row: A-loaded rows=%.3f swept chunks=%.2f match passes=%.2f band nodes=%.1f\n",
                    h[10] / rows, h[11] / rows, h[12] / rows, h[13] / rows);
       for (const StemClass& C : classes)
-        std::fprintf(stderr, "[stamps] class maxk=%d max_nl=%d waves/wg=%d grid=%d items=%zu\n",
-                     C.maxk, C.max_nl, C.nwaves, C.grid, C.n_items);
+        std::fprintf(stderr, "[stamps] class maxk=%d max_nl=%d max_edges=%d max_nch=%d waves/wg=%d grid=%d items=%zu\n",
+                     C.maxk, C.max_nl, C.max_edges, C.max_nch, C.nwaves, C.grid, C.n_items);
     }
 #endif
     ctx->last_launches = (int32_t)classes.size() + (big_x.empty() ? 0 : 1);
