@@ -174,7 +174,7 @@ __device__ __forceinline__ void wave_sync() {
 #define SK_NPF16 1
 #endif
 #ifndef SK_PW  // MATCH pass width in 64-node groups
-#define SK_PW 4
+#define SK_PW 3  // NS 193.7k against 192.2k pairs/s with 4 (r03, same box)
 #endif
 #ifndef SK_SEGSUM  // MATCH: same-parent runs summed per quad before the atomic (0 = off)
 #define SK_SEGSUM 1
