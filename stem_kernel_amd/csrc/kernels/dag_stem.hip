@@ -188,6 +188,9 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_PHI_EXP  // cost experiments only (wrong values): 1 phi rows load nothing, 2 no Phi tables
 #define SK_PHI_EXP 0
 #endif
+#ifndef SK_ROW_EXP  // cost experiments only (wrong values): child reads of gamma rows (1) / slab rows (2) all from one row
+#define SK_ROW_EXP 0
+#endif
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
 #define SK_MU 3
 #endif
@@ -405,6 +408,12 @@ __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int
 // component
 __device__ __forceinline__ const double* child_row(uint32_t c, const double* slab, const double* gamtab,
                                                    const double* phitab, int stride) {
+#if SK_ROW_EXP & 1
+  if (c & 0x8000u) c = 0x8000u;
+#endif
+#if SK_ROW_EXP & 2
+  if (!(c & 0xc000u)) c = 0u;
+#endif
   const double* base = (c & 0x8000u) ? gamtab : (c & 0x4000u) ? phitab : slab;
   return base + (size_t)(c & 0x3fffu) * stride;
 }

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out/diag
+SK_PACK_STATS=1 timeout -k 10 300 python3 -u bench.py --config ns --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/diag/pack.log 2>&1 || { tail -20 gpurun_out/diag/pack.log; exit 1; }
+grep "sk pack" gpurun_out/diag/pack.log
+bash tools/_stamps.sh
