@@ -40,18 +40,20 @@ __device__ __forceinline__ float f32_madd(float n, float a, float b) {
 
 // exp(x) for |x| < 2^40 (overflow to inf past ~709, underflow to 0):
 // x = (1024 m + j) ln2/1024 + r, |r| <= ln2/2048; k = 1024 m + j rounded by
-// the 1.5 * 2^52 shifter (its low word is k), r by a two-part ln2/1024 (the
-// high part has 32 significant bits, so k * hi is exact), e^r by its Taylor
-// series to degree 2 (truncation r^3/6 < 6.5e-12 relative: over the <= 2L
-// factors of one alignment path below 1e-8, against the 1e-6 parity gate),
-// times 2^(j/1024) from the workgroup's LDS table, times 2^m.  10 VALU and one
-// LDS read (degree 3: 11; the degree-5 form over a 64-entry table took 16).
+// the 1.5 * 2^52 shifter (its low word is k), r = fma(-k, C, x) with C the
+// double nearest ln2/1024 (one rounding: |k| |C - ln2/1024| <= 7.7e-14
+// relative for |x| <= 709, where exp is finite; a two-part Cody-Waite
+// constant buys nothing against the polynomial and cost one VALU), e^r by
+// its Taylor series to degree 2 (truncation r^3/6 < 6.5e-12 relative: over
+// the <= 2L factors of one alignment path below 1e-8, against the 1e-6 parity
+// gate), times 2^(j/1024) from the workgroup's LDS table, times 2^m.  9 VALU
+// and one LDS read (two-part reduction: 10; degree 3: 11; the degree-5 form
+// over a 64-entry table took 16).
 __device__ __forceinline__ double fast_exp(double x, const double* etab) {
   const double t = __builtin_fma(x, 1477.3197218702985, 6755399441055744.0);  // 1024/ln2, 1.5*2^52
   const int ki = __double2loint(t);
   const double k = t - 6755399441055744.0;
-  double r = __builtin_fma(-k, 6.769015435565962e-04, x);  // ln2/1024, high part
-  r = __builtin_fma(-k, -4.1024561256651217e-14, r);       // ln2/1024, low part
+  const double r = __builtin_fma(-k, 6.769015435155716e-04, x);  // ln2/1024
   double p = __builtin_fma(r, 0.5, 1.0);
   p = __builtin_fma(p, r, 1.0);
   return __builtin_amdgcn_ldexp(etab[ki & 1023] * p, ki >> 10);

@@ -2116,7 +2116,10 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
 #endif
     ctx->last_launches = (int32_t)classes.size() + (big_x.empty() ? 0 : 1);
   }
-  if (str) {
+  // SK_STR_SKIP=1: cost experiment only (wrong values): the string kernel of
+  // a stem + string kind is not launched
+  static const bool str_skip = std::getenv("SK_STR_SKIP") != nullptr;
+  if (str && !str_skip) {
     const hipStream_t SS = side ? ctx->side : S;
     sk::StrLaunch T;
     T.xset = xs_->dev;
@@ -2203,7 +2206,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     ctx->last_stem_ms = ms;
     SK_HIP(ctx, sk::lev_collect(ctx));
   }
-  if (str) {
+  if (str && !str_skip) {
     float ms = 0.f;
     SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev2, ctx->ev3));
     ctx->last_str_ms = ms;
