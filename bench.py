@@ -149,9 +149,17 @@ def algorithmic(kind, shapes, x, y):
         return "hbm", "GB/s", PEAK_HBM_GBS, \
             "SURVEY §8d: 32*|Vx|*|Vy| + S(x) + S(y) + 8 bytes per pair", dag_bytes(shapes, x, y)
     if kind == "stem4d":
+        if os.environ.get("SK4_NO_GSUM"):  # the four-state planes (A/B switch)
+            return "hbm", "GB/s", PEAK_HBM_GBS, \
+                "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
+                72.0 * stem4d_cells(lens, x, y)
+        # full_dp with the K chain summed (stem4d.hip): G0, G1 written once
+        # (16 B), G0 of (i,j-1), G1 of (i+1,j) and the stacking G0 of
+        # (i+1,j-1) read once (24 B); SURVEY §8d's 72 B counted K0, K1 too
         return "hbm", "GB/s", PEAK_HBM_GBS, \
-            "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
-            72.0 * stem4d_cells(lens, x, y)
+            "40 B per (i,j,k,l) cell (G0, G1 written; G0, G1, stacking G0 read; SURVEY §8d's 72 B " \
+            "less the K states, which are summed), [n(n+1)/2][m(m+1)/2] cells", \
+            40.0 * stem4d_cells(lens, x, y)
     return "valu", "TFLOP/s", PEAK_FP64_TFS, \
         "SURVEY §8d: 24 flop per cell (exp counted as 1), Lx*Ly cells", \
         24.0 * float(np.sum(lens[x].astype(np.float64) * lens[y]))

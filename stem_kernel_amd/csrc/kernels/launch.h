@@ -203,7 +203,7 @@ __host__ __device__ inline size_t bpla_wave_lds_bytes(int maxlen) {
 struct Stem4dPair {
   int32_t n = 0, m = 0;          // |x|, |y|
   int64_t plane_doubles = 0;     // per state, padded rows
-  int64_t scratch_off = 0;       // ring of 3 spans x (n+1) planes x 4 states
+  int64_t scratch_off = 0;       // ring of 3 spans x (n+1) planes x 4 states (2 + acc: gsum)
   int64_t x_bp = 0, y_bp = 0;    // into bpdiag
   int64_t x_chr = 0, y_chr = 0;  // into chars
   int64_t out_index = 0;
@@ -228,6 +228,10 @@ struct Stem4dLaunch {
   // doubles each (stem4d.hip k tiles)
   double* kbound = nullptr;
   int64_t kbound_stride = 0;
+  // full_dp with the K chain summed (stem4d.hip sk_stem4d_gsum_kernel): planes
+  // of two states (G0, G1) and a per-pair accumulator of n+1 doubles after
+  // the ring; 0 = the four-state planes
+  int32_t gsum = 0;
 };
 
 int stem4d_cpl(int m);

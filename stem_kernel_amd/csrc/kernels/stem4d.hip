@@ -342,6 +342,215 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
   if (m == 0 && i == 0 && j == n && lane == 0) P.out[pr.out_index] = 1.0;
 }
 
+// full_dp (no band) with the K chain summed.  For k < l, dp_init/dp_update
+// (:85-111) make K3(c) = K3(i,j,k+1,l) + src(c), K2(c) = K2(i,j,k,l-1) + K3(c),
+// K1(c) = K1(i+1,j,k,l) + K2(c), K0(c) = K0(i,j-1,k,l) + K1(c), where src(c)
+// is the stacking term (:325-331), K1/K2/K3 are zero on their boundaries
+// (the (j,j) planes and the diagonal cells, :294-297, :311-314) and K0 is 1 on
+// the (j,j) planes.  Unrolled, K0(0,n,0,m) = 1 + sum of src over every cell
+// i < j, k < l: each source reaches the result with coefficient one, and no
+// K value is read for anything else.  So only G0 and G1 go to HBM (16 B
+// written and 16 + 8 B read per cell instead of 32 + 40), K2/K3 leave the
+// registers, each plane's wave sums its sources (fixed lane order) into the
+// pair's accumulator of its i (acc[i], one writer per launch; a pair's spans
+// run in order on one stream), and the wave of the last plane (0, n) forms
+// 1 + sum_i acc[i] in i order: deterministic, equal to the reference's chain
+// up to the association of non-negative sums.  Plane layout: G0 at 0, G1 at
+// cp; acc follows the pair's ring.  k tiles (|y| >= 512) hand G3 on as in the
+// 4-state kernel.
+template <int CPL>
+__global__ void __launch_bounds__(256) sk_stem4d_gsum_kernel(Stem4dLaunch P) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t it = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (it >= P.n_items) return;
+  const int2 item = P.items[it];  // {pair slot, i}
+  const Stem4dPair pr = P.pairs[item.x];
+  const int i = item.y, d1 = P.d1, j = i + d1;
+  const int n = pr.n, m = pr.m;
+  const int64_t cp = pr.plane_doubles;  // per state
+  const int64_t ps = 2 * cp;            // plane stride (G0, G1)
+  double* ring = P.scratch + pr.scratch_off;
+  double* acc = ring + (int64_t)3 * (n + 1) * ps;
+  double* __restrict__ cur = ring + (int64_t)(d1 % 3) * (n + 1) * ps + (int64_t)i * ps;
+  const double g = P.gap;
+  constexpr int TW = 64 * CPL;
+  const int ntile = (m + TW) / TW;
+
+  if (d1 == 0) {  // plane (j,j): G0 = g^(l-k), G1 = 0  (:297-309); acc[j] = 0
+    for (int kt = 0; kt < ntile; ++kt) {
+      const int k0 = kt * TW + lane;
+      int R = 0;
+      for (int d2 = 0; d2 <= m; ++d2) {
+        const double gd = P.gpow[d2];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const int k = k0 + 64 * c;
+          if (k <= m - d2) {
+            cur[R + k] = gd;
+            cur[cp + R + k] = 0.0;
+          }
+        }
+        R += pad4(m + 1 - d2);
+      }
+    }
+    if (lane == 0) {
+      acc[i] = 0.0;
+      if (n == 0) P.out[pr.out_index] = 1.0;
+    }
+    return;
+  }
+
+  const double* span_p1 = ring + (int64_t)((d1 - 1) % 3) * (n + 1) * ps;
+  const double* __restrict__ A = span_p1 + (int64_t)i * ps;        // plane (i, j-1): G0
+  const double* __restrict__ B = span_p1 + (int64_t)(i + 1) * ps;  // plane (i+1, j): G0, G1
+  const double* Cg = d1 >= 2 ? ring + (int64_t)((d1 - 2) % 3) * (n + 1) * ps + (int64_t)(i + 1) * ps
+                             : nullptr;  // plane (i+1, j-1), G0
+  const float* bpx = P.bpdiag + pr.x_bp;  // prob(a, a+e) at e*n - e*(e-1)/2 + a
+  const float* bpy = P.bpdiag + pr.y_bp;
+  const uint8_t* xs = P.chars + pr.x_chr;
+  const uint8_t* ys = P.chars + pr.y_chr;
+  const float bound = P.bp_bound;
+  const int e1 = d1 - 1;  // bp_ij = prob(i, j-1) (:320)
+  const float bp_ij = bpx[(int64_t)e1 * n - (int64_t)e1 * (e1 - 1) / 2 + i];
+  const bool stack_on = bp_ij > bound && Cg != nullptr;
+  const uint8_t xi = xs[i], xj = xs[j - 1];
+  const double stk = P.stack, sub = P.subst;
+  double ksrc = 0.0;  // this plane's sources
+  // boundary columns of this plane: [2 parities][G3][span d2]
+  double* kbnd = ntile > 1 ? P.kbound + it * P.kbound_stride : nullptr;
+  const int bstride = m + 1;
+
+  for (int kt = ntile - 1; kt >= 0; --kt) {
+    const int kb = kt * TW;
+    const int k0 = kb + lane;
+    double* bnd_w = kbnd ? kbnd + (int64_t)(kt & 1) * bstride : nullptr;              // for tile kt-1
+    const double* bnd_r = kbnd ? kbnd + (int64_t)((kt + 1) & 1) * bstride : nullptr;  // of tile kt+1
+    const bool has_right = kt + 1 < ntile;
+    if (bnd_w && lane == 0) bnd_w[0] = 0.0;  // span 0 (the diagonal): G3 = 0
+    double G2[CPL], G3[CPL];
+    uint8_t yk[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      G2[c] = G3[c] = 0.0;
+      const int k = k0 + 64 * c;
+      yk[c] = k < m ? ys[k] : 0;
+    }
+    // d2 = 0: cells (l,l): G0 = G0(i+1,j,l,l) g, G1 = 0  (:313-317)
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int k = k0 + 64 * c;
+      if (k <= m) {
+        cur[k] = B[k] * g;
+        cur[cp + k] = 0.0;
+      }
+    }
+    // row d2's inputs, prefetched during row d2-1: G0 of (i,j-1), G1 of
+    // (i+1,j), prob_y(k, l-1), y[l-1] and G0(i+1,j-1) at (k+1, l-1)
+    double pG0[CPL], pG1[CPL], pGs[CPL];
+    float pbp[CPL];
+    uint8_t pyl[CPL];
+    int Rm1 = 0, R = pad4(m + 1);
+    auto fetch = [&](int d2, int Rd, int Rd2) __attribute__((always_inline)) {
+      const int kmax = m - d2;
+      const int e2 = d2 - 1;
+      const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int k = k0 + 64 * c;
+        pbp[c] = 0.0f;
+        pGs[c] = 0.0;
+        pyl[c] = 0;
+        if (k <= kmax) {
+          pG0[c] = A[Rd + k];
+          pG1[c] = B[cp + Rd + k];
+          if (stack_on) {
+            pbp[c] = bpy[ye + k];
+            pyl[c] = ys[k + d2 - 1];
+            if (d2 >= 2) pGs[c] = Cg[Rd2 + k + 1];
+          }
+        }
+      }
+    };
+    if (m >= 1) fetch(1, R, 0);
+    for (int d2 = 1; d2 <= m; ++d2) {
+      double cG0[CPL], cG1[CPL], cGs[CPL];
+      float cbp[CPL];
+      uint8_t cyl[CPL];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        cG0[c] = pG0[c];
+        cG1[c] = pG1[c];
+        cGs[c] = pGs[c];
+        cbp[c] = pbp[c];
+        cyl[c] = pyl[c];
+      }
+      const int Rn = R + pad4(m + 1 - d2);
+      if (d2 + 1 <= m) fetch(d2 + 1, Rn, Rm1);
+      // G3 of (k+1, l): my next cell, or the next lane's first (span d2-1)
+      const double rg = has_right ? bnd_r[d2 - 1] : 0.0;
+      double G3n[CPL];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const double hg = c + 1 < CPL ? bcast_lane0(G3[c + 1 < CPL ? c + 1 : c]) : rg;
+        G3n[c] = wave_shl1(G3[c], hg);
+      }
+      const int kmax = m - d2;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int k = k0 + 64 * c;
+        if (k <= kmax) {
+          // dp_init (:85-96): G terms; the K terms are the sources below
+          double G0 = cG0[c] * g;
+          double G1 = cG1[c] * g;
+          double g2 = G2[c] * g;
+          double g3 = G3n[c] * g;
+          if (stack_on) {  // :321-333
+            const float bp_kl = cbp[c];
+            if (bp_kl > bound) {
+              const double g0 = cGs[c];
+              if (xi == yk[c] && xj == cyl[c]) {
+                ksrc += g0 * stk * (double)bp_ij * (double)bp_kl;
+                g3 += g0;
+              } else {
+                ksrc += g0 * stk * sub * (double)bp_ij * (double)bp_kl;
+              }
+            }
+          }
+          // dp_update (:100-111)
+          g2 += g3;
+          G1 += g2;
+          G0 += G1;
+          cur[R + k] = G0;
+          cur[cp + R + k] = G1;
+          G2[c] = g2;
+          G3[c] = g3;
+        }
+      }
+      if (bnd_w && lane == 0) bnd_w[d2] = G3[0];
+      Rm1 = R;
+      R = Rn;
+    }
+    if (kbnd) {  // the next tile's lanes read what lane 0 stored
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+  }  // k tiles
+  for (int off = 32; off > 0; off >>= 1) ksrc += __shfl_xor(ksrc, off, 64);
+  if (lane == 0) acc[i] += ksrc;
+  if (i == 0 && j == n) {  // the last plane: K0(0,n,0,m) = 1 + sum_i acc[i]
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+      double K = 0.0;
+      for (int t = 0; t <= n; ++t) K += acc[t];
+      P.out[pr.out_index] = 1.0 + K;
+    }
+  }
+}
+
 int stem4d_cpl(int m) {
   if (m + 1 <= 64) return 1;
   if (m + 1 <= 128) return 2;
@@ -357,6 +566,8 @@ hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st) {
 #define SK_L(C)                                                                      \
   if (band)                                                                          \
     hipLaunchKernelGGL((sk_stem4d_kernel<C, true>), grid, block, 0, st, P);         \
+  else if (P.gsum)                                                                   \
+    hipLaunchKernelGGL((sk_stem4d_gsum_kernel<C>), grid, block, 0, st, P);          \
   else                                                                               \
     hipLaunchKernelGGL((sk_stem4d_kernel<C, false>), grid, block, 0, st, P);
   switch (cpl) {

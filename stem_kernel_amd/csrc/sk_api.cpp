@@ -1412,6 +1412,12 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // K3/G3 column to the next through per-item boundary columns
   const bool ktiles = max_m + 1 > 64 * cpl;
   const int64_t kb_stride = ktiles ? 4 * (int64_t)(max_m + 1) : 0;
+  // full_dp: G-only planes with the K chain summed (stem4d.hip); the banded
+  // and PairHMM-constrained partial_dp keep the four-state planes (their
+  // boundary approximations read K0 / K1 off the band)
+  const bool banded = ali_phmm || (!ali && kp->len_band > 0);
+  const bool gsum = !banded && !std::getenv("SK4_NO_GSUM");
+  const size_t nst = gsum ? 2 : 4;
   double total_ms = 0.0;
   int launches = 0;
   Stem4dBatch& Bt = ctx->s4d;
@@ -1428,7 +1434,8 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       p.n = xs_->ex[x[q]].len;
       p.m = ys_->ex[y[q]].len;
       p.plane_doubles = stem4d_plane_doubles(p.m);
-      const size_t rb = (size_t)3 * (p.n + 1) * 4 * (size_t)p.plane_doubles * 8;
+      const size_t rb = ((size_t)3 * (p.n + 1) * nst * (size_t)p.plane_doubles * 8 +
+                         (gsum ? (size_t)(p.n + 1) * 8 : 0) + 255) & ~(size_t)255;
       const double pb = (double)rb + (double)(p.n + 1) * (double)kb_stride * 8.0;
       if (!prs.empty() && bytes + pb > budget) break;
       p.scratch_off = (int64_t)(ring_bytes / 8);
@@ -1533,6 +1540,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     L.band_hi = n_band ? Bt.band + Bt.cap_band : nullptr;
     L.kbound = ktiles ? ctx->scratch + ring_bytes / 8 : nullptr;
     L.kbound_stride = kb_stride;
+    L.gsum = gsum ? 1 : 0;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     if (ali_phmm) {
       sk::PhmmLaunch H;
