@@ -615,7 +615,8 @@ def main():
             rf = roofline(a.config, kind, a.length, shapes, xs, ys, float(np.sum(k_ms)), float(np.sum(l_ms)),
                           int(np.sum(launches)), cells, a.pmc_json)
             rf["kernel"] = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
-                            "stem4d": "sk_stem4d_kernel", "bpla": "sk_bpla_fast_kernel"}[kind]
+                            "stem4d": "sk_stem4d_kernel" if os.environ.get("SK4_NO_GSUM") else "sk_stem4d_gsum_kernel",
+                            "bpla": "sk_bpla_fast_kernel"}[kind]
         cpu, parity = None, None
         if not a.no_cpu_baseline and world == 1 and not a.cpu_stub:  # rank 0 at N=1 only
             cpu, cpairs, cvals = cpu_baseline(cfg, eng.data, a.cpu_pairs)

@@ -12,7 +12,7 @@ case $CFG in
   ns) KIND=ss; KSUB=sk_dag_stem_kernel;;
   c2) KIND=ss; KSUB=sk_dag_stem_kernel;;
   c5) KIND=stem; KSUB=sk_dag_stem_kernel;;
-  c3) KIND=stem4d; KSUB=sk_stem4d_kernel;;
+  c3) KIND=stem4d; KSUB=sk_stem4d;;
   c4) KIND=bpla; KSUB=sk_bpla_fast;;
   *) echo "unknown config $CFG"; exit 2;;
 esac
