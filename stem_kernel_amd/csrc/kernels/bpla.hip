@@ -636,6 +636,10 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
   // l-1 sends its row B's sum, bS), u = row above at j (lane l-1's row B);
   // c1: column 1 (left is column 0: zero).  A row's left sum M + X is
   // shared by its Y recurrence and the diagonal sum it hands on.
+  // sB1 = bM + bX and sB2 = sB1 + bY of row B's latest outputs, carried from
+  // step to step: each is formed once per step (the row-B Y recurrence, the
+  // diagonal sum handed on, lane 63's boundary write), not once per use
+  double sB1 = 0.0, sB2 = 0.0;
   auto cells = [&](const BplaPos& yc, double dS, double uM, double uX, bool c1) __attribute__((always_inline)) {
     const double eA = expo(xA, yc);
     const double eB = expo(xB, yc);
@@ -645,7 +649,7 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
     const double nYA = c1 ? 0.0 : bg * sA + be * aY;
     const double nMB = __builtin_fma(eB, sA + aY, eB);  // diagonal: row A at j-1
     const double nXB = bg * nMA + be * nXA;
-    const double nYB = c1 ? 0.0 : bg * (bM + bX) + be * bY;
+    const double nYB = c1 ? 0.0 : bg * sB1 + be * bY;
     aM = nMA;
     aX = nXA;
     aY = nYA;
@@ -654,6 +658,9 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
     bY = nYB;
     accA += nMA;
     accB += nMB;
+    sB1 = nMB + nXB;
+    sB2 = sB1 + nYB;
+    __asm__ volatile("" : "+v"(sB2));  // formed here, once, ahead of lane 63's write
   };
 
   // interior step: lane 0's column jb, every lane active
@@ -679,13 +686,13 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
     }
     const double uM = wave_shr1(bM, b0);
     const double uX = wave_shr1(bX, b1);
-    uS = wave_shr1((bM + bX) + bY, b2);
+    uS = wave_shr1(sB2, b2);
     cells(yc, dS, uM, uX, false);
     if (lane == 63) {  // lane 63's column is jb - 63
       double* bw = bnd + 3 * (jb - 63);
       bw[0] = bM;
       bw[1] = bX;
-      bw[2] = (bM + bX) + bY;
+      bw[2] = sB2;
     }
     yofs += (unsigned)sizeof(BplaPos);
   };
@@ -731,7 +738,7 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
     const double* bj = bnd + 3 * (jb <= Ly ? jb : 0);
     uM = wave_shr1(bM, bj[0]);
     uX = wave_shr1(bX, bj[1]);
-    uS = wave_shr1((bM + bX) + bY, bj[2]);
+    uS = wave_shr1(sB2, bj[2]);
     if (FULL) {
       const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
       cells(yc, dS, uM, uX, wrap);
@@ -741,7 +748,7 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
         double* bw = bnd + 3 * j63;
         bw[0] = bM;
         bw[1] = bX;
-        bw[2] = (bM + bX) + bY;
+        bw[2] = sB2;
       }
     } else {
       const int jl = lane <= w ? w - lane + 1 : Lys + w - lane + 1;
@@ -753,7 +760,7 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
           double* bw = bnd + 3 * jl;
           bw[0] = bM;
           bw[1] = bX;
-          bw[2] = (bM + bX) + bY;
+          bw[2] = sB2;
         }
       }
     }
