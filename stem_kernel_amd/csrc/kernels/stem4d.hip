@@ -55,6 +55,9 @@ __device__ __forceinline__ int row_off(int m, int d2) {
 // BAND: partial_dp (stem_kernel.cpp:113-280) with the -b band constraints:
 // cells outside the band stay zero, K0 past c_high[j-1] and K1 below
 // c_low[i+1] take the reference's boundary approximations.
+#ifndef SK4_PF  // K-sum kernel: rows fetched ahead (1 or 2)
+#define SK4_PF 1
+#endif
 #ifndef SK4_MINB  // minimum 4-wave workgroups per CU (register budget knob)
 #define SK4_MINB 1
 #endif
@@ -447,46 +450,51 @@ __global__ void __launch_bounds__(256) sk_stem4d_gsum_kernel(Stem4dLaunch P) {
     }
     // row d2's inputs, prefetched during row d2-1: G0 of (i,j-1), G1 of
     // (i+1,j), prob_y(k, l-1), y[l-1] and G0(i+1,j-1) at (k+1, l-1)
-    double pG0[CPL], pG1[CPL], pGs[CPL];
-    float pbp[CPL];
-    uint8_t pyl[CPL];
+    struct Row {
+      double G0[CPL], G1[CPL], Gs[CPL];
+      float bp[CPL];
+      uint8_t yl[CPL];
+    };
+    Row p, q;
     int Rm1 = 0, R = pad4(m + 1);
-    auto fetch = [&](int d2, int Rd, int Rd2) __attribute__((always_inline)) {
+    auto fetch = [&](Row& r, int d2, int Rd, int Rd2) __attribute__((always_inline)) {
       const int kmax = m - d2;
       const int e2 = d2 - 1;
       const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         const int k = k0 + 64 * c;
-        pbp[c] = 0.0f;
-        pGs[c] = 0.0;
-        pyl[c] = 0;
+        r.bp[c] = 0.0f;
+        r.Gs[c] = 0.0;
+        r.yl[c] = 0;
         if (k <= kmax) {
-          pG0[c] = A[Rd + k];
-          pG1[c] = B[cp + Rd + k];
+          r.G0[c] = A[Rd + k];
+          r.G1[c] = B[cp + Rd + k];
           if (stack_on) {
-            pbp[c] = bpy[ye + k];
-            pyl[c] = ys[k + d2 - 1];
-            if (d2 >= 2) pGs[c] = Cg[Rd2 + k + 1];
+            r.bp[c] = bpy[ye + k];
+            r.yl[c] = ys[k + d2 - 1];
+            if (d2 >= 2) r.Gs[c] = Cg[Rd2 + k + 1];
           }
         }
       }
     };
-    if (m >= 1) fetch(1, R, 0);
+    // rows are fetched SK4_PF rows ahead (row 2 reads the stacking row 0)
+    if (m >= 1) fetch(p, 1, R, 0);
+    if (SK4_PF == 2 && m >= 2) fetch(q, 2, R + pad4(m), 0);
     for (int d2 = 1; d2 <= m; ++d2) {
-      double cG0[CPL], cG1[CPL], cGs[CPL];
-      float cbp[CPL];
-      uint8_t cyl[CPL];
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        cG0[c] = pG0[c];
-        cG1[c] = pG1[c];
-        cGs[c] = pGs[c];
-        cbp[c] = pbp[c];
-        cyl[c] = pyl[c];
-      }
+      const Row cr = p;
+      const double* cG0 = cr.G0;
+      const double* cG1 = cr.G1;
+      const double* cGs = cr.Gs;
+      const float* cbp = cr.bp;
+      const uint8_t* cyl = cr.yl;
       const int Rn = R + pad4(m + 1 - d2);
-      if (d2 + 1 <= m) fetch(d2 + 1, Rn, Rm1);
+      if (SK4_PF == 2) {
+        p = q;
+        if (d2 + 2 <= m) fetch(q, d2 + 2, Rn + pad4(m - d2), R);
+      } else if (d2 + 1 <= m) {
+        fetch(p, d2 + 1, Rn, Rm1);
+      }
       // G3 of (k+1, l): my next cell, or the next lane's first (span d2-1)
       const double rg = has_right ? bnd_r[d2 - 1] : 0.0;
       double G3n[CPL];
