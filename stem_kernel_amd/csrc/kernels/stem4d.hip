@@ -56,7 +56,7 @@ __device__ __forceinline__ int row_off(int m, int d2) {
 // cells outside the band stay zero, K0 past c_high[j-1] and K1 below
 // c_low[i+1] take the reference's boundary approximations.
 #ifndef SK4_PF  // K-sum kernel: rows fetched ahead (1 or 2)
-#define SK4_PF 1
+#define SK4_PF 2
 #endif
 #ifndef SK4_MINB  // minimum 4-wave workgroups per CU (register budget knob)
 #define SK4_MINB 1
