@@ -65,6 +65,26 @@ def test_stem4d_gram_matches_oracle(gpu_ctx, model, bound):
 
 
 @pytest.mark.gpu
+def test_stem4d_ksum_equals_four_state(gpu_ctx, monkeypatch):
+    """full_dp with the K chain summed (sk_stem4d_gsum_kernel: K0(0,n,0,m) = 1
+    + the sum of every stacking source) against the four-state
+    planes (SK4_NO_GSUM=1): equal up to the association of non-negative sums,
+    CPL 1-4, empty and one-residue sequences included, both against the oracle."""
+    seqs = _seqs() + ["", "G"] + ska.random_sequences(2, 130, 0x5EED0043)
+    ds, _ = make_examples(seqs)
+    kern = ska.StemKernel4D()
+    a = gpu_ctx.gram(ds, kern)
+    monkeypatch.setenv("SK4_NO_GSUM", "1")
+    b = gpu_ctx.gram(ds, kern)
+    assert rel_err(a, b) < 1e-12
+    n = len(seqs)
+    iu = list(zip(*np.triu_indices(n)))
+    ref = _oracle(seqs, kern, iu)
+    assert rel_err(a[tuple(np.array(iu).T)], ref) < TOL
+    assert a[n - 4, n - 4] == 1.0 and np.all(a[n - 4, :] == 1.0)  # the empty sequence: K = 1
+
+
+@pytest.mark.gpu
 def test_stem4d_params_and_predict(gpu_ctx):
     seqs = ska.random_sequences(5, 40, 0x5EED0033)
     ds, _ = make_examples(seqs)
