@@ -62,6 +62,9 @@ def oracle():
         L.orc_stem4d.restype = C.c_double
         L.orc_stem4d.argtypes = [C.c_char_p, _D, C.c_char_p, _D, C.c_double, C.c_double,
                                  C.c_double, C.c_float, C.c_int, C.c_uint]
+        L.orc_stem4d_ksum.restype = C.c_double
+        L.orc_stem4d_ksum.argtypes = [C.c_char_p, _D, C.c_char_p, _D, C.c_double, C.c_double,
+                                 C.c_double, C.c_float, C.c_int, C.c_uint]
         L.orc_stem4d_banded.restype = C.c_double
         L.orc_stem4d_banded.argtypes = [C.c_char_p, _D, C.c_char_p, _D, C.c_double, C.c_double,
                                         C.c_double, C.c_float, C.c_int, C.c_uint, C.c_uint]
@@ -231,6 +234,17 @@ def stem4d(x: str, bpx, y: str, bpy, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0
                                           bp_bound, model, loop, band)
     return oracle().orc_stem4d(x.encode(), px, y.encode(), py, gap, stack, subst, bp_bound,
                                model, loop)
+
+
+def stem4d_ksum(x: str, bpx, y: str, bpy, gap=0.8, stack=1.0, subst=0.5, bp_bound=0.0, model=0,
+                loop=3) -> float:
+    """full_dp's K as 1 + the sum of the stacking sources (the engine's K-sum
+    formulation), from the same loops as stem4d()."""
+    keep = [np.ascontiguousarray(b, dtype=np.float64) if b is not None else None for b in (bpx, bpy)]
+    px = keep[0].ctypes.data_as(_D) if keep[0] is not None and keep[0].size else None
+    py = keep[1].ctypes.data_as(_D) if keep[1] is not None and keep[1].size else None
+    return oracle().orc_stem4d_ksum(x.encode(), px, y.encode(), py, gap, stack, subst, bp_bound,
+                                    model, loop)
 
 
 def phmm_posterior(x: str, y: str, zerop_fixed=0) -> np.ndarray:

@@ -1071,10 +1071,15 @@ static float bp4_prob(const bp4 *B, int i, int j) {
 
 enum { S_K0 = 0, S_K1, S_K2, S_K3, S_G0, S_G1, S_G2, S_G3 };
 
-double orc_stem4d(const char *x, const double *bpx, const char *y, const double *bpy,
-                  double gap, double stack, double subst, float bp_bound, int model,
-                  unsigned loop) {
+/* srcsum (may be NULL): the sum of every stacking source the K3 updates add
+ * (:327-331), in the reference's loop order -- 1 + srcsum is the K-sum
+ * formulation of the engine's full_dp kernel, checked against
+ * K0(0,n,0,m) of the chain itself (tests/test_stem4d.py) */
+static double stem4d_full(const char *x, const double *bpx, const char *y, const double *bpy,
+                          double gap, double stack, double subst, float bp_bound, int model,
+                          unsigned loop, double *srcsum) {
   const int n = (int)strlen(x), m = (int)strlen(y);
+  double ssum = 0.0;
   const double g = gap;
   bp4 BX = {x, bpx, n, model, loop}, BY = {y, bpy, m, model, loop};
   /* planes (i,j) of columns j-1 and j; cell (k,l), k<=l, triangular */
@@ -1118,8 +1123,10 @@ double orc_stem4d(const char *x, const double *bpx, const char *y, const double 
               if (x[i] == y[k] && x[j - 1] == y[l - 1]) {
                 DP(cur, S_K3, i, k, l) += g0 * stack * bp_ij * bp_kl;
                 DP(cur, S_G3, i, k, l) += g0;
+                ssum += g0 * stack * bp_ij * bp_kl;
               } else {
                 DP(cur, S_K3, i, k, l) += g0 * stack * subst * bp_ij * bp_kl;
+                ssum += g0 * stack * subst * bp_ij * bp_kl;
               }
             }
           }
@@ -1139,7 +1146,23 @@ double orc_stem4d(const char *x, const double *bpx, const char *y, const double 
 #undef CELL
   free(col[0]);
   free(col[1]);
+  if (srcsum) *srcsum = ssum;
   return result;
+}
+
+double orc_stem4d(const char *x, const double *bpx, const char *y, const double *bpy,
+                  double gap, double stack, double subst, float bp_bound, int model,
+                  unsigned loop) {
+  return stem4d_full(x, bpx, y, bpy, gap, stack, subst, bp_bound, model, loop, NULL);
+}
+
+/* 1 + the sum of the stacking sources (the K-sum formulation) */
+double orc_stem4d_ksum(const char *x, const double *bpx, const char *y, const double *bpy,
+                       double gap, double stack, double subst, float bp_bound, int model,
+                       unsigned loop) {
+  double ssum = 0.0;
+  stem4d_full(x, bpx, y, bpy, gap, stack, subst, bp_bound, model, loop, &ssum);
+  return 1.0 + ssum;
 }
 
 /* Band constraints of StemKernel::alignment_constraints without alignment

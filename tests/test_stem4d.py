@@ -42,6 +42,24 @@ def test_oracle_normal_basepair_is_one():
             assert po.stem4d(a, None, b, None, bp_bound=1.0, model=2) == 1.0
 
 
+@pytest.mark.parametrize("model,bound", [(0, 0.0), (0, 0.2), (1, 0.5), (2, 0.5), (1, 1.0)])
+def test_oracle_ksum_equals_chain(model, bound):
+    """The K-sum identity behind the engine's full_dp kernel:
+    K0(0,n,0,m) of the reference's K0..K3 chain (stem_kernel.cpp:282-351,
+    restated in the oracle) equals 1 + the sum of the stacking sources, up to
+    the association of non-negative terms -- lengths 0, 1, short and ragged."""
+    s = ska.random_sequences(3, 23, 71) + ska.random_sequences(2, 9, 72) + ["", "c", "GGGAAACCC"]
+    for a in s:
+        for b in s:
+            xa, xb = a.lower(), b.lower()
+            bx = ska.fold(a) if a else np.zeros(0)
+            by = ska.fold(b) if b else np.zeros(0)
+            args = (xa, bx if model == 0 else None, xb, by if model == 0 else None, 0.7, 1.3, 0.4,
+                    bound, model, 3)
+            chain, ksum = po.stem4d(*args), po.stem4d_ksum(*args)
+            assert abs(chain - ksum) <= 1e-13 * abs(chain), (a, b, chain, ksum)
+
+
 def test_oracle_empty_and_defaults():
     assert po.stem4d("", None, "acgu", np.zeros(6)) == 1.0
     p = ska.StemKernel4D().params
