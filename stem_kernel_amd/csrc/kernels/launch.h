@@ -230,7 +230,8 @@ struct Stem4dLaunch {
   int64_t kbound_stride = 0;
   // full_dp with the K chain summed (stem4d.hip sk_stem4d_gsum_kernel): planes
   // of two states (G0, G1) and a per-pair accumulator of n+1 doubles after
-  // the ring; 0 = the four-state planes
+  // the ring; 0 = the four-state planes; 2 = the same planes with each plane's
+  // G1 pre-combined by the plane (i+1, j) (sk_stem4d_pre_kernel, one k tile)
   int32_t gsum = 0;
 };
 

@@ -559,6 +559,205 @@ __global__ void __launch_bounds__(256) sk_stem4d_gsum_kernel(Stem4dLaunch P) {
   }
 }
 
+// full_dp with the K chain summed and each plane's stacking chain produced one
+// span early.  A plane's G2 / G3 (and so its G1 = G1(i+1,j) g + G2) depend
+// only on its stacking sources, s(k,l) = G0(i+1,j-1,k+1,l-1) when
+// bp(i,j-1) and bp(k,l-1) pass the bound and the end bases match (:321-333).
+// The wave of plane (i+1, j) streams exactly those G0 rows one span earlier
+// (they are its A input, G0(i+1, j-1)), so it runs the chain of its consumer
+// (i, j) too and writes, beside its own G0, the consumer's G1 pre-combined:
+// B'(k,l) = G1(i+1,j,k,l) g + G2_(i,j)(k,l) -- the consumer's G1 in the
+// reference's own operation order.  A plane then reads G0 of (i, j-1) and its
+// B' (16 B per cell) and writes G0 and its consumer's B' (16 B): 32 B per cell
+// against the K-sum kernel's 40 (no stacking read); its consumer's sources
+// go to its own accumulator acc[i].  Single k tile (|y| < 512; the host runs
+// the K-sum kernel otherwise).  Plane layout: G0 at 0, B' (for the plane
+// (i-1, j)) at cp.
+template <int CPL>
+__global__ void __launch_bounds__(256) sk_stem4d_pre_kernel(Stem4dLaunch P) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t it = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (it >= P.n_items) return;
+  const int2 item = P.items[it];  // {pair slot, i}
+  const Stem4dPair pr = P.pairs[item.x];
+  const int i = item.y, d1 = P.d1, j = i + d1;
+  const int n = pr.n, m = pr.m;
+  const int64_t cp = pr.plane_doubles;
+  const int64_t ps = 2 * cp;
+  double* ring = P.scratch + pr.scratch_off;
+  double* acc = ring + (int64_t)3 * (n + 1) * ps;
+  double* __restrict__ cur = ring + (int64_t)(d1 % 3) * (n + 1) * ps + (int64_t)i * ps;
+  const double g = P.gap;
+  const int k0 = lane;
+
+  if (d1 == 0) {  // plane (j,j): G0 = g^(l-k); B' of (j-1, j) = 0 (no sources: bp(j-1,j-1) = 0)
+    int R = 0;
+    for (int d2 = 0; d2 <= m; ++d2) {
+      const double gd = P.gpow[d2];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int k = k0 + 64 * c;
+        if (k <= m - d2) {
+          cur[R + k] = gd;
+          cur[cp + R + k] = 0.0;
+        }
+      }
+      R += pad4(m + 1 - d2);
+    }
+    if (lane == 0) {
+      acc[i] = 0.0;
+      if (n == 0) P.out[pr.out_index] = 1.0;
+    }
+    return;
+  }
+
+  const double* span_p1 = ring + (int64_t)((d1 - 1) % 3) * (n + 1) * ps;
+  const double* __restrict__ A = span_p1 + (int64_t)i * ps;        // plane (i, j-1): G0
+  const double* __restrict__ B = span_p1 + (int64_t)(i + 1) * ps;  // plane (i+1, j): G0, this plane's B'
+  const float* bpx = P.bpdiag + pr.x_bp;
+  const float* bpy = P.bpdiag + pr.y_bp;
+  const uint8_t* xs = P.chars + pr.x_chr;
+  const uint8_t* ys = P.chars + pr.y_chr;
+  const float bound = P.bp_bound;
+  // the consumer: plane (i-1, j) of span d1+1, bp_c = prob(i-1, j-1) (:320)
+  const bool cons = i >= 1;
+  float bp_c = 0.0f;
+  uint8_t xci = 0, xcj = 0;
+  if (cons) {
+    const int e = d1;
+    bp_c = bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (i - 1)];
+    xci = xs[i - 1];
+    xcj = xs[j - 1];
+  }
+  const bool stack_c = cons && bp_c > bound;
+  const double stk = P.stack, sub = P.subst;
+  double ksrc = 0.0;  // the consumer's sources
+
+  uint8_t yk[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int k = k0 + 64 * c;
+    yk[c] = k < m ? ys[k] : 0;
+  }
+  // d2 = 0: cells (l,l): G0 = G0(i+1,j,l,l) g (:313-317); the consumer's
+  // G1 there is 0 (it reads its own diagonal from this plane's G0)
+  double Am1[CPL], Am2[CPL], G2c[CPL], G3c[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int k = k0 + 64 * c;
+    if (k <= m) {
+      cur[k] = B[k] * g;
+      cur[cp + k] = 0.0;
+    }
+    Am1[c] = (stack_c && k <= m) ? A[k] : 0.0;  // G0(i, j-1) diagonal: the sources of row 2
+    Am2[c] = 0.0;
+    G2c[c] = G3c[c] = 0.0;
+  }
+  struct Row {
+    double A[CPL], Bp[CPL];
+    float bp[CPL];
+    uint8_t yl[CPL];
+  };
+  Row p, q;
+  int R = pad4(m + 1);
+  auto fetch = [&](Row& r, int d2, int Rd) __attribute__((always_inline)) {
+    const int kmax = m - d2;
+    const int e2 = d2 - 1;
+    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int k = k0 + 64 * c;
+      r.A[c] = 0.0;
+      r.Bp[c] = 0.0;
+      r.bp[c] = 0.0f;
+      r.yl[c] = 0;
+      if (k <= kmax) {
+        r.A[c] = A[Rd + k];
+        r.Bp[c] = B[cp + Rd + k];
+        if (stack_c) {
+          r.bp[c] = bpy[ye + k];
+          r.yl[c] = ys[k + d2 - 1];
+        }
+      }
+    }
+  };
+  if (m >= 1) fetch(p, 1, R);
+  if (SK4_PF == 2 && m >= 2) fetch(q, 2, R + pad4(m));
+  for (int d2 = 1; d2 <= m; ++d2) {
+    const Row cr = p;
+    const int Rn = R + pad4(m + 1 - d2);
+    if (SK4_PF == 2) {
+      p = q;
+      if (d2 + 2 <= m) fetch(q, d2 + 2, Rn + pad4(m - d2));
+    } else if (d2 + 1 <= m) {
+      fetch(p, d2 + 1, Rn);
+    }
+    // the consumer's G3 at (k+1, l) (row d2-1) and G0(i, j-1) at (k+1, l-1)
+    // (row d2-2): the next lane's, or the next slot's lane 0
+    double G3n[CPL], A2[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const double hg = c + 1 < CPL ? bcast_lane0(G3c[c + 1 < CPL ? c + 1 : c]) : 0.0;
+      const double ha = c + 1 < CPL ? bcast_lane0(Am2[c + 1 < CPL ? c + 1 : c]) : 0.0;
+      G3n[c] = wave_shl1(G3c[c], hg);
+      A2[c] = wave_shl1(Am2[c], ha);
+    }
+    const int kmax = m - d2;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int k = k0 + 64 * c;
+      if (k <= kmax) {
+        // this plane: G1 = B' (its G1, formed by the plane (i+1, j)), G0 (:85-111)
+        const double G1 = cr.Bp[c];
+        double G0 = cr.A[c] * g;
+        G0 += G1;
+        cur[R + k] = G0;
+        if (cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
+          double g3 = G3n[c] * g;
+          if (stack_c && d2 >= 2) {
+            const float bp_kl = cr.bp[c];
+            if (bp_kl > bound) {
+              const double g0 = A2[c];
+              if (xci == yk[c] && xcj == cr.yl[c]) {
+                ksrc += g0 * stk * (double)bp_c * (double)bp_kl;
+                g3 += g0;
+              } else {
+                ksrc += g0 * stk * sub * (double)bp_c * (double)bp_kl;
+              }
+            }
+          }
+          double g2 = G2c[c] * g;
+          g2 += g3;
+          double Bn = G1 * g;
+          Bn += g2;
+          cur[cp + R + k] = Bn;
+          G2c[c] = g2;
+          G3c[c] = g3;
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      Am2[c] = Am1[c];
+      Am1[c] = cr.A[c];
+    }
+    R = Rn;
+  }
+  for (int off = 32; off > 0; off >>= 1) ksrc += __shfl_xor(ksrc, off, 64);
+  if (lane == 0) acc[i] += ksrc;
+  if (i == 0 && j == n) {  // the last plane: K0(0,n,0,m) = 1 + sum_i acc[i]
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+      double K = 0.0;
+      for (int t = 0; t <= n; ++t) K += acc[t];
+      P.out[pr.out_index] = 1.0 + K;
+    }
+  }
+}
+
 int stem4d_cpl(int m) {
   if (m + 1 <= 64) return 1;
   if (m + 1 <= 128) return 2;
@@ -574,6 +773,8 @@ hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st) {
 #define SK_L(C)                                                                      \
   if (band)                                                                          \
     hipLaunchKernelGGL((sk_stem4d_kernel<C, true>), grid, block, 0, st, P);         \
+  else if (P.gsum == 2)                                                              \
+    hipLaunchKernelGGL((sk_stem4d_pre_kernel<C>), grid, block, 0, st, P);           \
   else if (P.gsum)                                                                   \
     hipLaunchKernelGGL((sk_stem4d_gsum_kernel<C>), grid, block, 0, st, P);          \
   else                                                                               \

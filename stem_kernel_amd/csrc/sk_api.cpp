@@ -1540,7 +1540,10 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     L.band_hi = n_band ? Bt.band + Bt.cap_band : nullptr;
     L.kbound = ktiles ? ctx->scratch + ring_bytes / 8 : nullptr;
     L.kbound_stride = kb_stride;
-    L.gsum = gsum ? 1 : 0;
+    // one k tile: each plane's stacking chain produced one span early by the
+    // plane that streams its G0 rows (stem4d.hip sk_stem4d_pre_kernel)
+    static const bool no_pre = std::getenv("SK4_NO_PRE") != nullptr;
+    L.gsum = gsum ? (!ktiles && !no_pre ? 2 : 1) : 0;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     if (ali_phmm) {
       sk::PhmmLaunch H;
