@@ -153,13 +153,20 @@ def algorithmic(kind, shapes, x, y):
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
                 72.0 * stem4d_cells(lens, x, y)
-        # full_dp with the K chain summed (stem4d.hip): G0, G1 written once
-        # (16 B), G0 of (i,j-1), G1 of (i+1,j) and the stacking G0 of
-        # (i+1,j-1) read once (24 B); SURVEY §8d's 72 B counted K0, K1 too
+        if os.environ.get("SK4_NO_PRE") or int(lens[y].max()) + 1 > 256:
+            # full_dp with the K chain summed (stem4d.hip): G0, G1 written once
+            # (16 B), G0 of (i,j-1), G1 of (i+1,j) and the stacking G0 of
+            # (i+1,j-1) read once (24 B); SURVEY §8d's 72 B counted K0, K1 too
+            # (|y| > 255: CPL 8, or k tiles past 511, measured on this kernel)
+            return "hbm", "GB/s", PEAK_HBM_GBS, \
+                "40 B per (i,j,k,l) cell (G0, G1 written; G0, G1, stacking G0 read; SURVEY §8d's 72 B " \
+                "less the K states, which are summed), [n(n+1)/2][m(m+1)/2] cells", \
+                40.0 * stem4d_cells(lens, x, y)
+        # + each plane's stacking chain produced one span early (pre-combined G1)
         return "hbm", "GB/s", PEAK_HBM_GBS, \
-            "40 B per (i,j,k,l) cell (G0, G1 written; G0, G1, stacking G0 read; SURVEY §8d's 72 B " \
-            "less the K states, which are summed), [n(n+1)/2][m(m+1)/2] cells", \
-            40.0 * stem4d_cells(lens, x, y)
+            "32 B per (i,j,k,l) cell (G0 and the consumer's pre-combined G1 written, G0 and the own " \
+            "pre-combined G1 read; SURVEY §8d's 72 B less the summed K states and the stacking read), " \
+            "[n(n+1)/2][m(m+1)/2] cells", 32.0 * stem4d_cells(lens, x, y)
     return "valu", "TFLOP/s", PEAK_FP64_TFS, \
         "SURVEY §8d: 24 flop per cell (exp counted as 1), Lx*Ly cells", \
         24.0 * float(np.sum(lens[x].astype(np.float64) * lens[y]))
@@ -615,7 +622,8 @@ def main():
             rf = roofline(a.config, kind, a.length, shapes, xs, ys, float(np.sum(k_ms)), float(np.sum(l_ms)),
                           int(np.sum(launches)), cells, a.pmc_json)
             rf["kernel"] = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
-                            "stem4d": "sk_stem4d_kernel" if os.environ.get("SK4_NO_GSUM") else "sk_stem4d_gsum_kernel",
+                            "stem4d": "sk_stem4d_kernel" if os.environ.get("SK4_NO_GSUM") else
+                            "sk_stem4d_gsum_kernel" if os.environ.get("SK4_NO_PRE") else "sk_stem4d_pre_kernel",
                             "bpla": "sk_bpla_fast_kernel"}[kind]
         cpu, parity = None, None
         if not a.no_cpu_baseline and world == 1 and not a.cpu_stub:  # rank 0 at N=1 only
