@@ -153,11 +153,11 @@ def algorithmic(kind, shapes, x, y):
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
                 72.0 * stem4d_cells(lens, x, y)
-        if os.environ.get("SK4_NO_PRE") or int(lens[y].max()) + 1 > 256:
+        if os.environ.get("SK4_NO_PRE") or int(lens[y].max()) + 1 > 512:
             # full_dp with the K chain summed (stem4d.hip): G0, G1 written once
             # (16 B), G0 of (i,j-1), G1 of (i+1,j) and the stacking G0 of
             # (i+1,j-1) read once (24 B); SURVEY §8d's 72 B counted K0, K1 too
-            # (|y| > 255: CPL 8, or k tiles past 511, measured on this kernel)
+            # (|y| > 511: k tiles, which keep this kernel)
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 "40 B per (i,j,k,l) cell (G0, G1 written; G0, G1, stacking G0 read; SURVEY §8d's 72 B " \
                 "less the K states, which are summed), [n(n+1)/2][m(m+1)/2] cells", \
