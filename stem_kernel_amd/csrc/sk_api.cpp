@@ -383,6 +383,162 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     const uint64_t k = ((uint64_t)key_c << 32) | key_p;
     return (uint32_t)(std::lower_bound(phi_raw.begin(), phi_raw.end(), k) - phi_raw.begin());
   };
+  // y-role records of one example (its nodes sorted by length, the IY sweep
+  // schedule, node-major edges), formed from its x-role arrays once the loop
+  // below has packed them: independent per example, so they run on host
+  // threads and are appended in example order (bit-identical to a serial pass)
+  struct YJob {
+    int nb0, ebase, bbase, nl;
+    bool big;
+  };
+  struct YOut {
+    std::vector<uint32_t> ysc, ye2, yn_a, yn_b, yn_c;
+    std::vector<int32_t> ycs;
+    std::vector<uint4> yrec;
+    std::vector<float> yn_w, yn_nbp, yn_p0;
+    std::vector<double> yn_P;
+    int nch = 0;
+    std::string err;
+  };
+  std::vector<YJob> yjobs;
+  yjobs.reserve(n);
+  auto pack_y = [&](const YJob& J, YOut& Y) {
+    const int nl = J.nl, ebase = J.ebase, bbase = J.bbase;
+    const bool big = J.big;
+    // y-role numbering for the stem kernel: nodes sorted by length (span
+    // last - first), so the nodes inside a row's length band are one index
+    // range and a node's children (strictly shorter) come before it; edges
+    // grouped by parent level (the IY sweep walks levels) and contiguous per
+    // parent, packed child:11 | parent:11 | gaps:10 in sorted ids.
+    {
+      std::vector<int> srt(nl);
+      std::iota(srt.begin(), srt.end(), 0);
+      auto len_of = [&](int k) { return P.nd_b[J.nb0 + k] & 0xffff; };
+      std::stable_sort(srt.begin(), srt.end(), [&](int a, int b) { return len_of(a) < len_of(b); });
+      std::vector<int> pos(nl);
+      for (int i = 0; i < nl; ++i) pos[srt[i]] = i;
+      const int nb0 = J.nb0;
+      // IY sweep schedule.  The sweep is a stream of chunks of 64 edges: a
+      // chunk's R[child] reads are issued after the previous chunk's
+      // atomics, so an edge may go into any chunk after the one holding the
+      // last edge of its child (every node's value is final by then).  List
+      // scheduling, priority = height of the parent (longest path up to a
+      // root; the critical chain first), then the child's length; chunks
+      // are padded with dummy records (child == parent: weight 0).
+      if (big) {  // no sweep schedule: the big-y kernel walks the levels
+        const int lmax = nl ? (int)(P.nd_b[nb0 + srt[nl - 1]] & 0xffff) : 0;
+        for (int v = 0; v <= lmax + 1; ++v) Y.ycs.push_back(0);
+        Y.nch = 0;
+      } else {
+        std::vector<uint32_t> er;       // records child:11 | parent:11 | gaps:10
+        std::vector<int> epar, ech;
+        std::vector<std::vector<int>> by_child(nl), parents(nl);
+        for (int k = 0; k < nl; ++k) {
+          const uint32_t a = P.nd_a[nb0 + k];
+          const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
+          for (uint32_t t = 0; t < ne; ++t) {
+            const uint2 rec = P.ed[ebase + el + t];  // {child | gaps<<16, parent}
+            const int c = pos[rec.x & 0xffff], q = pos[k];
+            by_child[c].push_back((int)er.size());
+            parents[c].push_back(q);
+            epar.push_back(q);
+            ech.push_back(c);
+            er.push_back((uint32_t)c | ((uint32_t)q << 11) | ((rec.x >> 16) << 22));
+          }
+        }
+        const int ne_all = (int)er.size();
+        // sorted ids: a parent is strictly longer, so it has a larger id
+        std::vector<int> h(nl, 0), rem(nl, 0);
+        for (int i = nl - 1; i >= 0; --i)
+          for (int q : parents[i]) h[i] = std::max(h[i], h[q] + 1);
+        for (int f = 0; f < ne_all; ++f) rem[epar[f]]++;
+        typedef std::pair<std::pair<int, int>, int> Key;  // {{-height, child len}, edge}
+        std::priority_queue<Key, std::vector<Key>, std::greater<Key>> ready;
+        auto push_edges_of = [&](int c) {
+          for (int f : by_child[c])
+            ready.push({{-h[epar[f]], (int)(P.nd_b[nb0 + srt[c]] & 0xffff)}, f});
+        };
+        for (int c = 0; c < nl; ++c)
+          if (rem[c] == 0) push_edges_of(c);
+        std::vector<int32_t> cm;  // prefix maximum of the children's lengths
+        int32_t run = -1, placed = 0;
+        std::vector<int> take, done;
+        while (!ready.empty()) {
+          take.clear();
+          done.clear();
+          while (!ready.empty() && (int)take.size() < 64) {
+            take.push_back(ready.top().second);
+            ready.pop();
+          }
+          for (int f : take) {
+            run = std::max<int32_t>(run, (int32_t)(P.nd_b[nb0 + srt[ech[f]]] & 0xffff));
+            if (--rem[epar[f]] == 0) done.push_back(epar[f]);
+          }
+          if (sweep_lanes_greedy) {
+            uint32_t lanes[64];
+            assign_sweep_lanes(take, er, nl, lanes);
+            Y.ysc.insert(Y.ysc.end(), lanes, lanes + 64);
+          } else {
+            for (int f : take) Y.ysc.push_back(er[f]);
+            for (int j = (int)take.size(); j < 64; ++j) {
+              const uint32_t d = (uint32_t)(j % std::max(nl, 1));
+              Y.ysc.push_back(d | (d << 11));
+            }
+          }
+          placed += (int)take.size();
+          cm.push_back(run);
+          for (int q : done) push_edges_of(q);  // ready from the next chunk on
+        }
+        if (placed != ne_all) {
+          Y.err = "IY sweep schedule: DAG has a cycle";
+          return;
+        }
+        const int nch = (int)cm.size();
+        // first chunk whose prefix maximum reaches v, v = 0 .. lmax+1
+        const int lmax = nl ? (int)(P.nd_b[nb0 + srt[nl - 1]] & 0xffff) : 0;
+        for (int v = 0, c = 0; v <= lmax + 1; ++v) {
+          while (c < nch && cm[c] < v) ++c;
+          Y.ycs.push_back(c);
+        }
+        Y.nch = nch;
+      }
+      // node-major copy of the edges in sorted order (the MATCH sums of a
+      // run of consecutive nodes read one contiguous edge range); a node's
+      // record keeps its first edge there, E(q) = prefix sum of n_edges
+      const int ye2_base = (int)Y.ye2.size();
+      for (int i = 0; i < nl; ++i) {
+        const int k = srt[i];
+        const uint32_t a = P.nd_a[nb0 + k];
+        const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
+        const uint32_t nbf = a >> 24, bl = P.nd_b[nb0 + k] >> 16;
+        Y.yn_a.push_back(((uint32_t)Y.ye2.size() - ye2_base) | (a & 0xffff0000u));
+        for (uint32_t t = 0; t < ne; ++t) {
+          const uint2 rec = P.ed[ebase + el + t];
+          Y.ye2.push_back(big ? 0u : (uint32_t)pos[rec.x & 0xffff] | ((uint32_t)i << 11) |
+                                         ((rec.x >> 16) << 22));
+        }
+        // c = loop leaf-edge gaps:16 | first bp-freq code:4 | single-entry flag
+        // (one bp-freq entry, no gap column: the closed-form node score)
+        const bool one = nbf == 1 && P.nd_nbp[nb0 + k] == 0.0f;
+        const uint32_t bc0 = nbf ? P.bpf_code[bbase + bl] & 0xf : 0u;
+        Y.yn_c.push_back((P.nd_c[nb0 + k] & 0xffff) | (bc0 << 16) | ((one ? 1u : 0u) << 24));
+        Y.yn_p0.push_back(nbf ? P.bpf_p[bbase + bl] : 0.0f);
+        {
+          uint4 r;
+          r.x = Y.yn_a.back();
+          r.y = Y.yn_c.back();
+          std::memcpy(&r.z, &P.nd_w[nb0 + k], 4);
+          std::memcpy(&r.w, &Y.yn_p0.back(), 4);
+          Y.yrec.push_back(r);
+        }
+        Y.yn_b.push_back(P.nd_b[nb0 + k]);
+        Y.yn_w.push_back(P.nd_w[nb0 + k]);
+        Y.yn_nbp.push_back(P.nd_nbp[nb0 + k]);
+        Y.yn_P.push_back(P.nd_P[nb0 + k]);
+      }
+    }
+
+  };
   P.ex_node_base.push_back(0);
   P.ex_edge_base.push_back(0);
   P.ex_bpf_base.push_back(0);
@@ -473,143 +629,9 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     const bool big = nl > 2048 || big_gap;
     P.ex_big.push_back(big ? 1 : 0);
 
-    // y-role numbering for the stem kernel: nodes sorted by length (span
-    // last - first), so the nodes inside a row's length band are one index
-    // range and a node's children (strictly shorter) come before it; edges
-    // grouped by parent level (the IY sweep walks levels) and contiguous per
-    // parent, packed child:11 | parent:11 | gaps:10 in sorted ids.
-    {
-      std::vector<int> srt(nl);
-      std::iota(srt.begin(), srt.end(), 0);
-      auto len_of = [&](int k) { return P.nd_b[P.ex_node_base.back() + k] & 0xffff; };
-      std::stable_sort(srt.begin(), srt.end(), [&](int a, int b) { return len_of(a) < len_of(b); });
-      std::vector<int> pos(nl);
-      for (int i = 0; i < nl; ++i) pos[srt[i]] = i;
-      const int nb0 = P.ex_node_base.back();
-      // IY sweep schedule.  The sweep is a stream of chunks of 64 edges: a
-      // chunk's R[child] reads are issued after the previous chunk's
-      // atomics, so an edge may go into any chunk after the one holding the
-      // last edge of its child (every node's value is final by then).  List
-      // scheduling, priority = height of the parent (longest path up to a
-      // root; the critical chain first), then the child's length; chunks
-      // are padded with dummy records (child == parent: weight 0).
-      if (big) {  // no sweep schedule: the big-y kernel walks the levels
-        const int lmax = nl ? (int)(P.nd_b[nb0 + srt[nl - 1]] & 0xffff) : 0;
-        P.ex_ysc_base.push_back((int32_t)(P.ysc.size() / 64));
-        P.ex_ycs_base.push_back((int32_t)P.ycs.size());
-        for (int v = 0; v <= lmax + 1; ++v) P.ycs.push_back(0);
-        P.ex_nch.push_back(0);
-      } else {
-        std::vector<uint32_t> er;       // records child:11 | parent:11 | gaps:10
-        std::vector<int> epar, ech;
-        std::vector<std::vector<int>> by_child(nl), parents(nl);
-        for (int k = 0; k < nl; ++k) {
-          const uint32_t a = P.nd_a[nb0 + k];
-          const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
-          for (uint32_t t = 0; t < ne; ++t) {
-            const uint2 rec = P.ed[ebase + el + t];  // {child | gaps<<16, parent}
-            const int c = pos[rec.x & 0xffff], q = pos[k];
-            by_child[c].push_back((int)er.size());
-            parents[c].push_back(q);
-            epar.push_back(q);
-            ech.push_back(c);
-            er.push_back((uint32_t)c | ((uint32_t)q << 11) | ((rec.x >> 16) << 22));
-          }
-        }
-        const int ne_all = (int)er.size();
-        // sorted ids: a parent is strictly longer, so it has a larger id
-        std::vector<int> h(nl, 0), rem(nl, 0);
-        for (int i = nl - 1; i >= 0; --i)
-          for (int q : parents[i]) h[i] = std::max(h[i], h[q] + 1);
-        for (int f = 0; f < ne_all; ++f) rem[epar[f]]++;
-        typedef std::pair<std::pair<int, int>, int> Key;  // {{-height, child len}, edge}
-        std::priority_queue<Key, std::vector<Key>, std::greater<Key>> ready;
-        auto push_edges_of = [&](int c) {
-          for (int f : by_child[c])
-            ready.push({{-h[epar[f]], (int)(P.nd_b[nb0 + srt[c]] & 0xffff)}, f});
-        };
-        for (int c = 0; c < nl; ++c)
-          if (rem[c] == 0) push_edges_of(c);
-        P.ex_ysc_base.push_back((int32_t)(P.ysc.size() / 64));
-        std::vector<int32_t> cm;  // prefix maximum of the children's lengths
-        int32_t run = -1, placed = 0;
-        std::vector<int> take, done;
-        while (!ready.empty()) {
-          take.clear();
-          done.clear();
-          while (!ready.empty() && (int)take.size() < 64) {
-            take.push_back(ready.top().second);
-            ready.pop();
-          }
-          for (int f : take) {
-            run = std::max<int32_t>(run, (int32_t)(P.nd_b[nb0 + srt[ech[f]]] & 0xffff));
-            if (--rem[epar[f]] == 0) done.push_back(epar[f]);
-          }
-          if (sweep_lanes_greedy) {
-            uint32_t lanes[64];
-            assign_sweep_lanes(take, er, nl, lanes);
-            P.ysc.insert(P.ysc.end(), lanes, lanes + 64);
-          } else {
-            for (int f : take) P.ysc.push_back(er[f]);
-            for (int j = (int)take.size(); j < 64; ++j) {
-              const uint32_t d = (uint32_t)(j % std::max(nl, 1));
-              P.ysc.push_back(d | (d << 11));
-            }
-          }
-          placed += (int)take.size();
-          cm.push_back(run);
-          for (int q : done) push_edges_of(q);  // ready from the next chunk on
-        }
-        if (placed != ne_all) {
-          err = "IY sweep schedule: DAG has a cycle";
-          return SK_ERR_INVALID;
-        }
-        const int nch = (int)cm.size();
-        // first chunk whose prefix maximum reaches v, v = 0 .. lmax+1
-        const int lmax = nl ? (int)(P.nd_b[nb0 + srt[nl - 1]] & 0xffff) : 0;
-        P.ex_ycs_base.push_back((int32_t)P.ycs.size());
-        for (int v = 0, c = 0; v <= lmax + 1; ++v) {
-          while (c < nch && cm[c] < v) ++c;
-          P.ycs.push_back(c);
-        }
-        P.ex_nch.push_back(nch);
-        P.max_nch = std::max(P.max_nch, nch);
-      }
-      // node-major copy of the edges in sorted order (the MATCH sums of a
-      // run of consecutive nodes read one contiguous edge range); a node's
-      // record keeps its first edge there, E(q) = prefix sum of n_edges
-      const int ye2_base = (int)P.ye2.size();
-      for (int i = 0; i < nl; ++i) {
-        const int k = srt[i];
-        const uint32_t a = P.nd_a[nb0 + k];
-        const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
-        const uint32_t nbf = a >> 24, bl = P.nd_b[nb0 + k] >> 16;
-        P.yn_a.push_back(((uint32_t)P.ye2.size() - ye2_base) | (a & 0xffff0000u));
-        for (uint32_t t = 0; t < ne; ++t) {
-          const uint2 rec = P.ed[ebase + el + t];
-          P.ye2.push_back(big ? 0u : (uint32_t)pos[rec.x & 0xffff] | ((uint32_t)i << 11) |
-                                         ((rec.x >> 16) << 22));
-        }
-        // c = loop leaf-edge gaps:16 | first bp-freq code:4 | single-entry flag
-        // (one bp-freq entry, no gap column: the closed-form node score)
-        const bool one = nbf == 1 && P.nd_nbp[nb0 + k] == 0.0f;
-        const uint32_t bc0 = nbf ? P.bpf_code[bbase + bl] & 0xf : 0u;
-        P.yn_c.push_back((P.nd_c[nb0 + k] & 0xffff) | (bc0 << 16) | ((one ? 1u : 0u) << 24));
-        P.yn_p0.push_back(nbf ? P.bpf_p[bbase + bl] : 0.0f);
-        {
-          uint4 r;
-          r.x = P.yn_a.back();
-          r.y = P.yn_c.back();
-          std::memcpy(&r.z, &P.nd_w[nb0 + k], 4);
-          std::memcpy(&r.w, &P.yn_p0.back(), 4);
-          P.yrec.push_back(r);
-        }
-        P.yn_b.push_back(P.nd_b[nb0 + k]);
-        P.yn_w.push_back(P.nd_w[nb0 + k]);
-        P.yn_nbp.push_back(P.nd_nbp[nb0 + k]);
-        P.yn_P.push_back(P.nd_P[nb0 + k]);
-      }
-    }
+    // (the y-role records are formed after this loop, per example in
+    // parallel: pack_y below)
+    yjobs.push_back(YJob{P.ex_node_base.back(), ebase, bbase, nl, big});
 
     // x-role schedule: rows in reference (post-)order; a row's HBM slot is
     // recycled once its last parent has been produced (LIFO free list keeps
@@ -981,6 +1003,42 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     P.max_bpf = std::max(P.max_bpf, (int)P.bpf_code.size() - bbase);
     P.max_nlev = std::max(P.max_nlev, nlev);
     P.max_len = std::max(P.max_len, X.len);
+  }
+  {
+    std::vector<YOut> yo(yjobs.size());
+    const int nthr = (int)std::max<size_t>(1, std::min<size_t>({yjobs.size() / 8 + 1, (size_t)16,
+                                                                (size_t)std::max(1u, std::thread::hardware_concurrency())}));
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t e = next.fetch_add(1); e < yjobs.size(); e = next.fetch_add(1)) pack_y(yjobs[e], yo[e]);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthr; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    for (size_t e = 0; e < yo.size(); ++e) {
+      YOut& Y = yo[e];
+      if (!Y.err.empty()) {
+        err = Y.err;
+        return SK_ERR_INVALID;
+      }
+      P.ex_ysc_base.push_back((int32_t)(P.ysc.size() / 64));
+      P.ysc.insert(P.ysc.end(), Y.ysc.begin(), Y.ysc.end());
+      P.ex_ycs_base.push_back((int32_t)P.ycs.size());
+      P.ycs.insert(P.ycs.end(), Y.ycs.begin(), Y.ycs.end());
+      P.ex_nch.push_back(Y.nch);
+      P.max_nch = std::max(P.max_nch, Y.nch);
+      P.ye2.insert(P.ye2.end(), Y.ye2.begin(), Y.ye2.end());
+      P.yn_a.insert(P.yn_a.end(), Y.yn_a.begin(), Y.yn_a.end());
+      P.yn_b.insert(P.yn_b.end(), Y.yn_b.begin(), Y.yn_b.end());
+      P.yn_c.insert(P.yn_c.end(), Y.yn_c.begin(), Y.yn_c.end());
+      P.yn_p0.insert(P.yn_p0.end(), Y.yn_p0.begin(), Y.yn_p0.end());
+      P.yrec.insert(P.yrec.end(), Y.yrec.begin(), Y.yrec.end());
+      P.yn_w.insert(P.yn_w.end(), Y.yn_w.begin(), Y.yn_w.end());
+      P.yn_nbp.insert(P.yn_nbp.end(), Y.yn_nbp.begin(), Y.yn_nbp.end());
+      P.yn_P.insert(P.yn_P.end(), Y.yn_P.begin(), Y.yn_P.end());
+      YOut().ysc.swap(Y.ysc);  // free as we go
+    }
   }
   return SK_OK;
 }
