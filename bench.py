@@ -2,9 +2,10 @@
 """Benchmark of the stem-kernel Gram engine on MI355X.
 
 Default workload (BASELINE.json north_star / metric, ``--config ns``): the
-4096 x 4096 Gram matrix of SuStemStrKernel (== StemStrKernel of
-stem_kernel_lite/ss_kernel.h: DAG stem kernel + profile string kernel,
-default parameters of stem_kernel_lite/main.cpp:103-149) over synthetic RNA
+4096 x 4096 Gram matrix of LSuStemStrKernel -- the reference CLI's --log mode
+(stem_kernel_lite/main.cpp:187-191; its plain SuStemStrKernel default never
+runs, :180-186): beta*log(DAG stem kernel) + alpha*log(profile string kernel),
+default parameters of stem_kernel_lite/main.cpp:103-149 -- over synthetic RNA
 sequences of L = 200 nt (splitmix64 sequences, Nussinov-Boltzmann
 base-pairing probabilities, --basepair 0.01).  Units are Gram cells K(i,j),
 i <= j, exactly the cells the reference evaluates
@@ -58,9 +59,15 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 PEAK_FP64_TFS = 78.6    # FP64 vector
 
-# name -> kernel, n examples, length, slices, config id (seed 0x5EED0000+id)
+# name -> kernel family, n examples, length, slices, config id (seed
+# 0x5EED0000+id); `cls` overrides the family's kernel class.  NS runs the
+# reference CLI's --log mode (LSuStemStrKernel, stem_kernel_lite/main.cpp:
+# 187-191): plain SuStemStrKernel is the CLI's dead default (it prints a memory
+# estimate and returns, :180-186), and in the --log composition both DPs reach
+# the written Gram (in the plain sum the stem term is ~1e-32 of the string
+# term at L=200).  Same two DPs, plus a log epilogue in sk_combine_kernel.
 CONFIGS = {
-    "ns": dict(kernel="ss", n=4096, L=200, slices=48, cid=2, cpu_pairs=12288),
+    "ns": dict(kernel="ss", cls="LSuStemStrKernel", n=4096, L=200, slices=48, cid=2, cpu_pairs=12288),
     "c2": dict(kernel="ss", n=256, L=150, slices=4, cid=1, cpu_pairs=12288),
     "c3": dict(kernel="stem4d", n=1024, L=200, slices=2050, cid=2, cpu_pairs=32),
     "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=16, cid=3, cpu_pairs=196608),
@@ -122,10 +129,39 @@ def build_inputs(cfg, a):
     return seqs, ska.Dataset.synthetic(seqs, th=0.01, threads=threads)
 
 
-def make_kernel(kind):
+def make_kernel(kind, cls=None):
     import stem_kernel_amd as ska
+    if cls:
+        return getattr(ska, cls)()
     return {"ss": ska.SuStemStrKernel, "stem": ska.SuStemKernel, "stem4d": ska.StemKernel4D,
             "bpla": ska.BPLAKernel}[kind]()
+
+
+def components(kern):
+    """The component kernels of a stem + string composition (def_kernel.h:
+    86-111, 165-190): the DAG stem DP (SuStemKernel) and the profile string
+    kernel (StringKernel) with the composition's own parameters, so each DP is
+    checked on its own -- in a plain sum the stem term is invisible."""
+    import stem_kernel_amd as ska
+    p = kern.params
+    if p.kind in (ska.SU_STEM_STR, ska.LSU_STEM_STR):
+        return {"stem": ska.SuStemKernel(loop_gap=p.loop_gap, beta=p.beta, len_band=p.len_band),
+                "string": ska.StringKernel(gap=p.gap, alpha=p.alpha)}
+    return {}
+
+
+def compose(kind, p, stem, string):
+    """def_kernel.h:86-111 (SuStemStr: K_stem + K_str) and :165-190
+    (LSuStemStr: beta*log K_stem + alpha*log K_str), from the components,
+    in oracle/pyoracle.py kernel_value's operation order."""
+    import math
+
+    import stem_kernel_amd as ska
+    if kind == ska.SU_STEM_STR:
+        return stem + string
+    if kind == ska.LSU_STEM_STR:
+        return (p.beta * math.log(stem) + 0.0) + (p.alpha * math.log(string) + 0.0)
+    raise ValueError(kind)
 
 
 # ------------------------------------------------------------------ rooflines
@@ -268,7 +304,8 @@ def host_threads():
 def cpu_baseline(cfg, data, n_pairs, seed=7):
     """The C oracle (plain-C restatement of the reference kernels, oracle/)
     on a bounded random sample of the same Gram's pairs, host threads.
-    Returns (baseline dict, sampled pairs, oracle values)."""
+    Returns (baseline dict, sampled pairs, oracle values, oracle values of
+    each component DP of a composition)."""
     from concurrent.futures import ThreadPoolExecutor
 
     import stem_kernel_amd as ska
@@ -277,8 +314,9 @@ def cpu_baseline(cfg, data, n_pairs, seed=7):
     kind = cfg["kernel"]
     npool = min(len(data), 48 if kind == "stem4d" else 512)
     idx = [int(i) for i in rng.choice(len(data), size=npool, replace=False)]
-    kern = make_kernel(kind)
+    kern = make_kernel(kind, cfg.get("cls"))
     p = kern.params
+    split = bool(components(kern))
     if kind == "stem4d":
         prep = {i: (data[i].lower(), ska.fold(data[i])) for i in idx}
 
@@ -292,8 +330,13 @@ def cpu_baseline(cfg, data, n_pairs, seed=7):
             return po.OMData(rows, [ska.fold(r.replace("-", "")) for r in rows], 0.01)
         om = {i: om_of(i) for i in idx}
 
-        def one(ab):
-            return po.kernel_value(p.kind, om[ab[0]], om[ab[1]], p)
+        if split:  # the two DPs of the composition, each kept for parity
+            def one(ab):
+                x, y = om[ab[0]], om[ab[1]]
+                return (po.kernel_value(0, x, y, p), po.kernel_value(2, x, y, p))
+        else:
+            def one(ab):
+                return po.kernel_value(p.kind, om[ab[0]], om[ab[1]], p)
     pairs = []
     while len(pairs) < n_pairs:
         a, b = sorted(rng.choice(idx, size=2))
@@ -301,15 +344,20 @@ def cpu_baseline(cfg, data, n_pairs, seed=7):
     cores = host_threads()
     t = time.perf_counter()
     with ThreadPoolExecutor(cores) as ex:  # ctypes releases the GIL
-        vals = np.array(list(ex.map(one, pairs)))
+        vals = list(ex.map(one, pairs))
+        if split:
+            comp = {"stem": np.array([v[0] for v in vals]), "string": np.array([v[1] for v in vals])}
+            vals = np.array([compose(p.kind, p, a, b) for a, b in vals])
+        else:
+            comp, vals = {}, np.array(vals)
     dt = time.perf_counter() - t
-    what = {"ss": "SuStemStrKernel", "stem": "SuStemKernel", "stem4d": "4-D StemKernel full_dp",
-            "bpla": "BPLAKernel"}[kind]
+    what = cfg.get("cls") or {"ss": "SuStemStrKernel", "stem": "SuStemKernel",
+                              "stem4d": "4-D StemKernel full_dp", "bpla": "BPLAKernel"}[kind]
     return {"value": n_pairs / dt, "unit": "sequence-pairs/sec", "cores": cores, "kind": "port",
             "host_nproc": os.cpu_count(),
             "sample": f"{n_pairs} random pairs (i<=j) among {npool} of the {len(data)} examples, "
                       f"{what} via the C oracle on {cores} threads (all host cores this job "
-                      f"may use: affinity capped by OMP_NUM_THREADS), {dt:.1f}s wall"}, pairs, vals
+                      f"may use: affinity capped by OMP_NUM_THREADS), {dt:.1f}s wall"}, pairs, vals, comp
 
 
 # ------------------------------------------------------------------ ranks
@@ -378,7 +426,7 @@ class GpuEngine:
         self.ctx.upload(self.ds)
         torch.cuda.synchronize(self.dev)
         self.t_upload = time.perf_counter() - t0
-        self.kern = make_kernel(cfg["kernel"])
+        self.kern = make_kernel(cfg["kernel"], cfg.get("cls"))
         if self.dist_on:
             shard.rccl_init(self.ctx)
         else:
@@ -449,7 +497,7 @@ class CpuStubEngine(GpuEngine):
         self.data, self.ds = build_inputs(cfg, a)
         self.t_build = time.perf_counter() - t0
         self.t_upload = 0.0
-        self.kern = make_kernel(cfg["kernel"])
+        self.kern = make_kernel(cfg["kernel"], cfg.get("cls"))
         self.world, self.rank = world, rank
         self.checked = 0
 
@@ -627,17 +675,29 @@ def main():
                             "bpla": "sk_bpla_fast_kernel"}[kind]
         cpu, parity = None, None
         if not a.no_cpu_baseline and world == 1 and not a.cpu_stub:  # rank 0 at N=1 only
-            cpu, cpairs, cvals = cpu_baseline(cfg, eng.data, a.cpu_pairs)
+            cpu, cpairs, cvals, ccomp = cpu_baseline(cfg, eng.data, a.cpu_pairs)
             # the baseline's oracle values double as a parity check of the
-            # benched kernel classes on the same inputs (1e-6 relative)
+            # benched kernel classes on the same inputs (1e-6 relative): the
+            # headline kernel, and each DP of a composition on its own
             cx = np.array([p[0] for p in cpairs], np.int32)
             cy = np.array([p[1] for p in cpairs], np.int32)
-            got = eng.ctx.pairs(eng.ds, eng.kern, cx, cy)
-            err = float(np.max(np.abs(got - cvals) / np.maximum(np.abs(cvals), 1e-300)))
+
+            def rel(got, ref):
+                return float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300)))
+            err = rel(eng.ctx.pairs(eng.ds, eng.kern, cx, cy), cvals)
             parity = {"pairs": int(cx.size), "max_rel_err": err, "tol": 1e-6,
                       "ok": bool(err < 1e-6), "against": "C oracle (cpu_baseline sample)"}
+            if ccomp:
+                parity["components"] = {}
+                for name, ck in components(eng.kern).items():
+                    e = rel(eng.ctx.pairs(eng.ds, ck, cx, cy), ccomp[name])
+                    parity["components"][name] = {
+                        "kernel": type(ck).__name__, "max_rel_err": e,
+                        "ref_range": [float(np.min(ccomp[name])), float(np.max(ccomp[name]))]}
+                    parity["ok"] = parity["ok"] and bool(e < 1e-6)
+                    parity["max_rel_err"] = max(parity["max_rel_err"], e)
         kdesc = {
-            "ss": "SuStemStrKernel(alpha=0.2,beta=0.3,loop_gap=0.2,gap=0.8,band=10)",
+            "ss": (cfg.get("cls") or "SuStemStrKernel") + "(alpha=0.2,beta=0.3,loop_gap=0.2,gap=0.8,band=10)",
             "stem": "SuStemKernel(beta=0.3,loop_gap=0.2,band=10)",
             "stem4d": "StemKernel<double,BPMatrix>(gap=0.8,stack=1.0,subst=0.5,bp_bound=0) full_dp",
             "bpla": "BPLAKernel(gap=-8,ext=-0.75,alpha=4.5,beta=0.11)"}[kind]
@@ -664,6 +724,12 @@ def main():
                 "step_cells": step_kind,
                 "n_sequences": a.n, "length": cfg["L"], "pairs_per_step_per_gpu": per,
                 "kernel": kdesc, "basepair_th": 0.01,
+                "cli_mode": {"ns": "stem_kernel_lite --log (LSuStemStrKernel, main.cpp:187-191); the CLI's "
+                                   "plain SuStemStrKernel default only estimates memory (main.cpp:180-186)",
+                             "c2": "ss_kernel.h StemStrKernel (SuStemStr sum; the --log mode costs the same)",
+                             "c5": "stem_kernel_lite --no-string (SuStemKernel, main.cpp:193-198)",
+                             "c3": "stem_kernel (4-D) default -p BPMatrix full_dp",
+                             "c4": "bpla_kernel default"}[a.config],
                 "parallelism": f"cyclic cell plan x{world} (sk_comm_allgather, RCCL)"
                                + (" -- full Gram via sk_gram_sharded" if a.full else ""),
                 "mean_nodes": float(shapes[:, 0].mean()), "mean_edges": float(shapes[:, 1].mean()),

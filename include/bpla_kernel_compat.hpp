@@ -135,7 +135,8 @@ class BPLAKernel : public KernelBase<ValueType, DataT> {
     p.ext = param.at(3);
     std::vector<std::pair<std::string, Data>> ex{{"+1", x}, {"+1", y}};
     Engine& E = Engine::get();
-    sk_dataset* ds = E.dataset(ex, BuildSpec());
+    const Engine::DsPtr hold = E.dataset(ex, BuildSpec());
+    sk_dataset* ds = hold.get();
     const int32_t a = 0, b = 1;
     double v = 0.0, g[4];
     check(sk_bpla_gradients(E.ctx(), ds, ds, &p, &a, &b, 1, &v, g), E.ctx());

@@ -80,6 +80,7 @@ struct ExampleTraits;
 // row).
 class Engine {
  public:
+  typedef std::shared_ptr<sk_dataset> DsPtr;
   static Engine& get() {
     static Engine e;
     return e;
@@ -106,23 +107,29 @@ class Engine {
   }
   int world() const { return world_; }
 
-  // Packed, uploaded dataset of an ExampleSet of (label, D).
+  // Packed, uploaded dataset of an ExampleSet of (label, D).  The handle is
+  // shared: the cache keeps at most 8 sets and evicts the least recently used
+  // one, but a set stays alive while any caller still holds its handle (the
+  // predict loop adds one single-example test set per row beside one train
+  // set, so eviction must never free a set a call is still using).
   template <class ExampleSet>
-  sk_dataset* dataset(const ExampleSet& ex, const BuildSpec& spec) {
+  DsPtr dataset(const ExampleSet& ex, const BuildSpec& spec) {
     typedef typename ExampleSet::value_type::second_type D;
     const uint64_t key = fingerprint(ex, spec);
     {
       std::lock_guard<std::mutex> g(mu_);
       open_locked();
       auto it = cache_.find(key);
-      if (it != cache_.end()) return it->second.get();
+      if (it != cache_.end()) {
+        it->second.used = ++tick_;
+        return it->second.ds;
+      }
     }
     DsPtr ds = make_ds();
     for (const auto& e : ex) ExampleTraits<D>::add(ds.get(), e.first, e.second, spec);
     std::lock_guard<std::mutex> g(mu_);
     check(sk_dataset_upload(ctx_, ds.get()), ctx_);
-    if (cache_.size() >= 8) cache_.clear();
-    return cache_.emplace(key, std::move(ds)).first->second.get();  // (a racing build of the same set is dropped)
+    return insert_lru(cache_, key, std::move(ds), 8);  // (a racing build of the same set is dropped)
   }
 
   // One pair through the Kernel concept (Kernel::operator()(x, y)): each
@@ -131,11 +138,11 @@ class Engine {
   // uploaded and evaluated in one launch.
   template <class D>
   double pair(const D& x, const D& y, const BuildSpec& spec, const sk_kernel_params& p) {
-    sk_dataset* bx = single(x, spec);
-    sk_dataset* by = single(y, spec);
+    const DsPtr bx = single(x, spec);
+    const DsPtr by = single(y, spec);  // may evict bx from the cache: bx is still held
     DsPtr ds = make_ds();
-    check(sk_dataset_add_copy(ds.get(), bx, 0));
-    check(sk_dataset_add_copy(ds.get(), by, 0));
+    check(sk_dataset_add_copy(ds.get(), bx.get(), 0));
+    check(sk_dataset_add_copy(ds.get(), by.get(), 0));
     std::lock_guard<std::mutex> g(mu_);
     open_locked();
     check(sk_dataset_upload(ctx_, ds.get()), ctx_);
@@ -180,11 +187,30 @@ class Engine {
   }
 
  private:
-  typedef std::unique_ptr<sk_dataset, int (*)(sk_dataset*)> DsPtr;
+  struct Entry {
+    DsPtr ds;
+    uint64_t used;
+  };
   static DsPtr make_ds() {
     sk_dataset* raw = nullptr;
     check(sk_dataset_create(&raw));
     return DsPtr(raw, sk_dataset_free);
+  }
+  // caller holds mu_; evicts the least recently used entry when full (its
+  // set is freed when the last holder drops its handle)
+  DsPtr insert_lru(std::map<uint64_t, Entry>& m, uint64_t key, DsPtr ds, size_t cap) {
+    auto it = m.find(key);
+    if (it != m.end()) {
+      it->second.used = ++tick_;
+      return it->second.ds;
+    }
+    if (m.size() >= cap) {
+      auto old = m.begin();
+      for (auto j = m.begin(); j != m.end(); ++j)
+        if (j->second.used < old->second.used) old = j;
+      m.erase(old);
+    }
+    return m.emplace(key, Entry{std::move(ds), ++tick_}).first->second.ds;
   }
   Engine() {
     const char* e = std::getenv("SK_DEVICE");
@@ -199,7 +225,7 @@ class Engine {
     if (!ctx_) check(sk_open(device_, nullptr, &ctx_));
   }
   template <class D>
-  sk_dataset* single(const D& d, const BuildSpec& spec) {
+  DsPtr single(const D& d, const BuildSpec& spec) {
     Fnv f;
     ExampleTraits<D>::mix(f, d);
     const uint64_t t = spec.tag();
@@ -207,13 +233,15 @@ class Engine {
     {
       std::lock_guard<std::mutex> g(mu_);
       auto it = singles_.find(f.h);
-      if (it != singles_.end()) return it->second.get();
+      if (it != singles_.end()) {
+        it->second.used = ++tick_;
+        return it->second.ds;
+      }
     }
     DsPtr ds = make_ds();
     ExampleTraits<D>::add(ds.get(), "+1", d, spec);
     std::lock_guard<std::mutex> g(mu_);
-    if (singles_.size() >= 16384) singles_.clear();
-    return singles_.emplace(f.h, std::move(ds)).first->second.get();
+    return insert_lru(singles_, f.h, std::move(ds), 16384);
   }
   template <class ExampleSet>
   static uint64_t fingerprint(const ExampleSet& ex, const BuildSpec& spec) {
@@ -231,8 +259,9 @@ class Engine {
   int device_ = 0, world_ = 1;
   bool fold_notice_ = false;
   sk_context* ctx_ = nullptr;
-  std::map<uint64_t, DsPtr> cache_;
-  std::map<uint64_t, DsPtr> singles_;
+  uint64_t tick_ = 0;
+  std::map<uint64_t, Entry> cache_;
+  std::map<uint64_t, Entry> singles_;
 };
 
 // ------------------------------------------------------------------ kernels
@@ -284,7 +313,8 @@ class KernelMatrix {
                    uint /*n_th*/ = 1) {
     const auto t0 = std::chrono::steady_clock::now();
     Engine& E = Engine::get();
-    sk_dataset* ds = E.dataset(train, kernel.build_spec());
+    const Engine::DsPtr hold = E.dataset(train, kernel.build_spec());
+    sk_dataset* ds = hold.get();
     const uint n = (uint)train.size();
     resize(n, n);
     self_.assign(n, value_type());
@@ -305,8 +335,10 @@ class KernelMatrix {
                    bool norm_test = false, bool normalize = false, uint /*n_th*/ = 1) {
     const auto t0 = std::chrono::steady_clock::now();
     Engine& E = Engine::get();
-    sk_dataset* dtr = E.dataset(train, kernel.build_spec());
-    sk_dataset* dte = E.dataset(test, kernel.build_spec());
+    const Engine::DsPtr htr = E.dataset(train, kernel.build_spec());
+    const Engine::DsPtr hte = E.dataset(test, kernel.build_spec());  // may evict train: htr holds it
+    sk_dataset* dtr = htr.get();
+    sk_dataset* dte = hte.get();
     const uint nt = (uint)test.size(), ntr = (uint)train.size();
     resize(nt, ntr);
     for (uint i = 0; i != nt; ++i) label_[i] = test[i].first;
@@ -327,9 +359,11 @@ class KernelMatrix {
                           uint /*n_th*/ = 1, value_type* data_self = NULL) {
     const auto t0 = std::chrono::steady_clock::now();
     Engine& E = Engine::get();
-    sk_dataset* dtr = E.dataset(train, kernel.build_spec());
+    const Engine::DsPtr htr = E.dataset(train, kernel.build_spec());
     const ExampleSet one(1, data);
-    sk_dataset* dte = E.dataset(one, kernel.build_spec());
+    const Engine::DsPtr hte = E.dataset(one, kernel.build_spec());  // may evict train: htr holds it
+    sk_dataset* dtr = htr.get();
+    sk_dataset* dte = hte.get();
     std::vector<double> v(train.size());
     for (size_t i = 0; i < v.size() && i < matrix.size(); ++i) v[i] = (double)matrix[i];
     std::vector<int32_t> idx(sv_index.begin(), sv_index.end());
@@ -358,7 +392,8 @@ class KernelMatrix {
                          uint /*n_th*/ = 1) {
     const auto t0 = std::chrono::steady_clock::now();
     Engine& E = Engine::get();
-    sk_dataset* ds = E.dataset(train, kernel.build_spec());
+    const Engine::DsPtr hold = E.dataset(train, kernel.build_spec());
+    sk_dataset* ds = hold.get();
     std::vector<double> d(train.size());
     for (size_t i = 0; i < d.size() && i < diag.size(); ++i) d[i] = (double)diag[i];
     std::vector<int32_t> idx(sv_index.begin(), sv_index.end());

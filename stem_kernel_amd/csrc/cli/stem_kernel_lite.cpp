@@ -252,7 +252,7 @@ double now_s() {
 // stable C ABI (bzlib.h's BZFILE is opaque).
 class Bz2Writer {
  public:
-  explicit Bz2Writer(const std::string& path) {
+  explicit Bz2Writer(const std::string& path) : path_(path) {
     static std::string err;
     void* h = dlopen("libbz2.so.1", RTLD_NOW | RTLD_LOCAL);
     if (!h) h = dlopen("libbz2.so", RTLD_NOW | RTLD_LOCAL);
@@ -275,10 +275,10 @@ class Bz2Writer {
       throw err.c_str();
     }
   }
-  ~Bz2Writer() {
+  ~Bz2Writer() {  // on an error path only: finish() reports failures
     int e = 0;
     unsigned in = 0, out = 0;
-    if (bz_) close_(&e, bz_, 0, &in, &out);
+    if (bz_) close_(&e, bz_, 1, &in, &out);
     if (f_) std::fclose(f_);
   }
   void write(const std::string& s) {
@@ -286,7 +286,20 @@ class Bz2Writer {
     for (size_t o = 0; o < s.size(); o += 1u << 30) {
       const int n = (int)std::min<size_t>(s.size() - o, 1u << 30);
       write_(&e, bz_, const_cast<char*>(s.data() + o), n);
+      if (e != 0) fail();  // BZ_OK
     }
+  }
+  // flush the stream and close the file; a full disk or an I/O error throws
+  void finish() {
+    int e = 0;
+    unsigned in = 0, out = 0;
+    void* bz = bz_;
+    bz_ = nullptr;
+    if (bz) close_(&e, bz, 0, &in, &out);
+    FILE* f = f_;
+    f_ = nullptr;
+    const bool closed = f ? std::fclose(f) == 0 : true;
+    if (e != 0 || !closed) fail();
   }
 
  private:
@@ -298,6 +311,12 @@ class Bz2Writer {
   CloseFn close_ = nullptr;
   FILE* f_ = nullptr;
   void* bz_ = nullptr;
+  std::string path_;
+  [[noreturn]] void fail() const {
+    static std::string err;
+    err = path_ + ": cannot write";
+    throw err.c_str();
+  }
 };
 
 // text output (plain, gzip or bzip2 by suffix, as the reference's filtering
@@ -320,8 +339,21 @@ class TextSink {
   }
   void write(const std::string& s) {
     if (bz_) bz_->write(s);
-    else if (gz_) gzwrite(gz_, s.data(), (unsigned)s.size());
-    else out_ << s;
+    else if (gz_) {
+      if (!s.empty() && gzwrite(gz_, s.data(), (unsigned)s.size()) != (int)s.size()) fail();
+    } else if (!(out_ << s)) fail();
+  }
+  // the last write: flush and close, reporting a truncated file
+  void finish() {
+    if (bz_) bz_->finish();
+    else if (gz_) {
+      gzFile g = gz_;
+      gz_ = nullptr;
+      if (gzclose(g) != Z_OK) fail();
+    } else {
+      out_.close();
+      if (out_.fail()) fail();
+    }
   }
 
  private:
@@ -329,11 +361,17 @@ class TextSink {
   std::unique_ptr<Bz2Writer> bz_;
   gzFile gz_ = nullptr;
   std::ofstream out_;
+  [[noreturn]] void fail() const {
+    static std::string err;
+    err = path_ + ": cannot write";
+    throw err.c_str();
+  }
 };
 
 void write_text(const std::string& path, const std::string& text) {
   TextSink sink(path);
   sink.write(text);
+  sink.finish();
 }
 
 void flush_if_large(std::ostringstream& buf, std::unique_ptr<TextSink>& sink, const std::string& path,
@@ -344,6 +382,7 @@ void flush_if_large(std::ostringstream& buf, std::unique_ptr<TextSink>& sink, co
     sink->write(buf.str());
     buf.str("");
   }
+  if (final_flush) sink->finish();
 }
 
 // SVMPredict (libsvm/svm_util.cpp:11-80): one model, one prediction file;

@@ -95,10 +95,26 @@ int ctx_device(sk_context* ctx);
 void*& ctx_comm(sk_context* ctx);
 int ctx_fail(sk_context* ctx, int code, const std::string& msg);
 
+// What sk_comm_init leaves in the context: the communicator and the device
+// status word of sk_gram_sharded's agreement, allocated together so that a
+// sharded Gram has no failure point before its first collective.
+struct CommState {
+  ncclComm_t nc = nullptr;
+  int32_t* d_st = nullptr;  // 2 words: this rank's -status, the all-reduced max
+};
+
 void comm_destroy(void* comm) {
-  if (comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm));
+  CommState* c = static_cast<CommState*>(comm);
+  if (!c) return;
+  if (c->nc) (void)ncclCommDestroy(c->nc);
+  if (c->d_st) (void)hipFree(c->d_st);
+  delete c;
 }
 }  // namespace sk
+
+namespace {
+sk::CommState* comm_of(sk_context* ctx) { return static_cast<sk::CommState*>(sk::ctx_comm(ctx)); }
+}  // namespace
 
 extern "C" {
 
@@ -158,29 +174,39 @@ int sk_comm_init(sk_context* ctx, const uint8_t* id, size_t id_bytes, int32_t ra
   if (!ctx || !id || id_bytes < sizeof(ncclUniqueId) || world <= 0 || rank < 0 || rank >= world)
     return sk::ctx_fail(ctx, SK_ERR_INVALID, "sk_comm_init: bad argument");
   void*& c = sk::ctx_comm(ctx);
-  if (c) {
-    (void)ncclCommDestroy(static_cast<ncclComm_t>(c));
-    c = nullptr;
-  }
+  sk::comm_destroy(c);
+  c = nullptr;
   if (hipSetDevice(sk::ctx_device(ctx)) != hipSuccess)
     return sk::ctx_fail(ctx, SK_ERR_HIP, "sk_comm_init: hipSetDevice");
+  // the status word first: a rank that fails here never joins the
+  // communicator (its peers then wait in ncclCommInitRank, as for any rank
+  // that never calls sk_comm_init); once joined, sk_gram_sharded allocates
+  // nothing before its first collective
+  sk::CommState* st = new sk::CommState;
+  if (hipMalloc(&st->d_st, 2 * sizeof(int32_t)) != hipSuccess) {
+    st->d_st = nullptr;
+    sk::comm_destroy(st);
+    return sk::ctx_fail(ctx, SK_ERR_ALLOC, "sk_comm_init: status word");
+  }
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
-  ncclComm_t comm = nullptr;
-  const ncclResult_t r = ncclCommInitRank(&comm, world, u, rank);
-  if (r != ncclSuccess)
+  const ncclResult_t r = ncclCommInitRank(&st->nc, world, u, rank);
+  if (r != ncclSuccess) {
+    st->nc = nullptr;
+    sk::comm_destroy(st);
     return sk::ctx_fail(ctx, SK_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-  c = comm;
+  }
+  c = st;
   return SK_OK;
 }
 
 int sk_comm_allgather(sk_context* ctx, const double* send_dev, int64_t count, double* recv_dev) {
   if (!ctx || count < 0 || (count > 0 && (!send_dev || !recv_dev)))
     return sk::ctx_fail(ctx, SK_ERR_INVALID, "sk_comm_allgather: bad argument");
-  void* c = sk::ctx_comm(ctx);
+  sk::CommState* c = comm_of(ctx);
   if (!c) return sk::ctx_fail(ctx, SK_ERR_INVALID, "sk_comm_allgather: no communicator (sk_comm_init)");
-  const ncclResult_t r = ncclAllGather(send_dev, recv_dev, (size_t)count, ncclDouble,
-                                       static_cast<ncclComm_t>(c), sk::ctx_stream(ctx));
+  const ncclResult_t r = ncclAllGather(send_dev, recv_dev, (size_t)count, ncclDouble, c->nc,
+                                       sk::ctx_stream(ctx));
   if (r != ncclSuccess)
     return sk::ctx_fail(ctx, SK_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
   return SK_OK;
@@ -192,10 +218,11 @@ int sk_comm_allgather(sk_context* ctx, const double* send_dev, int64_t count, do
 // the ranks' status codes, so every rank returns an error instead of its
 // peers waiting in ncclAllGather forever.
 namespace {
-int agree_status(sk_context* ctx, int32_t* d_st, int rc) {
+int agree_status(sk_context* ctx, int rc) {
   hipStream_t S = sk::ctx_stream(ctx);
   int32_t h[2] = {-rc, 0};
-  ncclComm_t c = static_cast<ncclComm_t>(sk::ctx_comm(ctx));
+  ncclComm_t c = comm_of(ctx)->nc;
+  int32_t* d_st = comm_of(ctx)->d_st;
   if (hipMemcpyAsync(d_st, h, sizeof(int32_t), hipMemcpyHostToDevice, S) != hipSuccess ||
       ncclAllReduce(d_st, d_st + 1, 1, ncclInt32, ncclMax, c, S) != ncclSuccess ||
       hipMemcpyAsync(h + 1, d_st + 1, sizeof(int32_t), hipMemcpyDeviceToHost, S) != hipSuccess ||
@@ -211,11 +238,10 @@ int agree_status(sk_context* ctx, int32_t* d_st, int rc) {
 int sk_gram_sharded(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp, int normalize,
                     double* out) {
   if (!ctx || !ds || !kp || !out) return sk::ctx_fail(ctx, SK_ERR_INVALID, "null argument");
-  void* c = sk::ctx_comm(ctx);
+  sk::CommState* c = comm_of(ctx);
   if (!c) return sk::ctx_fail(ctx, SK_ERR_INVALID, "sk_gram_sharded: no communicator (sk_comm_init)");
   int world = 0, rank = 0;
-  if (ncclCommCount(static_cast<ncclComm_t>(c), &world) != ncclSuccess ||
-      ncclCommUserRank(static_cast<ncclComm_t>(c), &rank) != ncclSuccess)
+  if (ncclCommCount(c->nc, &world) != ncclSuccess || ncclCommUserRank(c->nc, &rank) != ncclSuccess)
     return sk::ctx_fail(ctx, SK_ERR_HIP, "sk_gram_sharded: communicator query");
   const int32_t n = sk_dataset_size(ds);
   if (n < 0) return sk::ctx_fail(ctx, SK_ERR_INVALID, "sk_gram_sharded: dataset");
@@ -225,20 +251,12 @@ int sk_gram_sharded(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp,
   int rc = sk_shard_cells(n, rank, world, x.data(), y.data());
   if (rc) return sk::ctx_fail(ctx, rc, "sk_gram_sharded: plan");
   hipStream_t S = sk::ctx_stream(ctx);
-  int32_t* d_st = nullptr;
-  if (hipMalloc(&d_st, 2 * sizeof(int32_t)) != hipSuccess) {
-    // cannot take part in the status agreement: abort the communicator so
-    // the peers' collectives fail instead of waiting
-    (void)ncclCommAbort(static_cast<ncclComm_t>(c));
-    sk::ctx_comm(ctx) = nullptr;
-    return sk::ctx_fail(ctx, SK_ERR_ALLOC, "sk_gram_sharded: status word (communicator aborted)");
-  }
   double* d = nullptr;
   if (hipMalloc(&d, (size_t)per * (world + 1) * sizeof(double)) != hipSuccess) {
     d = nullptr;
     rc = sk::ctx_fail(ctx, SK_ERR_ALLOC, "sk_gram_sharded: device buffers");
   }
-  rc = agree_status(ctx, d_st, rc);  // all ranks have their buffers (or all stop)
+  rc = agree_status(ctx, rc);  // all ranks have their buffers (or all stop)
   std::vector<double> g;
   if (rc == SK_OK) {
     double* d_mine = d;
@@ -250,7 +268,7 @@ int sk_gram_sharded(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp,
     if (lrc != SK_OK) (void)hipMemsetAsync(d_mine, 0, (size_t)per * sizeof(double), S);
     // the all-gather runs on every rank, failed or not
     const int grc = sk_comm_allgather(ctx, d_mine, per, d_all);
-    rc = agree_status(ctx, d_st, lrc != SK_OK ? lrc : grc);
+    rc = agree_status(ctx, lrc != SK_OK ? lrc : grc);
     if (rc == SK_OK) {
       g.resize((size_t)per * world);
       if (hipMemcpyAsync(g.data(), d_all, g.size() * sizeof(double), hipMemcpyDeviceToHost, S) !=
@@ -261,7 +279,6 @@ int sk_gram_sharded(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp,
   }
   (void)hipStreamSynchronize(S);
   if (d) (void)hipFree(d);
-  (void)hipFree(d_st);
   if (rc) return rc;
   return sk_shard_assemble(n, world, g.data(), per, normalize, out);
 }

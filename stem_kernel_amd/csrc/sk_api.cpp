@@ -1600,7 +1600,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     L.kbound_stride = kb_stride;
     // one k tile: each plane's stacking chain produced one span early by the
     // plane that streams its G0 rows (stem4d.hip sk_stem4d_pre_kernel)
-    static const bool no_pre = std::getenv("SK4_NO_PRE") != nullptr;
+    const bool no_pre = std::getenv("SK4_NO_PRE") != nullptr;  // per call (A/B tests)
     L.gsum = gsum ? (!ktiles && !no_pre ? 2 : 1) : 0;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     if (ali_phmm) {

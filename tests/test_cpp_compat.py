@@ -39,7 +39,10 @@ def test_compat_app_matches_engine(gpu_ctx, tmp_path, normalize):
     import stem_kernel_amd as ska
     exe = _build(tmp_path)
     train = ska.random_sequences(6, 80, 0x5EED0001)
-    test = ska.random_sequences(3, 75, 0x5EED0011)
+    # 12 test rows against one train set: the engine's dataset cache holds 8
+    # sets, so the predict loop's single-row sets evict while the train set
+    # is in use (a shared handle keeps it alive)
+    test = ska.random_sequences(12, 75, 0x5EED0011)
     _write_fa(tmp_path / "train.fa", train)
     _write_fa(tmp_path / "test.fa", test)
     out = subprocess.run([exe, str(tmp_path / "train.fa"), str(tmp_path / "test.fa"),
