@@ -173,6 +173,15 @@ def dag_bytes(shapes, x, y):
     return float(np.sum(32.0 * V[x] * V[y] + S[x] + S[y] + 8.0))
 
 
+def col_waves(lens, y):
+    """Waves per pair of the 4-D column kernel, as run_stem4d picks them for a
+    batch: the class's register budget (CPL 1-2: 16, 4: 12, 8: 8), at most
+    m - 2 (the smallest y of the batch; one batch per bench step)."""
+    m = lens[y]
+    cpl = 1 if m.max() + 1 <= 64 else 2 if m.max() + 1 <= 128 else 4 if m.max() + 1 <= 256 else 8
+    return int(max(1, min({1: 16, 2: 16, 4: 12, 8: 8}[cpl], int(m.min()) - 2)))
+
+
 def stem4d_cells(lens, x, y):
     n, m = lens[x].astype(np.float64), lens[y].astype(np.float64)
     return float(np.sum((n + 1) * (n + 2) / 2 * (m + 1) * (m + 2) / 2))
@@ -189,6 +198,15 @@ def algorithmic(kind, shapes, x, y):
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
                 72.0 * stem4d_cells(lens, x, y)
+        if not (os.environ.get("SK4_NO_PRE") or os.environ.get("SK4_NO_COL")) and int(lens[y].max()) + 1 <= 512:
+            # column-pipelined full_dp (stem4d.hip sk_stem4d_col_kernel): G0 of
+            # (i,j-1) read and G0 of (i,j) written (16 B); every W-th plane's
+            # pre-combined G1 crosses the round wrap through HBM (+16 B)
+            W = col_waves(lens, y)
+            return "hbm", "GB/s", PEAK_HBM_GBS, \
+                f"16 B per (i,j,k,l) cell (G0 of (i,j-1) read, G0 of (i,j) written) + 16 B per cell of " \
+                f"every W-th plane (W = {W}: the pre-combined G1 across the round wrap), " \
+                "[n(n+1)/2][m(m+1)/2] cells", (16.0 + 16.0 / W) * stem4d_cells(lens, x, y)
         if os.environ.get("SK4_NO_PRE") or int(lens[y].max()) + 1 > 512:
             # full_dp with the K chain summed (stem4d.hip): G0, G1 written once
             # (16 B), G0 of (i,j-1), G1 of (i+1,j) and the stacking G0 of
@@ -671,7 +689,8 @@ def main():
                           int(np.sum(launches)), cells, a.pmc_json)
             rf["kernel"] = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
                             "stem4d": "sk_stem4d_kernel" if os.environ.get("SK4_NO_GSUM") else
-                            "sk_stem4d_gsum_kernel" if os.environ.get("SK4_NO_PRE") else "sk_stem4d_pre_kernel",
+                            "sk_stem4d_gsum_kernel" if os.environ.get("SK4_NO_PRE") else
+                            "sk_stem4d_pre_kernel" if os.environ.get("SK4_NO_COL") else "sk_stem4d_col_kernel",
                             "bpla": "sk_bpla_fast_kernel"}[kind]
         cpu, parity = None, None
         if not a.no_cpu_baseline and world == 1 and not a.cpu_stub:  # rank 0 at N=1 only

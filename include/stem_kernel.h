@@ -394,7 +394,8 @@ int sk_last_launch_ms(const sk_context *ctx, double *ms_sum, int32_t *n_launches
  * big-y kernel ran (y examples over 2,048 non-leaf nodes or with a stem edge
  * gap over 1,023, which the register classes cannot hold); *stem4d_mask has
  * bit log2(CPL) set for every 4-D stem class run (CPL = 1, 2, 4, 8 cells per
- * lane), shifted by 4 for the banded (partial_dp) variant. */
+ * lane), shifted by 4 for the banded (partial_dp) variant and by 8 for the
+ * column-pipelined full_dp kernel. */
 int sk_last_classes(const sk_context *ctx, uint32_t *stem_maxk_mask, uint32_t *stem4d_mask);
 /* RIBOSUM85-60 tables as compiled into the library (pinning tests). */
 void sk_ribosum_tables(float *s16, float *p256);

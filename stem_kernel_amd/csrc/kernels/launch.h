@@ -237,6 +237,14 @@ struct Stem4dLaunch {
 
 int stem4d_cpl(int m);
 hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st);
+// full_dp, column-pipelined (stem4d.hip sk_stem4d_col_kernel): one workgroup
+// of `waves` waves per pair (pairs[0..n_pairs)); per pair n planes of
+// plane_doubles (G0) and one B' plane at scratch_off; |y| < 512, and
+// m + 1 >= waves + 3
+size_t stem4d_col_lds_bytes(int cpl, int waves);
+int stem4d_col_max_waves(int cpl);
+hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves,
+                             hipStream_t st);
 
 // PairHMM alignment constraints of a 4-D batch (-a, stem_kernel.cpp:14-81):
 // one wavefront per pair writes c_low/c_high (n+1 each at pair.band_off).

@@ -758,6 +758,302 @@ __global__ void __launch_bounds__(256) sk_stem4d_pre_kernel(Stem4dLaunch P) {
   }
 }
 
+// full_dp, column-pipelined (r04): one WORKGROUP per pair walks the x
+// columns j = 1..n, and in column j the planes i = j-1, j-2, ..., 0, which
+// its W waves take in turn, each wave one row (y span d2) behind the previous.
+// Plane (i, j) needs G0(i, j-1) (the previous column's plane i, HBM) and its
+// pre-combined G1, B'(i, j) = G1(i+1, j) g + G2_(i,j), which the wave of plane
+// (i+1, j) forms from ITS A input -- G0(i+1, j-1), the stacking sources of
+// (i, j) -- one step earlier (the scheme of sk_stem4d_pre_kernel).  Here B'
+// goes from wave w to wave w+1 through an LDS double buffer instead of HBM,
+// so a cell costs the G0 read of (i, j-1) and the G0 write of (i, j) (in
+// place: plane slot i holds G0(i, j) of the latest column): 16 B, plus 16 B
+// for every W-th plane, whose B' crosses the round wrap (wave W-1 -> wave 0,
+// R - W + 1 steps later) through one plane-sized HBM buffer per pair.
+//
+// Schedule: positions p = 0, 1, ... run column by column; column j holds its
+// j planes (i = j-1 at offset 0) and then bubbles up to c_j = max(j, PF + 1)
+// positions, PF = 2 rows fetched ahead.  Position p is wave p % W's plane of
+// round p / W, and wave w processes row s of it at step T(p) + s, T(p) =
+// (p / W) R + p % W, R = m + 1 rows; one workgroup barrier per step.  Since
+// R >= W + PF + 1 (the host's choice of W), T is increasing with
+// T(p2) - T(p1) >= p2 - p1, so:
+//  * B' of row s is written by wave w-1 at step t-1 and read by wave w at
+//    step t (LDS slot t & 1), or, at the wrap, at least PF + 1 steps later;
+//  * the A row s + PF that a plane prefetches at step T(p) + s was written
+//    (by the previous column's plane i, >= PF + 2 positions earlier) at a
+//    step before that;
+//  * row 0 is never stored: G0(i, j, l, l) = g^(j-i) (the repeated products
+//    of gap_powers, as the chain G0(i+1,j,l,l) g forms it, :313-317).
+// The K chain is summed (sk_stem4d_gsum_kernel): every lane keeps one running
+// sum of its consumers' stacking sources over all its planes; the pair's
+// K = 1 + the waves' lane-reduced sums in wave order.
+constexpr int SK4C_PF = 2;
+
+__device__ __forceinline__ int s4c_cols(int j) { return j > SK4C_PF + 1 ? j : SK4C_PF + 1; }
+
+// position -> plane of the column schedule; advance() moves on by W positions
+struct S4cPos {
+  int j = 1, off = 0;  // column, offset in the column (i = j - 1 - off; off >= j: bubble)
+  __device__ void advance(int W, int n) {
+    off += W;
+    while (j <= n && off >= s4c_cols(j)) {
+      off -= s4c_cols(j);
+      ++j;
+    }
+  }
+  __device__ bool valid(int n) const { return j <= n; }
+  __device__ bool plane(int n) const { return j <= n && off < j; }
+  __device__ int i() const { return j - 1 - off; }
+};
+
+// waves per workgroup at most: 4, 3 and 2 per SIMD (the register budget)
+template <int CPL>
+constexpr int s4c_max_waves() {
+  return CPL <= 2 ? 16 : CPL == 4 ? 12 : 8;
+}
+
+template <int CPL>
+__global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kernel(Stem4dLaunch P) {
+  extern __shared__ __attribute__((aligned(16))) double s4c_lds[];
+  constexpr int TW = 64 * CPL;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int W = blockDim.x >> 6;
+  const Stem4dPair pr = P.pairs[blockIdx.x];
+  const int n = pr.n, m = pr.m, R = m + 1;
+  const int64_t cp = pr.plane_doubles;
+  double* __restrict__ planes = P.scratch + pr.scratch_off;  // slot i: G0(i, latest j)
+  double* __restrict__ wrapb = planes + (int64_t)n * cp;     // B' across the round wrap
+  const float* bpx = P.bpdiag + pr.x_bp;
+  const float* bpy = P.bpdiag + pr.y_bp;
+  const uint8_t* xs = P.chars + pr.x_chr;
+  const uint8_t* ys = P.chars + pr.y_chr;
+  const double* gpow = P.gpow;
+  const float bound = P.bp_bound;
+  const double g = P.gap, stk = P.stack, sub = P.subst;
+  // links: wave w writes link w (slot t & 1), wave w+1 reads it a step later
+  double* link_out = s4c_lds + (int64_t)w * 2 * TW;
+  const double* link_in = s4c_lds + (int64_t)(w - 1) * 2 * TW;
+  double* red = s4c_lds + (int64_t)W * 2 * TW;  // W per-wave sums
+
+  // steps: T(last position) + R
+  int64_t np = 0;
+  for (int j = 1; j <= n; ++j) np += s4c_cols(j);
+  const int64_t total = np > 0 ? ((np - 1) / W) * R + (np - 1) % W + R : 0;
+
+  // per-plane constants of the plane at a position
+  struct Plane {
+    int i, j;
+    bool on, first, cons, stack;
+    float bp_c;
+    uint8_t xci, xcj;
+  };
+  auto describe = [&](const S4cPos& q) __attribute__((always_inline)) -> Plane {
+    Plane d;
+    d.on = q.plane(n);
+    d.i = d.on ? q.i() : 0;
+    d.j = d.on ? q.j : 1;
+    d.first = d.i == d.j - 1;
+    d.cons = d.on && d.i >= 1;
+    d.bp_c = 0.0f;
+    d.xci = d.xcj = 0;
+    if (d.cons) {  // the consumer (i-1, j): bp(i-1, j-1) (:320)
+      const int e = d.j - d.i;
+      d.bp_c = bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (d.i - 1)];
+      d.xci = xs[d.i - 1];
+      d.xcj = xs[d.j - 1];
+    }
+    d.stack = d.cons && d.bp_c > bound;
+    return d;
+  };
+  // one row's HBM inputs, fetched PF rows ahead: G0(i, j-1) (A), the wrap
+  // B' (wave 0 of a non-first plane), prob_y(k, l-1), y[l-1]
+  struct Row {
+    double A[CPL], Bw[CPL];
+    float bp[CPL];
+    uint8_t yl[CPL];
+  };
+  auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
+    const int kmax = m - s;
+    const int ro = row_off(m, s);
+    const int e2 = s - 1;
+    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+    const double* Ai = planes + (int64_t)d.i * cp + ro;
+    const bool wrap_in = w == 0 && !d.first;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int k = lane + 64 * c;
+      r.A[c] = 0.0;
+      r.Bw[c] = 0.0;
+      r.bp[c] = 0.0f;
+      r.yl[c] = 0;
+      if (d.on && s >= 1 && k <= kmax) {
+        r.A[c] = d.first ? gpow[s] : Ai[k];  // G0(j-1, j-1) = g^(l-k)
+        if (wrap_in) r.Bw[c] = wrapb[ro + k];
+        if (d.stack) {
+          r.bp[c] = bpy[ye + k];
+          r.yl[c] = ys[k + s - 1];
+        }
+      }
+    }
+  };
+
+  uint8_t yk[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int k = lane + 64 * c;
+    yk[c] = k < m ? ys[k] : 0;
+  }
+  double ksrc = 0.0;
+  double Am1[CPL], Am2[CPL], G2c[CPL], G3c[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) Am1[c] = Am2[c] = G2c[c] = G3c[c] = 0.0;
+
+  // this wave's position (p = w) and the fetch cursor PF rows ahead
+  S4cPos cur;
+  cur.advance(w, n);  // from position 0
+  Plane dc = describe(cur);
+  S4cPos fpos = cur;
+  Plane df = dc;
+  int fs = 0;  // fetch cursor: (fpos, fs)
+  Row r0, r1;
+  auto fetch_next = [&](Row& r) __attribute__((always_inline)) {
+    fetch(r, df, fs);
+    if (++fs == R) {
+      fs = 0;
+      fpos.advance(W, n);
+      df = describe(fpos);
+    }
+  };
+  // a wave's first rows are fetched PF steps before its first step (t = w),
+  // not earlier: their A rows may be written in the steps before
+  if (w == 0) fetch_next(r0);
+  if (w <= 1) fetch_next(w == 0 ? r1 : r0);
+  int s = 0;
+
+  for (int64_t t = 0; t < total; ++t) {
+    if (t > 0) __syncthreads();
+    if (!cur.valid(n)) continue;  // (every wave takes every barrier)
+    if (t < w) {
+      if (t == w - 2) fetch_next(r0);
+      if (t == w - 1) fetch_next(r1);
+      continue;
+    }
+    const Row cr = r0;
+    r0 = r1;
+    fetch_next(r1);
+    if (dc.on) {
+      const int kmax = m - s;
+      if (s == 0) {  // cells (l, l): G0 = g^(j-i), never stored; chain registers reset
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const int k = lane + 64 * c;
+          Am1[c] = (dc.stack && k <= m) ? gpow[dc.j - 1 - dc.i] : 0.0;  // G0(i, j-1, l, l)
+          Am2[c] = G2c[c] = G3c[c] = 0.0;
+        }
+      } else {
+        const int ro = row_off(m, s);
+        double* __restrict__ out = planes + (int64_t)dc.i * cp + ro;
+        const bool wrap_in = w == 0;
+        const double* lin = link_in + ((t - 1) & 1) * TW;
+        double* lout = dc.cons && w + 1 < W ? link_out + (t & 1) * TW : nullptr;
+        // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at (k+1, l-1)
+        double G3n[CPL], A2[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const double hg = c + 1 < CPL ? bcast_lane0(G3c[c + 1 < CPL ? c + 1 : c]) : 0.0;
+          const double ha = c + 1 < CPL ? bcast_lane0(Am2[c + 1 < CPL ? c + 1 : c]) : 0.0;
+          G3n[c] = wave_shl1(G3c[c], hg);
+          A2[c] = wave_shl1(Am2[c], ha);
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const int k = lane + 64 * c;
+          if (k <= kmax) {
+            // this plane: G1 = B' (formed by the plane (i+1, j)), G0 (:85-111)
+            const double G1 = dc.first ? 0.0 : wrap_in ? cr.Bw[c] : lin[k];
+            double G0 = cr.A[c] * g;
+            G0 += G1;
+            out[k] = G0;
+            if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
+              double g3 = G3n[c] * g;
+              if (dc.stack && s >= 2) {
+                const float bp_kl = cr.bp[c];
+                if (bp_kl > bound) {
+                  const double g0 = A2[c];
+                  if (dc.xci == yk[c] && dc.xcj == cr.yl[c]) {
+                    ksrc += g0 * stk * (double)dc.bp_c * (double)bp_kl;
+                    g3 += g0;
+                  } else {
+                    ksrc += g0 * stk * sub * (double)dc.bp_c * (double)bp_kl;
+                  }
+                }
+              }
+              double g2 = G2c[c] * g;
+              g2 += g3;
+              double Bn = G1 * g;
+              Bn += g2;
+              if (lout) lout[k] = Bn;
+              else wrapb[ro + k] = Bn;
+              G2c[c] = g2;
+              G3c[c] = g3;
+            }
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          Am2[c] = Am1[c];
+          Am1[c] = cr.A[c];
+        }
+      }
+    }
+    if (++s == R) {
+      s = 0;
+      cur.advance(W, n);
+      dc = describe(cur);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) ksrc += __shfl_xor(ksrc, off, 64);
+  if (lane == 0) red[w] = ksrc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double K = 0.0;
+    for (int v = 0; v < W; ++v) K += red[v];
+    P.out[pr.out_index] = 1.0 + K;
+  }
+}
+
+int stem4d_col_max_waves(int cpl) {
+  return cpl <= 2 ? s4c_max_waves<2>() : cpl == 4 ? s4c_max_waves<4>() : s4c_max_waves<8>();
+}
+
+size_t stem4d_col_lds_bytes(int cpl, int waves) {
+  return ((size_t)waves * 2 * 64 * cpl + waves) * sizeof(double);
+}
+
+hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves,
+                             hipStream_t st) {
+  if (n_pairs == 0) return hipSuccess;
+  const size_t lds = stem4d_col_lds_bytes(cpl, waves);
+  const dim3 grid((unsigned)n_pairs), block(64 * waves);
+#define SK_L(C)                                                                                   \
+  {                                                                                               \
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(sk_stem4d_col_kernel<C>),    \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);     \
+    if (e != hipSuccess) return e;                                                                \
+    hipLaunchKernelGGL((sk_stem4d_col_kernel<C>), grid, block, lds, st, P);                       \
+  }
+  switch (cpl) {
+    case 1: SK_L(1) break;
+    case 2: SK_L(2) break;
+    case 4: SK_L(4) break;
+    default: SK_L(8) break;
+  }
+#undef SK_L
+  return hipGetLastError();
+}
+
 int stem4d_cpl(int m) {
   if (m + 1 <= 64) return 1;
   if (m + 1 <= 128) return 2;

@@ -1430,7 +1430,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     chall.insert(chall.end(), chr.begin(), chr.end());
     return SK_OK;
   };
-  int max_m = 0;
+  int max_m = 0, max_n = 0;
   double cells = 0.0;
   for (int64_t k = 0; k < n; ++k) {
     int rc = touch(xs_->ex[x[k]], tx[x[k]]);
@@ -1439,6 +1439,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     if (rc) return rc;
     const double a = xs_->ex[x[k]].len, b = ys_->ex[y[k]].len;
     max_m = std::max(max_m, (int)b);
+    max_n = std::max(max_n, (int)a);
     cells += (a + 1) * (a + 2) / 2 * (b + 1) * (b + 2) / 2;
   }
   ctx->last_cells = cells;
@@ -1451,7 +1452,9 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
     return xs_->ex[x[a]].len > xs_->ex[x[b]].len;
   });
-  const std::vector<double> gp = gap_powers(kp->gap, max_m + 2);
+  // g^k for y spans (d1 = 0 planes) and, in the column kernel, x spans (the
+  // diagonal cells G0(i, j, l, l) = g^(j-i))
+  const std::vector<double> gp = gap_powers(kp->gap, std::max(max_m, max_n) + 2);
   // device-side tables for the whole call
   const size_t nb_bp = std::max<size_t>(bpall.size(), 1), nb_ch = std::max<size_t>(chall.size(), 1);
   size_t need = nb_bp * 4 + nb_ch + gp.size() * 8 + 4096;
@@ -1476,6 +1479,10 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   const bool banded = ali_phmm || (!ali && kp->len_band > 0);
   const bool gsum = !banded && !std::getenv("SK4_NO_GSUM");
   const size_t nst = gsum ? 2 : 4;
+  // full_dp with one k tile: the column-pipelined kernel (one workgroup per
+  // pair, B' handed on through LDS; stem4d.hip sk_stem4d_col_kernel) unless
+  // SK4_NO_COL / SK4_NO_PRE (A/B: the span kernels)
+  const bool colk = gsum && !ktiles && !std::getenv("SK4_NO_COL") && !std::getenv("SK4_NO_PRE");
   double total_ms = 0.0;
   int launches = 0;
   Stem4dBatch& Bt = ctx->s4d;
@@ -1492,8 +1499,11 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       p.n = xs_->ex[x[q]].len;
       p.m = ys_->ex[y[q]].len;
       p.plane_doubles = stem4d_plane_doubles(p.m);
-      const size_t rb = ((size_t)3 * (p.n + 1) * nst * (size_t)p.plane_doubles * 8 +
-                         (gsum ? (size_t)(p.n + 1) * 8 : 0) + 255) & ~(size_t)255;
+      // column kernel: n G0 planes (slot i) + the round wrap's B' plane;
+      // span kernels: a ring of three spans of n + 1 planes (+ acc)
+      const size_t rb = colk ? ((size_t)(p.n + 1) * (size_t)p.plane_doubles * 8 + 255) & ~(size_t)255
+                             : ((size_t)3 * (p.n + 1) * nst * (size_t)p.plane_doubles * 8 +
+                                (gsum ? (size_t)(p.n + 1) * 8 : 0) + 255) & ~(size_t)255;
       const double pb = (double)rb + (double)(p.n + 1) * (double)kb_stride * 8.0;
       if (!prs.empty() && bytes + pb > budget) break;
       p.scratch_off = (int64_t)(ring_bytes / 8);
@@ -1507,6 +1517,51 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       maxn = std::max(maxn, p.n);
       prs.push_back(p);
       ++b1;
+    }
+    if (colk) {
+      // one launch for the batch: W waves per pair, W <= m - 2 for every pair
+      // (the schedule's R >= W + PF + 1) and the class's register budget
+      int min_m = INT32_MAX;
+      for (const auto& p : prs) min_m = std::min(min_m, p.m);
+      const int W = std::max(1, std::min(sk::stem4d_col_max_waves(cpl), min_m - 2));
+      rc = ensure_scratch(ctx, ring_bytes + 64);
+      if (rc) return rc;
+      if (Bt.cap_pairs < prs.size()) {
+        if (Bt.pairs) {
+          SK_HIP(ctx, hipStreamSynchronize(S));
+          (void)hipFree(Bt.pairs);
+        }
+        Bt.cap_pairs = std::max<size_t>(prs.size(), 64);
+        SK_HIP(ctx, hipMalloc(&Bt.pairs, Bt.cap_pairs * sizeof(sk::Stem4dPair)));
+      }
+      SK_HIP(ctx, hipMemcpyAsync(Bt.pairs, prs.data(), prs.size() * sizeof(sk::Stem4dPair),
+                                 hipMemcpyHostToDevice, S));
+      sk::Stem4dLaunch L;
+      L.pairs = Bt.pairs;
+      L.scratch = ctx->scratch;
+      L.bpdiag = d_bp;
+      L.chars = d_ch;
+      L.gpow = d_gp;
+      L.gap = kp->gap;
+      L.stack = kp->stack;
+      L.subst = kp->subst;
+      L.bp_bound = (float)kp->bp_bound;
+      L.out = out_dev;
+      L.gsum = 3;
+      SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
+      SK_HIP(ctx, sk::lev_mark(ctx, S));
+      SK_HIP(ctx, sk::launch_stem4d_col(L, (int64_t)prs.size(), cpl, W, S));
+      SK_HIP(ctx, sk::lev_mark(ctx, S));
+      ctx->last_s4d_classes |= 1u << ((cpl == 1 ? 0 : cpl == 2 ? 1 : cpl == 4 ? 2 : 3) + 8);
+      ++launches;
+      SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
+      SK_HIP(ctx, hipStreamSynchronize(S));
+      SK_HIP(ctx, sk::lev_collect(ctx));
+      float ms = 0.f;
+      SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+      total_ms += ms;
+      b0 = b1;
+      continue;
     }
     // partial_dp constraints per pair: x position -> [c_low, c_high].  With
     // -a the PairHMM kernel writes them on the device; with -b alone

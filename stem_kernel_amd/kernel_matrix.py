@@ -594,12 +594,14 @@ class Context:
     def last_classes(self):
         """Kernel instantiations the last compute call launched: the DAG stem
         register classes (MAXK values; 0 = the big-y kernel, dag_stem_big.hip)
-        and the 4-D classes as (CPL, banded)."""
+        and the 4-D classes as (CPL, banded); `stem4d_col` lists the CPLs that
+        ran the column-pipelined full_dp kernel (also in `stem4d`, unbanded)."""
         a, b = C.c_uint32(), C.c_uint32()
         self._chk(lib().sk_last_classes(self._h, C.byref(a), C.byref(b)))
         maxk = sorted(4 * k for k in range(32) if a.value >> k & 1)
-        s4d = sorted((1 << (k & 3), bool(k & 4)) for k in range(8) if b.value >> k & 1)
-        return dict(stem_maxk=maxk, stem4d=s4d)
+        s4d = sorted({(1 << (k & 3), bool(k & 4)) for k in range(12) if b.value >> k & 1})
+        col = sorted(1 << (k & 3) for k in range(8, 12) if b.value >> k & 1)
+        return dict(stem_maxk=maxk, stem4d=s4d, stem4d_col=col)
 
 
 def format_libsvm(matrix: np.ndarray, labels: Sequence[str]) -> str:
