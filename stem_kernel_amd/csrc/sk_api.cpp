@@ -43,8 +43,8 @@ struct DeviceBuffers {
   }
 };
 
-template <class T>
-hipError_t upload(DeviceBuffers& db, const std::vector<T>& v, const T** out) {
+template <class V, class T = typename V::value_type>
+hipError_t upload(DeviceBuffers& db, const V& v, const T** out) {
   void* p = nullptr;
   const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
   hipError_t e = hipMalloc(&p, bytes);
@@ -68,6 +68,30 @@ float4 bpla_weight(const Example& X, int i) {
 }
 
 // Packed host image of a dataset (device_set.h layout).
+// vectors whose resize() leaves new elements uninitialised (trivial types):
+// the packed arrays are sized once and filled on host threads, which then
+// also take the page faults, instead of one thread zero-filling them first
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using pvec = std::vector<T, NoInitAlloc<T>>;
+
 struct HostPack {
   std::vector<int32_t> ex_nl, ex_node_base, ex_edge_base, ex_bpf_base, ex_lvl_base, ex_nlev,
       ex_len, ex_pos_base, ex_has_w;
@@ -81,39 +105,42 @@ struct HostPack {
   // records); they go to sk_dag_stem_big_kernel (level-order arrays)
   std::vector<uint8_t> ex_big;
   std::vector<float> ex_nseqs;
-  std::vector<uint32_t> nd_a, nd_b, nd_c;
-  std::vector<float> nd_w, nd_nbp;
-  std::vector<double> nd_P;
-  std::vector<uint2> ed;
-  std::vector<uint32_t> bpf_code;
-  std::vector<float> bpf_p;
-  std::vector<int32_t> lvl;
-  std::vector<float4> pos_prof;
-  std::vector<float> pos_w;
-  std::vector<uint8_t> pos_chr;
-  std::vector<float4> pos_lru;
+  pvec<uint32_t> nd_a, nd_b, nd_c;
+  pvec<float> nd_w, nd_nbp;
+  pvec<double> nd_P;
+  pvec<uint2> ed;
+  pvec<uint32_t> bpf_code;
+  pvec<float> bpf_p;
+  pvec<int32_t> lvl;
+  pvec<float4> pos_prof;
+  pvec<float> pos_w;
+  pvec<uint8_t> pos_chr;
+  pvec<float4> pos_lru;
   std::vector<int32_t> ex_nslots, ex_xch_base;
-  std::vector<sk::XRow> xrow;
-  std::vector<uint32_t> yn_a, yn_b, yn_c, ye2, ysc;
-  std::vector<uint4> yrec;
-  std::vector<float> yn_w, yn_nbp, yn_p0;
-  std::vector<double> yn_P;
-  std::vector<int32_t> ycs, ex_ysc_base, ex_nch, ex_ycs_base;
-  std::vector<uint32_t> xr_node, xr_ch;
+  pvec<sk::XRow> xrow;
+  pvec<uint32_t> yn_a, yn_b, yn_c, ye2, ysc;
+  pvec<uint4> yrec;
+  pvec<float> yn_w, yn_nbp, yn_p0;
+  pvec<double> yn_P;
+  pvec<int32_t> ycs;
+  std::vector<int32_t> ex_ysc_base, ex_nch, ex_ycs_base;
+  pvec<uint32_t> xr_node, xr_ch;
   // gamma schedule (device_set.h): the x rows without the gamma rows, the
   // gamma rows' K inputs, the dataset's gamma keys and the y gapless flags
-  std::vector<sk::XRow> xgrow;
-  std::vector<uint32_t> xg_node, xg_ch, xg_clg, gr_info, gam_key;
-  std::vector<float> xg_cpf, gr_pf;
-  std::vector<double> gr_P;
+  pvec<sk::XRow> xgrow;
+  std::vector<uint32_t> gam_key;
+  pvec<uint32_t> xg_node, xg_ch, xg_clg, gr_info;
+  pvec<float> xg_cpf, gr_pf;
+  pvec<double> gr_P;
   std::vector<int32_t> ex_xg_base, ex_nlxg, ex_xgch_base, ex_gr_base, ex_gapless;
   // phi rows (combination rows of the gamma schedule): per child record its
   // weight recipe, the rows' Gamma_{code,len} K inputs, each example's phi
   // components (phi key per type-2 record, in record order), the phi keys
-  std::vector<uint8_t> xg_cty;
-  std::vector<uint32_t> gra_gidx, gra_row, phk_idx, phi_al, phi_g;
+  pvec<uint8_t> xg_cty;
+  std::vector<uint32_t> phi_al, phi_g;
+  pvec<uint32_t> gra_gidx, gra_row, phk_idx;
   std::vector<int32_t> ex_gra_base, ex_phk_base;
-  std::vector<uint64_t> ex_phi_bits;  // per example, the phi keys it uses (bitset)
+  pvec<uint64_t> ex_phi_bits;  // per example, the phi keys it uses (bitset)
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
   int32_t max_nch = 0;
 };
@@ -320,6 +347,9 @@ static void assign_sweep_lanes(const std::vector<int>& take, const std::vector<u
 // --------------------------------------------------------------- packing
 int pack_dataset(sk_dataset* ds, std::string& err) {
   HostPack& P = ds->pack;
+  const bool tstats = std::getenv("SK_HOST_STATS") != nullptr;
+  auto tnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double tp0 = tnow();
   // SK_SWEEP_LANES=0: sweep chunks in schedule order (A/B diagnostics)
   const char* lanes_env = std::getenv("SK_SWEEP_LANES");
   const bool sweep_lanes_greedy = !lanes_env || std::atoi(lanes_env) != 0;
@@ -353,15 +383,41 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     return !is_gamma(X, v);
   };
   std::vector<uint64_t> phi_raw;  // child gamma key:32 | code:16 | len:16 (sorted: by child key)
-  for (int e = 0; e < n; ++e) {
-    const Example& X = ds->ex[e];
-    for (int v = 0; v < X.n_nodes(); ++v) {
-      if (is_gamma(X, v)) P.gam_key.push_back(gamma_key(X, v));
-      if (is_phi(X, v)) {
-        P.gam_key.push_back(gamma_key(X, v));
-        for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k)
-          phi_raw.push_back(((uint64_t)gamma_key(X, X.edge_to[k]) << 32) | gamma_key(X, v));
+  const int nthr = (int)std::max<size_t>(1, std::min<size_t>({(size_t)n / 8 + 1, (size_t)16,
+                                                              (size_t)std::max(1u, std::thread::hardware_concurrency())}));
+  {  // every example's keys (host threads, one slice each), then one sorted set
+    std::vector<std::vector<uint32_t>> tk(nthr);
+    std::vector<std::vector<uint64_t>> tp(nthr);
+    auto keys = [&](int t) {
+      for (int e = (int)((int64_t)n * t / nthr); e < (int)((int64_t)n * (t + 1) / nthr); ++e) {
+        const Example& X = ds->ex[e];
+        for (int v = 0; v < X.n_nodes(); ++v) {
+          if (is_gamma(X, v)) tk[t].push_back(gamma_key(X, v));
+          if (is_phi(X, v)) {
+            tk[t].push_back(gamma_key(X, v));
+            for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k)
+              tp[t].push_back(((uint64_t)gamma_key(X, X.edge_to[k]) << 32) | gamma_key(X, v));
+          }
+        }
+        auto& k1 = tk[t];  // keep each slice's lists short
+        if (k1.size() > 4096) {
+          std::sort(k1.begin(), k1.end());
+          k1.erase(std::unique(k1.begin(), k1.end()), k1.end());
+        }
+        auto& p1 = tp[t];
+        if (p1.size() > 4096) {
+          std::sort(p1.begin(), p1.end());
+          p1.erase(std::unique(p1.begin(), p1.end()), p1.end());
+        }
       }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthr; ++t) th.emplace_back(keys, t);
+    keys(0);
+    for (auto& t : th) t.join();
+    for (int t = 0; t < nthr; ++t) {
+      P.gam_key.insert(P.gam_key.end(), tk[t].begin(), tk[t].end());
+      phi_raw.insert(phi_raw.end(), tp[t].begin(), tp[t].end());
     }
   }
   std::sort(P.gam_key.begin(), P.gam_key.end());
@@ -539,12 +595,28 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     }
 
   };
-  P.ex_node_base.push_back(0);
-  P.ex_edge_base.push_back(0);
-  P.ex_bpf_base.push_back(0);
-  P.ex_lvl_base.push_back(0);
-  P.ex_pos_base.push_back(0);
-  for (int e = 0; e < n; ++e) {
+  // x-role records of one example (nodes in level order, the x schedules,
+  // per-position tables), formed per example on host threads and appended
+  // in example order below (bit-identical to one serial pass; example-local
+  // offsets, the dataset's bases added when appending)
+  struct XOut {
+    std::vector<uint32_t> nd_a, nd_b, nd_c, xr_ch, xr_node, gr_info, xg_ch, xg_clg, phk_idx, gra_gidx,
+        gra_row, xg_node;
+    std::vector<float> nd_w, nd_nbp, bpf_p, gr_pf, xg_cpf, ex_nseqs, pos_w;
+    std::vector<double> nd_P, gr_P;
+    std::vector<uint2> ed;
+    std::vector<uint32_t> bpf_code;
+    std::vector<int32_t> lvl, ex_nslots, ex_nlxg, ex_gapless, ex_nl, ex_nlev, ex_len, ex_has_w;
+    std::vector<uint8_t> ex_big, xg_cty, pos_chr, ex_dyadic, ex_str_fast, ex_onehot;
+    std::vector<sk::XRow> xrow, xgrow;
+    std::vector<float4> pos_prof, pos_lru;
+    std::vector<uint64_t> ex_phi_bits;
+    int nl = 0, nlev = 0, max_slots = 0, n_nostore = 0, n_nodes = 0, gslots = 0;
+    bool big = false;
+    int rc = SK_OK;
+    std::string err;
+  };
+  auto pack_x = [&](int e, XOut& O) {
     const Example& X = ds->ex[e];
     const int nn = X.n_nodes();
     // level of every node (children first in reference numbering)
@@ -561,8 +633,9 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         else lv = std::max(lv, c + 1);
       }
       if (any_leaf && e1 - e0 != 1) {
-        err = "unexpected DAG shape: stem with a leaf child";
-        return SK_ERR_INVALID;
+        O.err = "unexpected DAG shape: stem with a leaf child";
+        O.rc = SK_ERR_INVALID;
+        return;
       }
       level[v] = lv;
       nlev = std::max(nlev, lv + 1);
@@ -574,8 +647,9 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
                      [&](int a, int b) { return level[a] < level[b]; });
     const int nl = (int)order.size();
     if (nl >= 0xffff) {
-      err = "example too large: more than 65534 non-leaf DAG nodes";
-      return SK_ERR_UNSUPPORTED;
+      O.err = "example too large: more than 65534 non-leaf DAG nodes";
+      O.rc = SK_ERR_UNSUPPORTED;
+      return;
     }
     std::vector<int> nid(nn, -1);
     for (int k = 0; k < nl; ++k) nid[order[k]] = k;
@@ -585,53 +659,55 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     for (int v = nn - 1; v >= 0; --v)
       for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) Pw[X.edge_to[k]] += Pw[v];
 
-    const int ebase = (int)P.ed.size(), bbase = (int)P.bpf_code.size();
+
     bool big_gap = false;
     for (int k = 0; k < nl; ++k) {
       const int v = order[k];
       const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
       const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
       const bool loop = level[v] == 0;  // single leaf child
-      const uint32_t eloc = (uint32_t)P.ed.size() - ebase, bloc = (uint32_t)P.bpf_code.size() - bbase;
+      const uint32_t eloc = (uint32_t)O.ed.size(), bloc = (uint32_t)O.bpf_code.size();
       const uint32_t ne = loop ? 0u : e1 - e0;
       if (eloc > 0xffff || bloc > 0xffff || ne > 0xff || b1 - b0 > 0xff ||
           X.last[v] - X.first[v] > 0xffff) {
-        err = "example too large for the 16-bit packed DAG layout";
-        return SK_ERR_UNSUPPORTED;
+        O.err = "example too large for the 16-bit packed DAG layout";
+        O.rc = SK_ERR_UNSUPPORTED;
+        return;
       }
-      P.nd_a.push_back(eloc | (ne << 16) | ((b1 - b0) << 24));
-      P.nd_b.push_back((X.last[v] - X.first[v]) | (bloc << 16));
-      P.nd_c.push_back(loop ? X.edge_gaps[e0] : 0u);
-      P.nd_w.push_back(X.weight[v]);
-      P.nd_nbp.push_back(X.prof5[(size_t)X.first[v] * 5 + 4]);
-      P.nd_P.push_back(Pw[v]);
+      O.nd_a.push_back(eloc | (ne << 16) | ((b1 - b0) << 24));
+      O.nd_b.push_back((X.last[v] - X.first[v]) | (bloc << 16));
+      O.nd_c.push_back(loop ? X.edge_gaps[e0] : 0u);
+      O.nd_w.push_back(X.weight[v]);
+      O.nd_nbp.push_back(X.prof5[(size_t)X.first[v] * 5 + 4]);
+      O.nd_P.push_back(Pw[v]);
       if (!loop) {
         for (uint32_t t = e0; t < e1; ++t) {
           const int c = nid[X.edge_to[t]];
           if (c < 0 || X.edge_gaps[t] > 0xffff) {
-            err = c < 0 ? "unexpected DAG shape: stem with a leaf child" : "gap count exceeds 65535";
-            return c < 0 ? SK_ERR_INVALID : SK_ERR_UNSUPPORTED;
+            O.err = c < 0 ? "unexpected DAG shape: stem with a leaf child" : "gap count exceeds 65535";
+            O.rc = c < 0 ? SK_ERR_INVALID : SK_ERR_UNSUPPORTED;
+            return;
           }
           big_gap |= X.edge_gaps[t] > 1023;
-          P.ed.push_back(make_uint2((uint32_t)c | (X.edge_gaps[t] << 16), (uint32_t)k));
+          O.ed.push_back(make_uint2((uint32_t)c | (X.edge_gaps[t] << 16), (uint32_t)k));
         }
       }
       for (uint32_t t = b0; t < b1; ++t) {
-        P.bpf_code.push_back(X.bpf_code[t]);
-        P.bpf_p.push_back(X.bpf_p[t]);
+        O.bpf_code.push_back(X.bpf_code[t]);
+        O.bpf_p.push_back(X.bpf_p[t]);
       }
     }
     std::vector<int32_t> lv(nlev + 1, 0);
     for (int k = 0; k < nl; ++k) lv[level[order[k]] + 1]++;
     for (int l = 0; l < nlev; ++l) lv[l + 1] += lv[l];
-    P.lvl.insert(P.lvl.end(), lv.begin(), lv.end());
+    O.lvl.insert(O.lvl.end(), lv.begin(), lv.end());
     // the register-class kernel's y records: child:11 | parent:11 | gaps:10
     const bool big = nl > 2048 || big_gap;
-    P.ex_big.push_back(big ? 1 : 0);
+    O.ex_big.push_back(big ? 1 : 0);
 
-    // (the y-role records are formed after this loop, per example in
-    // parallel: pack_y below)
-    yjobs.push_back(YJob{P.ex_node_base.back(), ebase, bbase, nl, big});
+    // (the y-role records are formed after the x-role pass: pack_y below)
+    O.nl = nl;
+    O.big = big;
 
     // x-role schedule: rows in reference (post-)order; a row's HBM slot is
     // recycled once its last parent has been produced (LIFO free list keeps
@@ -644,7 +720,6 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       std::vector<uint32_t> slot(nn, 0xffff);
       std::vector<int> free_list;
       int nslots = 0;
-      P.ex_xch_base.push_back((int32_t)P.xr_ch.size());
       for (int v = 0; v < nn; ++v) {
         if (level[v] < 0) continue;
         const bool loop = level[v] == 0;
@@ -654,7 +729,7 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         if (!loop) {
           for (uint32_t k = e0; k < e1; ++k) {
             const int c = X.edge_to[k];
-            P.xr_ch.push_back(slot[c] | (X.edge_gaps[k] << 16));
+            O.xr_ch.push_back(slot[c] | (X.edge_gaps[k] << 16));
             ++nch;
           }
         }
@@ -680,26 +755,21 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         xr.bp0 = b1 > b0 ? X.bpf_p[b0] : 0.0f;
         xr.P = Pw[v];
         // bpf_beg in the level-order bpf array of this example (see nd_b)
-        xr.c = (P.nd_b[P.ex_node_base.back() + nid[v]] >> 16) |
-               ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16);
-        P.xrow.push_back(xr);
-        P.xr_node.push_back((uint32_t)nid[v]);
+        xr.c = (O.nd_b[nid[v]] >> 16) | ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16);
+        O.xrow.push_back(xr);
+        O.xr_node.push_back((uint32_t)nid[v]);
       }
       if (nslots >= 0xffff) {
-        err = "too many live DAG rows";
-        return SK_ERR_UNSUPPORTED;
+        O.err = "too many live DAG rows";
+        O.rc = SK_ERR_UNSUPPORTED;
+        return;
       }
-      P.ex_nslots.push_back(nslots);
-      P.max_slots = std::max(P.max_slots, nslots);
+      O.ex_nslots.push_back(nslots);
+      O.max_slots = std::max(O.max_slots, nslots);
 
       // the gamma schedule: the same post-order without the gamma rows
       // (slots only among the remaining rows; a gamma child is a record
       // 0x8000 | gamma index, its weight factors g^lg pf in xg_clg / xg_cpf)
-      P.ex_xg_base.push_back((int32_t)P.xgrow.size());
-      P.ex_xgch_base.push_back((int32_t)P.xg_ch.size());
-      P.ex_gr_base.push_back((int32_t)P.gr_info.size());
-      P.ex_gra_base.push_back((int32_t)P.gra_gidx.size());
-      P.ex_phk_base.push_back((int32_t)P.phk_idx.size());
       std::vector<uint32_t> gslot(nn, 0xffff);
       std::vector<int> gfree;
       int gslots = 0, nlxg = 0;
@@ -825,9 +895,9 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
         const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
         if (gam_on && is_gamma(X, v)) {
-          P.gr_info.push_back(gamma_idx(gamma_key(X, v)) | (X.edge_gaps[e0] << 16));
-          P.gr_pf.push_back(X.bpf_p[b0]);
-          P.gr_P.push_back(Pw[v]);
+          O.gr_info.push_back(gamma_idx(gamma_key(X, v)) | (X.edge_gaps[e0] << 16));
+          O.gr_pf.push_back(X.bpf_p[b0]);
+          O.gr_P.push_back(Pw[v]);
           continue;
         }
         const bool loop = level[v] == 0;
@@ -842,33 +912,33 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
             const uint32_t kc = gamma_key(X, c);
             const uint32_t pi = phi_idx(kp, kc);
             for (int ty : {2, 4}) {
-              P.xg_ch.push_back(((ty == 2 ? 0x4000u | pi : 0x8000u | gamma_idx(kc))) | (X.edge_gaps[k] << 16));
-              P.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
-              P.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
-              P.xg_cty.push_back((uint8_t)ty);
+              O.xg_ch.push_back(((ty == 2 ? 0x4000u | pi : 0x8000u | gamma_idx(kc))) | (X.edge_gaps[k] << 16));
+              O.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
+              O.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
+              O.xg_cty.push_back((uint8_t)ty);
             }
-            P.phk_idx.push_back(pi);
+            O.phk_idx.push_back(pi);
           }
-          P.xg_ch.push_back(0x8000u | gamma_idx(kp));
-          P.xg_clg.push_back(0u);
-          P.xg_cpf.push_back(0.0f);
-          P.xg_cty.push_back(3);
-          P.gra_gidx.push_back(gamma_idx(kp));
-          P.gra_row.push_back((uint32_t)P.xgrow.size());
+          O.xg_ch.push_back(0x8000u | gamma_idx(kp));
+          O.xg_clg.push_back(0u);
+          O.xg_cpf.push_back(0.0f);
+          O.xg_cty.push_back(3);
+          O.gra_gidx.push_back(gamma_idx(kp));
+          O.gra_row.push_back((uint32_t)O.xgrow.size());  // (+ the example's xgrow base)
           nch = 2 * (e1 - e0) + 1;
         } else if (!loop) {
           for (uint32_t k = e0; k < e1; ++k) {
             const int c = X.edge_to[k];
             if (gam_on && is_gamma(X, c)) {
-              P.xg_ch.push_back((0x8000u | gamma_idx(gamma_key(X, c))) | (X.edge_gaps[k] << 16));
-              P.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
-              P.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
-              P.xg_cty.push_back(1);
+              O.xg_ch.push_back((0x8000u | gamma_idx(gamma_key(X, c))) | (X.edge_gaps[k] << 16));
+              O.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
+              O.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
+              O.xg_cty.push_back(1);
             } else {
-              P.xg_ch.push_back(gslot[c] | (X.edge_gaps[k] << 16));
-              P.xg_clg.push_back(0u);
-              P.xg_cpf.push_back(1.0f);
-              P.xg_cty.push_back(0);
+              O.xg_ch.push_back(gslot[c] | (X.edge_gaps[k] << 16));
+              O.xg_clg.push_back(0u);
+              O.xg_cpf.push_back(1.0f);
+              O.xg_cty.push_back(0);
             }
             ++nch;
           }
@@ -899,74 +969,48 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         xr.nbp = X.prof5[(size_t)X.first[v] * 5 + 4];
         xr.bp0 = b1 > b0 ? X.bpf_p[b0] : 0.0f;
         xr.P = Pw[v];
-        xr.c = (P.nd_b[P.ex_node_base.back() + nid[v]] >> 16) |
-               ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16) | (phi ? 0x80000000u : 0u);
-        P.xgrow.push_back(xr);
-        P.xg_node.push_back((uint32_t)nid[v]);
+        xr.c = (O.nd_b[nid[v]] >> 16) | ((b1 > b0 ? (uint32_t)X.bpf_code[b0] : 0u) << 16) |
+               (phi ? 0x80000000u : 0u);
+        O.xgrow.push_back(xr);
+        O.xg_node.push_back((uint32_t)nid[v]);
         ++nlxg;
       }
       if (phi_on) {  // this example's phi keys as a bitset (items take unions)
         const size_t W = (P.phi_al.size() + 63) / 64;
-        const size_t base = P.ex_phi_bits.size();
-        P.ex_phi_bits.resize(base + W, 0ull);
-        for (size_t j = (size_t)P.ex_phk_base.back(); j < P.phk_idx.size(); ++j)
-          P.ex_phi_bits[base + P.phk_idx[j] / 64] |= 1ull << (P.phk_idx[j] % 64);
-      }
-      if (std::getenv("SK_PACK_STATS")) {  // diagnostic: rows, unstored rows, slots
-        static long s_rows = 0, s_nost = 0, s_slots = 0, s_nodes = 0, s_st = 0, s_slab = 0, s_gam = 0,
-                    s_phi = 0, s_reg = 0;
-        s_rows += nlxg;
-        s_nodes += nn;
-        for (int v = 0; v < nn; ++v) s_nost += nostore[v];
-        s_slots += gslots;
-        // row reads the kernel issues: slab / Gamma / Phi child records, minus
-        // the previous row (taken from registers); stored rows
-        {
-          uint32_t prev = 0xffffu;
-          size_t k = (size_t)P.ex_xgch_base.back();
-          for (size_t r = (size_t)P.ex_xg_base.back(); r < P.xgrow.size(); ++r) {
-            const int ne = P.xgrow[r].a & 0xff;
-            for (int t = 0; t < ne; ++t, ++k) {
-              const uint32_t c = P.xg_ch[k] & 0xffffu;
-              if (c == prev) ++s_reg;
-              else if (c & 0x8000u) ++s_gam;
-              else if (c & 0x4000u) ++s_phi;
-              else ++s_slab;
-            }
-            prev = P.xgrow[r].b >> 16;
-            s_st += prev < 0x4000u;
-          }
-        }
-        if (e + 1 == n)
-          fprintf(stderr,
-                  "[sk pack] gamma schedule: %ld nodes, %ld rows, %ld unstored, %ld slots; stored %ld, reads: "
-                  "slab %ld gamma %ld phi %ld, from registers %ld\n",
-                  s_nodes, s_rows, s_nost, s_slots, s_st, s_slab, s_gam, s_phi, s_reg);
+        O.ex_phi_bits.assign(W, 0ull);
+        for (size_t j = 0; j < O.phk_idx.size(); ++j)
+          O.ex_phi_bits[O.phk_idx[j] / 64] |= 1ull << (O.phk_idx[j] % 64);
       }
       if (gslots >= 0x4000) {  // slot ids share the record with the gamma / phi flags
-        err = "too many live DAG rows";
-        return SK_ERR_UNSUPPORTED;
+        O.err = "too many live DAG rows";
+        O.rc = SK_ERR_UNSUPPORTED;
+        return;
       }
-      P.ex_nlxg.push_back(nlxg);
-      P.max_slots = std::max(P.max_slots, gslots);
+      O.ex_nlxg.push_back(nlxg);
+      O.max_slots = std::max(O.max_slots, gslots);
+      O.n_nostore = 0;
+      for (int v = 0; v < nn; ++v) O.n_nostore += nostore[v];
+      O.n_nodes = nn;
+      O.gslots = gslots;
     }
     {  // y role: no gap column in any non-leaf node (the Gamma rows need it)
       bool gl = true;
-      for (int k = 0; k < nl; ++k) gl &= P.nd_nbp[P.ex_node_base.back() + k] == 0.0f;
-      P.ex_gapless.push_back(gl ? 1 : 0);
+      for (int k = 0; k < nl; ++k) gl &= O.nd_nbp[k] == 0.0f;
+      O.ex_gapless.push_back(gl ? 1 : 0);
     }
-    P.ex_nl.push_back(nl);
-    P.ex_nlev.push_back(nlev);
-    P.ex_nseqs.push_back(X.n_seqs);
-    P.ex_len.push_back(X.len);
-    P.ex_has_w.push_back(X.has_bp ? 1 : 0);
+    O.ex_nl.push_back(nl);
+    O.ex_nlev.push_back(nlev);
+    O.nlev = nlev;
+    O.ex_nseqs.push_back(X.n_seqs);
+    O.ex_len.push_back(X.len);
+    O.ex_has_w.push_back(X.has_bp ? 1 : 0);
     for (int i = 0; i < X.len; ++i) {
       const float* c = &X.prof5[(size_t)i * 5];
-      P.pos_prof.push_back(make_float4(c[0], c[1], c[2], c[3]));
-      P.pos_w.push_back(X.has_bp ? X.pos_weight[i] : 1.0f);
-      P.pos_chr.push_back((uint8_t)X.rows[0][i]);
+      O.pos_prof.push_back(make_float4(c[0], c[1], c[2], c[3]));
+      O.pos_w.push_back(X.has_bp ? X.pos_weight[i] : 1.0f);
+      O.pos_chr.push_back((uint8_t)X.rows[0][i]);
     }
-    for (int i = 0; i < X.len; ++i) P.pos_lru.push_back(bpla_weight(X, i));
+    for (int i = 0; i < X.len; ++i) O.pos_lru.push_back(bpla_weight(X, i));
     {
       bool dy = true;  // the device's dyadic_sum test (bpla.hip), in host float
       for (int i = 0; i < X.len; ++i)
@@ -974,13 +1018,13 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
           const float v = X.prof5[(size_t)i * 5 + k] * 256.0f;
           dy = dy && v == std::rint(v);
         }
-      P.ex_dyadic.push_back(dy ? 1 : 0);
+      O.ex_dyadic.push_back(dy ? 1 : 0);
       bool full = true;
       for (int i = 0; i < X.len; ++i) {
         const float* c = &X.prof5[(size_t)i * 5];
         full = full && (c[0] + c[1] + c[2] + c[3]) > 0.0f;
       }
-      P.ex_str_fast.push_back(dy && full ? 1 : 0);
+      O.ex_str_fast.push_back(dy && full ? 1 : 0);
       bool oh = true;  // the device's onehot_code test (profile_string.hip)
       for (int i = 0; i < X.len && oh; ++i) {
         const float* c = &X.prof5[(size_t)i * 5];
@@ -991,19 +1035,130 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
         }
         oh = ones == 1 && zeros == 3;
       }
-      P.ex_onehot.push_back(oh ? 1 : 0);
+      O.ex_onehot.push_back(oh ? 1 : 0);
     }
-    P.ex_node_base.push_back((int32_t)P.nd_a.size());
-    P.ex_edge_base.push_back((int32_t)P.ed.size());
-    P.ex_bpf_base.push_back((int32_t)P.bpf_code.size());
-    P.ex_lvl_base.push_back((int32_t)P.lvl.size());
-    P.ex_pos_base.push_back((int32_t)P.pos_prof.size());
-    P.max_nl = std::max(P.max_nl, nl);
-    P.max_edges = std::max(P.max_edges, (int)P.ed.size() - ebase);
-    P.max_bpf = std::max(P.max_bpf, (int)P.bpf_code.size() - bbase);
-    P.max_nlev = std::max(P.max_nlev, nlev);
-    P.max_len = std::max(P.max_len, X.len);
+  };
+  const double tp1 = tnow();
+  double tpx = tp1;
+  {
+    std::vector<XOut> xo(n);
+    std::atomic<int> next{0};
+    auto work = [&]() {
+      for (int e = next.fetch_add(1); e < n; e = next.fetch_add(1)) pack_x(e, xo[e]);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthr; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    tpx = tnow();
+    P.ex_node_base.push_back(0);
+    P.ex_edge_base.push_back(0);
+    P.ex_bpf_base.push_back(0);
+    P.ex_lvl_base.push_back(0);
+    P.ex_pos_base.push_back(0);
+    // per-example arrays at their prefix-sum offsets, copied on the threads
+#define SK_BIG(X) X(nd_a) X(nd_b) X(nd_c) X(nd_w) X(nd_nbp) X(nd_P) X(ed) X(bpf_code) X(bpf_p) X(lvl) \
+  X(xr_ch) X(xrow) X(xr_node) X(gr_info) X(gr_pf) X(gr_P) X(xg_ch) X(xg_clg) X(xg_cpf) X(xg_cty)    \
+  X(phk_idx) X(gra_gidx) X(gra_row) X(xgrow) X(xg_node) X(pos_prof) X(pos_w) X(pos_chr) X(pos_lru)  \
+  X(ex_phi_bits)
+#define SK_OFF(f) std::vector<size_t> off_##f(n + 1, 0);
+    SK_BIG(SK_OFF)
+#undef SK_OFF
+    auto app = [](auto& dst, const auto& src) { dst.insert(dst.end(), src.begin(), src.end()); };
+    std::vector<long> st_nodes(n), st_nost(n), st_slots(n);  // (SK_PACK_STATS)
+    for (int e = 0; e < n; ++e) {
+      XOut& O = xo[e];
+      st_nodes[e] = O.n_nodes;
+      st_nost[e] = O.n_nostore;
+      st_slots[e] = O.gslots;
+      if (O.rc) {  // the first failing example, as the serial pass would report it
+        err = O.err;
+        return O.rc;
+      }
+#define SK_ACC(f) off_##f[e + 1] = off_##f[e] + O.f.size();
+      SK_BIG(SK_ACC)
+#undef SK_ACC
+      yjobs.push_back(YJob{(int)off_nd_a[e], (int)off_ed[e], (int)off_bpf_code[e], O.nl, O.big});
+      P.ex_xch_base.push_back((int32_t)off_xr_ch[e]);
+      P.ex_xg_base.push_back((int32_t)off_xgrow[e]);
+      P.ex_xgch_base.push_back((int32_t)off_xg_ch[e]);
+      P.ex_gr_base.push_back((int32_t)off_gr_info[e]);
+      P.ex_gra_base.push_back((int32_t)off_gra_gidx[e]);
+      P.ex_phk_base.push_back((int32_t)off_phk_idx[e]);
+      app(P.ex_big, O.ex_big); app(P.ex_nslots, O.ex_nslots); app(P.ex_nlxg, O.ex_nlxg);
+      app(P.ex_gapless, O.ex_gapless); app(P.ex_nl, O.ex_nl); app(P.ex_nlev, O.ex_nlev);
+      app(P.ex_nseqs, O.ex_nseqs); app(P.ex_len, O.ex_len); app(P.ex_has_w, O.ex_has_w);
+      app(P.ex_dyadic, O.ex_dyadic); app(P.ex_str_fast, O.ex_str_fast); app(P.ex_onehot, O.ex_onehot);
+      P.max_slots = std::max(P.max_slots, O.max_slots);
+      P.ex_node_base.push_back((int32_t)off_nd_a[e + 1]);
+      P.ex_edge_base.push_back((int32_t)off_ed[e + 1]);
+      P.ex_bpf_base.push_back((int32_t)off_bpf_code[e + 1]);
+      P.ex_lvl_base.push_back((int32_t)off_lvl[e + 1]);
+      P.ex_pos_base.push_back((int32_t)off_pos_prof[e + 1]);
+      P.max_nl = std::max(P.max_nl, O.nl);
+      P.max_edges = std::max(P.max_edges, (int)O.ed.size());
+      P.max_bpf = std::max(P.max_bpf, (int)O.bpf_code.size());
+      P.max_nlev = std::max(P.max_nlev, O.nlev);
+      P.max_len = std::max(P.max_len, ds->ex[e].len);
+    }
+    const double tq1 = tnow();
+#define SK_SIZE(f) P.f.resize(off_##f[n]);
+    SK_BIG(SK_SIZE)
+#undef SK_SIZE
+    const double tq2 = tnow();
+    {
+      std::atomic<int> nx{0};
+      auto copy = [&]() {
+        for (int e = nx.fetch_add(1); e < n; e = nx.fetch_add(1)) {
+          XOut& O = xo[e];
+          for (uint32_t& r : O.gra_row) r += (uint32_t)off_xgrow[e];  // example-local -> dataset row
+#define SK_CPY(f) std::copy(O.f.begin(), O.f.end(), P.f.begin() + off_##f[e]);
+          SK_BIG(SK_CPY)
+#undef SK_CPY
+          O = XOut();  // free as we go
+        }
+      };
+      std::vector<std::thread> tc;
+      for (int t = 1; t < nthr; ++t) tc.emplace_back(copy);
+      copy();
+      for (auto& t : tc) t.join();
+    }
+    if (tstats) fprintf(stderr, "[sk pack] offsets %.1f ms, resize %.1f ms, copy %.1f ms\n", tq1 - tpx, tq2 - tq1, tnow() - tq2);
+#undef SK_BIG
+    if (tstats) fprintf(stderr, "[sk pack] keys %.1f ms, x-role %.1f ms (%d threads) + append %.1f ms\n",
+                        tp1 - tp0, tpx - tp1, nthr, tnow() - tpx);
+    if (std::getenv("SK_PACK_STATS")) {  // diagnostic: rows, unstored rows, slots
+      long s_rows = 0, s_nost = 0, s_slots = 0, s_nodes = 0, s_st = 0, s_slab = 0, s_gam = 0, s_phi = 0,
+           s_reg = 0;
+      for (int e = 0; e < n; ++e) {
+        s_rows += P.ex_nlxg[e];
+        s_nodes += st_nodes[e];
+        s_nost += st_nost[e];
+        s_slots += st_slots[e];
+        // row reads the kernel issues: slab / Gamma / Phi child records, minus
+        // the previous row (taken from registers); stored rows
+        uint32_t prev = 0xffffu;
+        size_t k = (size_t)P.ex_xgch_base[e];
+        for (size_t r = (size_t)P.ex_xg_base[e]; r < (size_t)P.ex_xg_base[e] + P.ex_nlxg[e]; ++r) {
+          const int ne = P.xgrow[r].a & 0xff;
+          for (int t = 0; t < ne; ++t, ++k) {
+            const uint32_t c = P.xg_ch[k] & 0xffffu;
+            if (c == prev) ++s_reg;
+            else if (c & 0x8000u) ++s_gam;
+            else if (c & 0x4000u) ++s_phi;
+            else ++s_slab;
+          }
+          prev = P.xgrow[r].b >> 16;
+          s_st += prev < 0x4000u;
+        }
+      }
+      fprintf(stderr,
+              "[sk pack] gamma schedule: %ld nodes, %ld rows, %ld unstored, %ld slots; stored %ld, reads: "
+              "slab %ld gamma %ld phi %ld, from registers %ld\n",
+              s_nodes, s_rows, s_nost, s_slots, s_st, s_slab, s_gam, s_phi, s_reg);
+    }
   }
+  const double tp2 = tnow();
   {
     std::vector<YOut> yo(yjobs.size());
     const int nthr = (int)std::max<size_t>(1, std::min<size_t>({yjobs.size() / 8 + 1, (size_t)16,
@@ -1016,29 +1171,47 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     for (int t = 1; t < nthr; ++t) th.emplace_back(work);
     work();
     for (auto& t : th) t.join();
-    for (size_t e = 0; e < yo.size(); ++e) {
+    const double ty1 = tnow();
+    // appended at prefix-sum offsets, copied on the threads (as the x role)
+    const size_t ny = yo.size();
+#define SK_YBIG(X) X(ysc) X(ycs) X(ye2) X(yn_a) X(yn_b) X(yn_c) X(yn_p0) X(yrec) X(yn_w) X(yn_nbp) X(yn_P)
+#define SK_OFF(f) std::vector<size_t> off_##f(ny + 1, 0);
+    SK_YBIG(SK_OFF)
+#undef SK_OFF
+    for (size_t e = 0; e < ny; ++e) {
       YOut& Y = yo[e];
       if (!Y.err.empty()) {
         err = Y.err;
         return SK_ERR_INVALID;
       }
-      P.ex_ysc_base.push_back((int32_t)(P.ysc.size() / 64));
-      P.ysc.insert(P.ysc.end(), Y.ysc.begin(), Y.ysc.end());
-      P.ex_ycs_base.push_back((int32_t)P.ycs.size());
-      P.ycs.insert(P.ycs.end(), Y.ycs.begin(), Y.ycs.end());
+#define SK_ACC(f) off_##f[e + 1] = off_##f[e] + Y.f.size();
+      SK_YBIG(SK_ACC)
+#undef SK_ACC
+      P.ex_ysc_base.push_back((int32_t)(off_ysc[e] / 64));
+      P.ex_ycs_base.push_back((int32_t)off_ycs[e]);
       P.ex_nch.push_back(Y.nch);
       P.max_nch = std::max(P.max_nch, Y.nch);
-      P.ye2.insert(P.ye2.end(), Y.ye2.begin(), Y.ye2.end());
-      P.yn_a.insert(P.yn_a.end(), Y.yn_a.begin(), Y.yn_a.end());
-      P.yn_b.insert(P.yn_b.end(), Y.yn_b.begin(), Y.yn_b.end());
-      P.yn_c.insert(P.yn_c.end(), Y.yn_c.begin(), Y.yn_c.end());
-      P.yn_p0.insert(P.yn_p0.end(), Y.yn_p0.begin(), Y.yn_p0.end());
-      P.yrec.insert(P.yrec.end(), Y.yrec.begin(), Y.yrec.end());
-      P.yn_w.insert(P.yn_w.end(), Y.yn_w.begin(), Y.yn_w.end());
-      P.yn_nbp.insert(P.yn_nbp.end(), Y.yn_nbp.begin(), Y.yn_nbp.end());
-      P.yn_P.insert(P.yn_P.end(), Y.yn_P.begin(), Y.yn_P.end());
-      YOut().ysc.swap(Y.ysc);  // free as we go
     }
+#define SK_SIZE(f) P.f.resize(off_##f[ny]);
+    SK_YBIG(SK_SIZE)
+#undef SK_SIZE
+    next = 0;
+    auto copy = [&]() {
+      for (size_t e = next.fetch_add(1); e < ny; e = next.fetch_add(1)) {
+        YOut& Y = yo[e];
+#define SK_CPY(f) std::copy(Y.f.begin(), Y.f.end(), P.f.begin() + off_##f[e]);
+        SK_YBIG(SK_CPY)
+#undef SK_CPY
+        Y = YOut();  // free as we go
+      }
+    };
+    th.clear();
+    for (int t = 1; t < nthr; ++t) th.emplace_back(copy);
+    copy();
+    for (auto& t : th) t.join();
+#undef SK_YBIG
+    if (tstats) fprintf(stderr, "[sk pack] y-role %.1f ms (%d threads) + append %.1f ms\n", ty1 - tp2, nthr,
+                        tnow() - ty1);
   }
   return SK_OK;
 }

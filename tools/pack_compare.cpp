@@ -6,7 +6,8 @@
 //   /tmp/pc_old 2048 200   (likewise with -DSRC=... the tree's sk_api.cpp)
 #include SRC
 #include <chrono>
-template <class T> static uint64_t hv(const std::vector<T>& v, uint64_t h) {
+template <class V> static uint64_t hv(const V& v, uint64_t h) {
+  typedef typename V::value_type T;
   const unsigned char* p = reinterpret_cast<const unsigned char*>(v.data());
   for (size_t i = 0; i < v.size() * sizeof(T); ++i) h = (h ^ p[i]) * 1099511628211ull;
   return h ^ v.size();
