@@ -371,11 +371,52 @@ def cpu_baseline(cfg, data, n_pairs, seed=7):
     dt = time.perf_counter() - t
     what = cfg.get("cls") or {"ss": "SuStemStrKernel", "stem": "SuStemKernel",
                               "stem4d": "4-D StemKernel full_dp", "bpla": "BPLAKernel"}[kind]
-    return {"value": n_pairs / dt, "unit": "sequence-pairs/sec", "cores": cores, "kind": "port",
+    value = n_pairs / dt
+    return {"value": value, "unit": "sequence-pairs/sec", "cores": cores, "kind": "port",
             "host_nproc": os.cpu_count(),
+            "cores_why": ("the job's CPU share: the GPU box caps each job at OMP_NUM_THREADS (16) of its "
+                          f"{os.cpu_count()} host threads, which other jobs share"),
+            "calibration": calibration(cfg, value, cores),
             "sample": f"{n_pairs} random pairs (i<=j) among {npool} of the {len(data)} examples, "
                       f"{what} via the C oracle on {cores} threads (all host cores this job "
                       f"may use: affinity capped by OMP_NUM_THREADS), {dt:.1f}s wall"}, pairs, vals, comp
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def calibration(cfg, value, cores):
+    """How the port relates to the reference's own CPU code
+    (profiles/r04_cpu_calibration.json, tools/cpu_calib.py): on one core of
+    the build container the port runs the L=200 DAG stem DP `port_over_reference`
+    times as fast as the reference's stem_kernel_lite/stem_kernel.cpp did in
+    the survey's probe (BASELINE.md, 57 ms per pair).  The GPU box's CPU is
+    another model, so only the port's rate is measured here; the reference's
+    rate on these cores is estimated as value / port_over_reference."""
+    path = os.path.join(ROOT, "profiles", "r04_cpu_calibration.json")
+    try:
+        with open(path) as f:
+            c = json.load(f)
+    except (OSError, ValueError):
+        return None
+    out = {"source": os.path.relpath(path, ROOT), "box_cpu_model": cpu_model(),
+           "container_cpu_model": c.get("cpu_model"),
+           "port_over_reference_in_container": c.get("port_over_reference"),
+           "port_pairs_per_s_per_thread_here": value / max(cores, 1)}
+    if cfg["kernel"] in ("ss", "stem") and cfg["L"] == 200 and c.get("port_over_reference"):
+        out["reference_equivalent_value"] = value / c["port_over_reference"]
+        out["box_over_container_per_core"] = (value / max(cores, 1)) / c["port_pairs_per_s_per_core"]
+        out["note"] = ("reference_equivalent_value assumes the port/reference ratio measured in the "
+                       "container holds on the box's CPU model, which is unverified")
+    return out
 
 
 # ------------------------------------------------------------------ ranks
