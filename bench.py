@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--length", type=int, default=None)
     ap.add_argument("--slices", type=int, default=None)
     ap.add_argument("--full", action="store_true", help="time every slice (whole Gram)")
+    ap.add_argument("--sync", action="store_true",
+                    help="synchronous compute calls (default: sk_set_async, step t+1 planned while step t runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-pairs", type=int, default=None, help="pairs in the CPU sample")
     ap.add_argument("--pmc-json", default=None, help="traffic profile (default profiles/<kind>_traffic.json)")
@@ -486,6 +488,10 @@ class GpuEngine:
         torch.cuda.synchronize(self.dev)
         self.t_upload = time.perf_counter() - t0
         self.kern = make_kernel(cfg["kernel"], cfg.get("cls"))
+        # asynchronous calls: the host plans step t+1 while the GPU runs step
+        # t; timings are collected over the timed steps (totals())
+        self.async_on = not a.sync
+        self.ctx.set_async(self.async_on)
         if self.dist_on:
             shard.rccl_init(self.ctx)
         else:
@@ -503,12 +509,18 @@ class GpuEngine:
 
     def step(self, x, y):
         self.ctx.pairs_device(self.ds, self.kern, x, y, self.out.data_ptr())
-        tm = dict(self.ctx.last_timing(), **self.ctx.last_launch_ms())
+        tm = None if self.async_on else dict(self.ctx.last_timing(), **self.ctx.last_launch_ms())
         self.ctx.allgather(self.out.data_ptr(), self.per, self.gathered.data_ptr())
         return tm
 
     def full(self):
         self.ctx.gram_sharded(self.ds, self.kern, normalize=False)
+        return None if self.async_on else dict(self.ctx.last_timing(), **self.ctx.last_launch_ms())
+
+    def totals(self):
+        """Summed timings of the calls since the last totals() (async mode;
+        after a sync)."""
+        self.ctx.sync_timing()
         return dict(self.ctx.last_timing(), **self.ctx.last_launch_ms())
 
     def sync(self):
@@ -692,23 +704,32 @@ def main():
     for w in range(a.warmup):
         run_step(w)
     eng.sync()
+    if getattr(eng, "async_on", False):
+        eng.totals()  # (the warmup's timings, dropped)
     eng.barrier()
     eng.sync()
     t0 = time.perf_counter()
     local_pairs = 0
     k_ms, work, cells, launches, l_ms = [], [], [], [], []
-    for k in range(a.steps):
-        x, y, tm = run_step(a.warmup + k)
-        local_pairs += x.size
+
+    def add(tm):
         k_ms.append(tm["stem_ms"])
         cells.append(tm["cells"])
         launches.append(tm["launches"])
         l_ms.append(tm["ms_sum"])
+    for k in range(a.steps):
+        x, y, tm = run_step(a.warmup + k)
+        local_pairs += x.size
+        if tm is not None:
+            add(tm)
         work.append((x, y))
     eng.sync()
     eng.barrier()
     eng.sync()
     elapsed = time.perf_counter() - t0
+    if getattr(eng, "async_on", False):  # every timed call's events, summed (outside the timed region)
+        add(eng.totals())
+        cells = [cells[0] / a.steps] * a.steps
     if eng.dist_on:
         elapsed, total_pairs = eng.reduce_max_sum(elapsed, local_pairs)
     else:

@@ -388,6 +388,17 @@ int sk_last_timing(const sk_context *ctx, double *stem_ms, double *string_ms,
  * duration a kernel-trace profiler reports.  Launches on several streams
  * overlap, so the sum can exceed sk_last_timing's span. */
 int sk_last_launch_ms(const sk_context *ctx, double *ms_sum, int32_t *n_launches);
+/* Asynchronous compute calls (default off).  With on != 0, sk_pairs_device
+ * (and every call that returns its results on the device) returns once its
+ * work is enqueued on the context's stream, so the host plans call t+1
+ * while the GPU runs call t; host inputs are staged through pinned buffers,
+ * so they may be freed when the call returns.  Results are ready after a
+ * stream synchronisation.  The timing queries above then report totals:
+ * sk_sync_timing waits for every call since the previous sk_sync_timing and
+ * makes their summed timings (spans, launches, cells) what sk_last_timing and
+ * sk_last_launch_ms return.  Turning async off resolves what is pending. */
+int sk_set_async(sk_context *ctx, int32_t on);
+int sk_sync_timing(sk_context *ctx);
 /* Kernel instantiations launched by the last compute call (parity-coverage
  * diagnostic): *stem_maxk_mask has bit MAXK/4 set for every DAG stem register
  * class run (MAXK = 4, 8, ..., 32 64-node slots per lane) and bit 0 when the

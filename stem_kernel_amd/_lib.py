@@ -90,6 +90,8 @@ SIGNATURES = {
     "sk_random_sequences": (C.c_int, [C.POINTER(C.c_uint64), C.c_int32, C.c_int32, C.c_char_p]),
     "sk_last_timing": (C.c_int, [_P, _F64P, _F64P, _F64P, _I32P]),
     "sk_last_launch_ms": (C.c_int, [_P, _F64P, _I32P]),
+    "sk_set_async": (C.c_int, [_P, C.c_int32]),
+    "sk_sync_timing": (C.c_int, [_P]),
     "sk_shard_count": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "sk_shard_cells": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, _I32P, _I32P]),
     "sk_shard_assemble": (C.c_int, [C.c_int32, C.c_int32, _F64P, C.c_int64, C.c_int, _F64P]),

@@ -195,10 +195,39 @@ struct sk_context {
   // a fourth stream: the 4-D kernel's span launches run in parts on all four
   hipStream_t aux = nullptr;
   hipEvent_t eva = nullptr;
-  // per-launch events of the dominant kernel (sk_last_launch_ms): a start and
-  // an end event around each launch on the launch's own stream
-  std::vector<hipEvent_t> lev;
-  size_t lev_used = 0;
+  // Timing of a compute call: its span events (ev0..ev3 are the current
+  // set's) and per-launch events of the dominant kernel (sk_last_launch_ms: a
+  // start and an end event around each launch on the launch's own stream).
+  // Synchronous calls use set 0 and are resolved before they return; with
+  // sk_set_async the sets rotate through a ring and a call returns once its
+  // work is enqueued: its set stays pending until sk_sync_timing, or until
+  // the ring comes round to it, and is then added to the acc_* totals.
+  struct TSet {
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    std::vector<hipEvent_t> lev;
+    size_t lev_used = 0;
+    bool pending = false, stem = false, str = false;
+    double cells = 0.0;
+    int32_t launches = 0;
+  };
+  static constexpr int kTSets = 4;
+  TSet tset[kTSets];
+  int tk = 0;
+  bool async = false;
+  double acc_stem_ms = 0.0, acc_str_ms = 0.0, acc_cells = 0.0, acc_launch_ms = 0.0;
+  int32_t acc_launch_n = 0, acc_launches = 0;
+  // pinned staging of an asynchronous call's host-to-device uploads (the
+  // host buffers die when the call returns; pageable copies would wait for
+  // the stream): one ring slot per call parity, reused once its copies are
+  // done (its event)
+  struct Stage {
+    std::vector<std::pair<char*, size_t>> blocks;
+    size_t blk = 0, off = 0;
+    hipEvent_t ev = nullptr;
+    bool recorded = false;
+  };
+  Stage stage[2];
+  uint64_t ncalls = 0;
   double last_launch_ms_sum = 0.0;
   int32_t last_launch_n = 0;
   double last_stem_ms = 0.0, last_str_ms = 0.0, last_cells = 0.0;
@@ -216,31 +245,142 @@ hipStream_t ctx_stream(sk_context* ctx) { return ctx->stream; }
 
 // start or end event of one dominant-kernel launch, on the launch's stream
 hipError_t lev_mark(sk_context* ctx, hipStream_t s) {
-  if (ctx->lev_used == ctx->lev.size()) {
+  sk_context::TSet& T = ctx->tset[ctx->tk];
+  if (T.lev_used == T.lev.size()) {
     hipEvent_t e = nullptr;
     const hipError_t r = hipEventCreate(&e);
     if (r != hipSuccess) return r;
-    ctx->lev.push_back(e);
+    T.lev.push_back(e);
   }
-  return hipEventRecord(ctx->lev[ctx->lev_used++], s);
+  return hipEventRecord(T.lev[T.lev_used++], s);
 }
 
 // after the launch streams are synchronized: adds the marked launches'
 // durations to the call's sum
 hipError_t lev_collect(sk_context* ctx) {
-  for (size_t i = 0; i + 1 < ctx->lev_used; i += 2) {
+  sk_context::TSet& T = ctx->tset[ctx->tk];
+  for (size_t i = 0; i + 1 < T.lev_used; i += 2) {
     float ms = 0.f;
-    const hipError_t r = hipEventElapsedTime(&ms, ctx->lev[i], ctx->lev[i + 1]);
+    const hipError_t r = hipEventElapsedTime(&ms, T.lev[i], T.lev[i + 1]);
     if (r != hipSuccess) return r;
     ctx->last_launch_ms_sum += ms;
     ++ctx->last_launch_n;
   }
-  ctx->lev_used = 0;
+  T.lev_used = 0;
   return hipSuccess;
 }
 
-void lev_reset(sk_context* ctx) {
-  ctx->lev_used = 0;
+// A pending asynchronous call's timing, into the acc_* totals (waits for it).
+hipError_t tset_resolve(sk_context* ctx, int k) {
+  sk_context::TSet& T = ctx->tset[k];
+  if (!T.pending) return hipSuccess;
+  T.pending = false;
+  float ms = 0.f;
+  hipError_t r;
+  if (T.stem) {
+    if ((r = hipEventSynchronize(T.ev[1])) != hipSuccess) return r;
+    if ((r = hipEventElapsedTime(&ms, T.ev[0], T.ev[1])) != hipSuccess) return r;
+    ctx->acc_stem_ms += ms;
+  }
+  if (T.str) {
+    if ((r = hipEventSynchronize(T.ev[3])) != hipSuccess) return r;
+    if ((r = hipEventElapsedTime(&ms, T.ev[2], T.ev[3])) != hipSuccess) return r;
+    ctx->acc_str_ms += ms;
+  }
+  for (size_t i = 0; i + 1 < T.lev_used; i += 2) {
+    if ((r = hipEventSynchronize(T.lev[i + 1])) != hipSuccess) return r;
+    if ((r = hipEventElapsedTime(&ms, T.lev[i], T.lev[i + 1])) != hipSuccess) return r;
+    ctx->acc_launch_ms += ms;
+    ++ctx->acc_launch_n;
+  }
+  T.lev_used = 0;
+  ctx->acc_cells += T.cells;
+  ctx->acc_launches += T.launches;
+  return hipSuccess;
+}
+
+// Start of a compute call: its timing set (and, async, its staging slot).
+hipError_t call_begin(sk_context* ctx) {
+  hipError_t r;
+  if (ctx->async) {
+    const int k = (ctx->tk + 1) % sk_context::kTSets;
+    if ((r = tset_resolve(ctx, k)) != hipSuccess) return r;  // the ring came round
+    ctx->tk = k;
+    sk_context::Stage& G = ctx->stage[ctx->ncalls++ & 1];
+    if (G.recorded && (r = hipEventSynchronize(G.ev)) != hipSuccess) return r;
+    G.recorded = false;
+    G.blk = G.off = 0;
+  } else {
+    ctx->tk = 0;
+  }
+  sk_context::TSet& T = ctx->tset[ctx->tk];
+  for (int i = 0; i < 4; ++i)
+    if (!T.ev[i] && (r = hipEventCreate(&T.ev[i])) != hipSuccess) return r;
+  T.lev_used = 0;
+  T.pending = false;
+  ctx->ev0 = T.ev[0];
+  ctx->ev1 = T.ev[1];
+  ctx->ev2 = T.ev[2];
+  ctx->ev3 = T.ev[3];
+  return hipSuccess;
+}
+
+// Host-to-device upload of a compute call: straight from the caller's memory
+// (synchronous calls), or through the call's pinned staging slot (async).
+hipError_t h2d(sk_context* ctx, void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if (!ctx->async) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+  sk_context::Stage& G = ctx->stage[(ctx->ncalls - 1) & 1];
+  const size_t need = (bytes + 255) & ~(size_t)255;
+  while (G.blk < G.blocks.size() && G.off + need > G.blocks[G.blk].second) {
+    ++G.blk;
+    G.off = 0;
+  }
+  if (G.blk == G.blocks.size()) {
+    const size_t cap = std::max(need, (size_t)8 << 20);
+    void* p = nullptr;
+    const hipError_t r = hipHostMalloc(&p, cap, hipHostMallocDefault);
+    if (r != hipSuccess) return r;
+    G.blocks.push_back({static_cast<char*>(p), cap});
+    G.off = 0;
+  }
+  char* p = G.blocks[G.blk].first + G.off;
+  G.off += need;
+  std::memcpy(p, src, bytes);
+  return hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s);
+}
+
+// End of a compute call whose span events (ev0/ev1: stem, ev2/ev3: string)
+// and launch events were recorded on streams joined into `s`: synchronous,
+// its timing becomes last_*; async, it stays pending.
+hipError_t call_finish(sk_context* ctx, hipStream_t s, bool stem, bool str) {
+  sk_context::TSet& T = ctx->tset[ctx->tk];
+  T.stem = stem;
+  T.str = str;
+  T.cells = ctx->last_cells;
+  T.launches = ctx->last_launches;
+  hipError_t r;
+  if (ctx->async) {
+    sk_context::Stage& G = ctx->stage[(ctx->ncalls - 1) & 1];
+    if ((r = hipEventRecord(G.ev, s)) != hipSuccess) return r;
+    G.recorded = true;
+    T.pending = true;
+    return hipSuccess;
+  }
+  if ((r = hipStreamSynchronize(s)) != hipSuccess) return r;
+  float ms = 0.f;
+  if (stem) {
+    if ((r = hipEventElapsedTime(&ms, T.ev[0], T.ev[1])) != hipSuccess) return r;
+    ctx->last_stem_ms = ms;
+  }
+  if (str) {
+    if ((r = hipEventElapsedTime(&ms, T.ev[2], T.ev[3])) != hipSuccess) return r;
+    ctx->last_str_ms = ms;
+  }
+  return lev_collect(ctx);
+}
+
+void lev_reset(sk_context* ctx) {  // (the call's launch events: call_begin)
   ctx->last_launch_ms_sum = 0.0;
   ctx->last_launch_n = 0;
 }
@@ -1410,13 +1550,12 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   sk::BplaPos* d_tab = ntab ? A.take<sk::BplaPos>(ntab) : nullptr;
   int2* d_items = items.empty() ? nullptr : A.take<int2>(items.size());
   if (d_items)
-    SK_HIP(ctx, hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(int2),
-                               hipMemcpyHostToDevice, ctx->stream));
+    SK_HIP(ctx, sk::h2d(ctx, d_items, items.data(), items.size() * sizeof(int2), ctx->stream));
   hipStream_t S = ctx->stream;
-  SK_HIP(ctx, hipMemcpyAsync(d_tb, kp->score_table, 16 * 8, hipMemcpyHostToDevice, S));
-  SK_HIP(ctx, hipMemcpyAsync(d_px, x, nb * 4, hipMemcpyHostToDevice, S));
-  SK_HIP(ctx, hipMemcpyAsync(d_py, y, nb * 4, hipMemcpyHostToDevice, S));
-  if (permute) SK_HIP(ctx, hipMemcpyAsync(d_oidx, oidx.data(), nb * 8, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, sk::h2d(ctx, d_tb, kp->score_table, 16 * 8, S));
+  SK_HIP(ctx, sk::h2d(ctx, d_px, x, nb * 4, S));
+  SK_HIP(ctx, sk::h2d(ctx, d_py, y, nb * 4, S));
+  if (permute) SK_HIP(ctx, sk::h2d(ctx, d_oidx, oidx.data(), nb * 8, S));
   SK_HIP(ctx, hipMemsetAsync(d_ctr, 0, 8 * sizeof(unsigned long long), S));
   sk::BplaLaunch T;
   T.xset = xs_->dev;
@@ -1518,15 +1657,11 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   }
   SK_HIP(ctx, hipEventRecord(ctx->ev1, S));
   const double tb3 = host_stats ? now_ms() : 0.0;
-  SK_HIP(ctx, hipStreamSynchronize(S));
-  SK_HIP(ctx, sk::lev_collect(ctx));
-  float ms = 0.f;
-  SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-  ctx->last_stem_ms = ms;
   ctx->last_launches = (n_fast ? 1 : 0) + (n_fast < n ? 1 : 0);
+  SK_HIP(ctx, sk::call_finish(ctx, S, true, false));
   if (host_stats)
     fprintf(stderr, "[sk bpla host] plan %.3f ms, uploads %.3f ms, launches %.3f ms, wait %.3f ms (GPU %.3f ms)\n",
-            tb1 - tb0, tb2 - tb1, tb3 - tb2, now_ms() - tb3, (double)ms);
+            tb1 - tb0, tb2 - tb1, tb3 - tb2, now_ms() - tb3, ctx->async ? -1.0 : ctx->last_stem_ms);
   return SK_OK;
 }
 
@@ -1903,8 +2038,20 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   for (int64_t k = 0; k < n; ++k)
     if (x[k] < 0 || x[k] >= nx || y[k] < 0 || y[k] >= ny)
       return fail(ctx, SK_ERR_RANGE, "pair index out of range");
+  SK_HIP(ctx, sk::call_begin(ctx));
   if (kind_is_bpla(kp->kind)) return run_bpla(ctx, xs_, ys_, kp, x, y, n, out_dev);
-  if (kp->kind == SK_STEM4D) return run_stem4d(ctx, xs_, ys_, kp, x, y, n, out_dev);
+  if (kp->kind == SK_STEM4D) {
+    // synchronous batches (each waits for its spans): its totals are final
+    rc = run_stem4d(ctx, xs_, ys_, kp, x, y, n, out_dev);
+    if (rc == SK_OK && ctx->async) {
+      ctx->acc_stem_ms += ctx->last_stem_ms;
+      ctx->acc_cells += ctx->last_cells;
+      ctx->acc_launches += ctx->last_launches;
+      ctx->acc_launch_ms += ctx->last_launch_ms_sum;
+      ctx->acc_launch_n += ctx->last_launch_n;
+    }
+    return rc;
+  }
 
   const bool stem = kind_has_stem(kp->kind), str = kind_has_str(kp->kind);
   const HostPack& PX = xs_->pack;
@@ -2211,10 +2358,10 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   const std::vector<double> gl = gap_powers(kp->loop_gap, max_len + 4);
   const std::vector<double> gs = gap_powers(kp->gap, max_len + 4);
   hipStream_t S = ctx->stream;
-  SK_HIP(ctx, hipMemcpyAsync(d_co, co.data(), 256 * 8, hipMemcpyHostToDevice, S));
-  SK_HIP(ctx, hipMemcpyAsync(d_st, st.data(), 16 * 8, hipMemcpyHostToDevice, S));
-  SK_HIP(ctx, hipMemcpyAsync(d_gp_loop, gl.data(), gl.size() * 8, hipMemcpyHostToDevice, S));
-  SK_HIP(ctx, hipMemcpyAsync(d_gp_str, gs.data(), gs.size() * 8, hipMemcpyHostToDevice, S));
+  SK_HIP(ctx, sk::h2d(ctx, d_co, co.data(), 256 * 8, S));
+  SK_HIP(ctx, sk::h2d(ctx, d_st, st.data(), 16 * 8, S));
+  SK_HIP(ctx, sk::h2d(ctx, d_gp_loop, gl.data(), gl.size() * 8, S));
+  SK_HIP(ctx, sk::h2d(ctx, d_gp_str, gs.data(), gs.size() * 8, S));
   SK_HIP(ctx, hipMemsetAsync(d_ctr, 0, 64 * sizeof(int), S));
 
   double* stem_out = (combine_mode(kp->kind) == sk::kCombineStem) ? out_dev : d_stem;
@@ -2224,25 +2371,23 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   // here, ahead of the stem launches
   const bool side = stem && str;
   if (str) {
-    SK_HIP(ctx, hipMemcpyAsync(d_px, spx.empty() ? x : spx.data(), nb * 4, hipMemcpyHostToDevice, S));
-    SK_HIP(ctx, hipMemcpyAsync(d_py, spy.empty() ? y : spy.data(), nb * 4, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, sk::h2d(ctx, d_px, spx.empty() ? x : spx.data(), nb * 4, S));
+    SK_HIP(ctx, sk::h2d(ctx, d_py, spy.empty() ? y : spy.data(), nb * 4, S));
     if (d_soidx)
-      SK_HIP(ctx, hipMemcpyAsync(d_soidx, soidx.data(), soidx.size() * 8, hipMemcpyHostToDevice, S));
+      SK_HIP(ctx, sk::h2d(ctx, d_soidx, soidx.data(), soidx.size() * 8, S));
     if (side) {
       SK_HIP(ctx, hipEventRecord(ctx->evf, S));
       SK_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->evf, 0));
     }
   }
   if (stem) {
-    SK_HIP(ctx, hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(int4),
-                               hipMemcpyHostToDevice, S));
-    SK_HIP(ctx, hipMemcpyAsync(d_ixs, ixs.data(), nb * 4, hipMemcpyHostToDevice, S));
-    SK_HIP(ctx, hipMemcpyAsync(d_oidx, ioidx.data(), nb * 8, hipMemcpyHostToDevice, S));
+    SK_HIP(ctx, sk::h2d(ctx, d_items, items.data(), items.size() * sizeof(int4), S));
+    SK_HIP(ctx, sk::h2d(ctx, d_ixs, ixs.data(), nb * 4, S));
+    SK_HIP(ctx, sk::h2d(ctx, d_oidx, ioidx.data(), nb * 8, S));
     if (phi_on) {
-      SK_HIP(ctx, hipMemcpyAsync(d_iphi_off, item_phi_off.data(), item_phi_off.size() * 4,
-                                 hipMemcpyHostToDevice, S));
+      SK_HIP(ctx, sk::h2d(ctx, d_iphi_off, item_phi_off.data(), item_phi_off.size() * 4, S));
       if (!item_phi.empty())
-        SK_HIP(ctx, hipMemcpyAsync(d_iphi, item_phi.data(), item_phi.size() * 4, hipMemcpyHostToDevice, S));
+        SK_HIP(ctx, sk::h2d(ctx, d_iphi, item_phi.data(), item_phi.size() * 4, S));
     }
     const double gap2 = kp->loop_gap * kp->loop_gap;
     const size_t nnd = std::max<size_t>(PX.nd_a.size(), 1);
@@ -2367,9 +2512,9 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     }
     if (!big_x.empty()) {
       const size_t nbig = big_x.size();
-      SK_HIP(ctx, hipMemcpyAsync(d_bx, big_x.data(), nbig * 4, hipMemcpyHostToDevice, S));
-      SK_HIP(ctx, hipMemcpyAsync(d_by, big_y.data(), nbig * 4, hipMemcpyHostToDevice, S));
-      SK_HIP(ctx, hipMemcpyAsync(d_bo, big_o.data(), nbig * 8, hipMemcpyHostToDevice, S));
+      SK_HIP(ctx, sk::h2d(ctx, d_bx, big_x.data(), nbig * 4, S));
+      SK_HIP(ctx, sk::h2d(ctx, d_by, big_y.data(), nbig * 4, S));
+      SK_HIP(ctx, sk::h2d(ctx, d_bo, big_o.data(), nbig * 8, S));
       sk::StemBigLaunch BL;
       BL.xset = xs_->dev;
       BL.yset = ys_->dev;
@@ -2495,19 +2640,8 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   const int32_t mode = combine_mode(kp->kind);
   if (mode != sk::kCombineStem && mode != sk::kCombineStr)
     SK_HIP(ctx, sk::launch_combine(d_stem, d_str, out_dev, n, mode, kp->alpha, kp->beta, S));
-  // timings (blocking read of the events happens in sk_last_timing callers)
-  SK_HIP(ctx, hipStreamSynchronize(S));
-  if (stem) {
-    float ms = 0.f;
-    SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-    ctx->last_stem_ms = ms;
-    SK_HIP(ctx, sk::lev_collect(ctx));
-  }
-  if (str && !str_skip) {
-    float ms = 0.f;
-    SK_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev2, ctx->ev3));
-    ctx->last_str_ms = ms;
-  }
+  // timings: now (synchronous calls), or when sk_sync_timing asks (async)
+  SK_HIP(ctx, sk::call_finish(ctx, S, stem, str && !str_skip));
   return SK_OK;
 }
 
@@ -2523,6 +2657,7 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
   rc = check_set(ctx, ys_);
   if (rc) return rc;
   if (n <= 0) return n < 0 ? fail(ctx, SK_ERR_INVALID, "negative pair count") : SK_OK;
+  SK_HIP(ctx, sk::call_begin(ctx));  // (synchronous: a fresh timing set, not a pending one)
   for (int64_t k = 0; k < n; ++k) {
     if (x[k] < 0 || x[k] >= (int)xs_->ex.size() || y[k] < 0 || y[k] >= (int)ys_->ex.size())
       return fail(ctx, SK_ERR_INVALID, "pair index out of range");
@@ -2727,7 +2862,10 @@ int pairs_host(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   SK_HIP(ctx, hipMalloc(&d, (size_t)n * sizeof(double)));
   int rc = run_pairs(ctx, xs_, ys_, kp, x, y, n, d);
   if (rc == SK_OK) {
-    hipError_t e = hipMemcpy(out, d, (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
+    // the results are on the context's stream (an asynchronous call has not
+    // waited for them): read them in its order
+    hipError_t e = hipMemcpyAsync(out, d, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) rc = fail(ctx, SK_ERR_HIP, hipGetErrorString(e));
   }
   (void)hipFree(d);
@@ -2825,8 +2963,9 @@ int sk_open(int device, void* hip_stream, sk_context** out) {
       hipEventCreateWithFlags(&c->evj, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->evk, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->evx, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess) {
+      hipEventCreateWithFlags(&c->stage[0].ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->stage[1].ev, hipEventDisableTiming) != hipSuccess ||
+      sk::call_begin(c.get()) != hipSuccess) {  // (creates timing set 0: ev0..ev3)
     sk_close(c.release());
     return SK_ERR_HIP;
   }
@@ -2854,9 +2993,15 @@ int sk_close(sk_context* ctx) {
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   for (hipEvent_t e : {ctx->evf, ctx->evj, ctx->evk, ctx->evx, ctx->eva})
     if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {ctx->ev0, ctx->ev1, ctx->ev2, ctx->ev3})
-    if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : ctx->lev) (void)hipEventDestroy(e);
+  for (auto& T : ctx->tset) {  // (ev0..ev3 are the current set's)
+    for (hipEvent_t e : T.ev)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : T.lev) (void)hipEventDestroy(e);
+  }
+  for (auto& G : ctx->stage) {
+    if (G.ev) (void)hipEventDestroy(G.ev);
+    for (auto& b : G.blocks) (void)hipHostFree(b.first);
+  }
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SK_OK;
@@ -3499,6 +3644,32 @@ int sk_last_timing(const sk_context* ctx, double* stem_ms, double* string_ms, do
   if (string_ms) *string_ms = ctx->last_str_ms;
   if (cells) *cells = ctx->last_cells;
   if (launches) *launches = ctx->last_launches;
+  return SK_OK;
+}
+
+int sk_set_async(sk_context* ctx, int32_t on) {
+  if (!ctx) return SK_ERR_INVALID;
+  if (ctx->async && !on) {  // resolve what is pending first
+    const int rc = sk_sync_timing(ctx);
+    if (rc) return rc;
+  }
+  ctx->async = on != 0;
+  return SK_OK;
+}
+
+int sk_sync_timing(sk_context* ctx) {
+  if (!ctx) return SK_ERR_INVALID;
+  if (!ctx->async) return SK_OK;
+  for (int k = 0; k < sk_context::kTSets; ++k)
+    if (sk::tset_resolve(ctx, k) != hipSuccess) return fail(ctx, SK_ERR_HIP, "sk_sync_timing: event");
+  ctx->last_stem_ms = ctx->acc_stem_ms;
+  ctx->last_str_ms = ctx->acc_str_ms;
+  ctx->last_cells = ctx->acc_cells;
+  ctx->last_launches = ctx->acc_launches;
+  ctx->last_launch_ms_sum = ctx->acc_launch_ms;
+  ctx->last_launch_n = ctx->acc_launch_n;
+  ctx->acc_stem_ms = ctx->acc_str_ms = ctx->acc_cells = ctx->acc_launch_ms = 0.0;
+  ctx->acc_launch_n = ctx->acc_launches = 0;
   return SK_OK;
 }
 

@@ -584,6 +584,16 @@ class Context:
         self._chk(lib().sk_last_timing(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return dict(stem_ms=a.value, string_ms=b.value, cells=c.value, launches=d.value)
 
+    def set_async(self, on: bool = True) -> None:
+        """sk_set_async: compute calls return once enqueued (results on the
+        device after a stream sync); timings then come from sync_timing()."""
+        self._chk(lib().sk_set_async(self._h, 1 if on else 0))
+
+    def sync_timing(self) -> None:
+        """sk_sync_timing: wait for every asynchronous call since the last
+        sync_timing; last_timing() / last_launch_ms() then report their sums."""
+        self._chk(lib().sk_sync_timing(self._h))
+
     def last_launch_ms(self):
         """Per-launch HIP-event durations of the last call's dominant kernel:
         (summed ms, launch count); launches on several streams overlap."""
