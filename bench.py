@@ -68,7 +68,10 @@ PEAK_FP64_TFS = 78.6    # FP64 vector
 # term at L=200).  Same two DPs, plus a log epilogue in sk_combine_kernel.
 CONFIGS = {
     "ns": dict(kernel="ss", cls="LSuStemStrKernel", n=4096, L=200, slices=48, cid=2, cpu_pairs=12288),
-    "c2": dict(kernel="ss", n=256, L=150, slices=4, cid=1, cpu_pairs=12288),
+    # C2's whole Gram is 32,896 pairs (0.2 s): a step is the whole Gram, the
+    # unit the reference computes per call (kernel_matrix.cpp:485-575), not a
+    # slice whose launch fill and tail would dominate ("whole": steps repeat it)
+    "c2": dict(kernel="ss", n=256, L=150, slices=1, whole=True, cid=1, cpu_pairs=12288),
     "c3": dict(kernel="stem4d", n=1024, L=200, slices=2050, cid=2, cpu_pairs=32),
     "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=16, cid=3, cpu_pairs=196608),
     "c5": dict(kernel="stem", n=8192, L=300, slices=128, cid=4, cpu_pairs=4096),
@@ -680,7 +683,8 @@ def main():
     S = a.slices
     if a.full:
         a.steps, a.warmup = 1, 0
-    S = max(S, (a.warmup + a.steps) * world)
+    if not cfg.get("whole"):
+        S = max(S, (a.warmup + a.steps) * world)
     S = -(-S // world) * world  # a multiple of N: rank r's slices are cells k % N == r
     slice_of, per, step_kind, n_cells = make_plan(kind, a.n, world, rank, S)
     eng.alloc(per)

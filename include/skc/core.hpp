@@ -474,10 +474,11 @@ inline void fold_rows(RowsData& d, const BPMatrixOptions& opts) {
     }
     return;
   }
-  if (opts.no_LonelyPairs) throw "--noLonelyPairs is not supported by the engine's fold";
   if (opts.alifold || opts.contrafold || opts.n_samples > 0)
     throw "only the FOLD method (McCaskill per row) is supported by the engine";
-  Engine::get().fold(erased, (opts.no_GU ? SK_FOLD_NO_GU : 0) | (opts.no_closingGU ? SK_FOLD_NO_CLOSING_GU : 0),
+  Engine::get().fold(erased,
+                     (opts.no_GU ? SK_FOLD_NO_GU : 0) | (opts.no_closingGU ? SK_FOLD_NO_CLOSING_GU : 0) |
+                         (opts.no_LonelyPairs ? SK_FOLD_NO_LONELY_PAIRS : 0),
                      d.bpp);
 }
 

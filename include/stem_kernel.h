@@ -284,8 +284,8 @@ int sk_fold_synthetic(const char *seq, int32_t n, int32_t no_gu, double *out);
  * never pair.  out: for each k in order, n_k(n_k-1)/2 doubles in the packed
  * layout of sk_dataset_add, concatenated.  log_z (optional): ln Z per
  * sequence.  flags: SK_FOLD_NO_GU (--noGU), SK_FOLD_NO_CLOSING_GU
- * (--noClosingGU); SK_FOLD_NO_LONELY_PAIRS (--noLonelyPairs) is
- * SK_ERR_UNSUPPORTED.  Sequences up to ~1,400 nt (SK_ERR_UNSUPPORTED when Z
+ * (--noClosingGU), SK_FOLD_NO_LONELY_PAIRS (--noLonelyPairs: the legacy
+ * ViennaRNA pair-type filter, pairs that can only be isolated removed).  Sequences up to ~1,400 nt (SK_ERR_UNSUPPORTED when Z
  * leaves the double range). */
 #define SK_FOLD_NO_GU 1
 #define SK_FOLD_NO_CLOSING_GU 2

@@ -42,7 +42,7 @@
 //     Turner-1999 core loop model, parity against ViennaRNA unpinned; a
 //     one-line notice goes to stderr the first time it folds); MData folds
 //     each gap-erased, lowercased row with it (honouring --noGU and
-//     --noClosingGU; --noLonelyPairs and --use-alifold are refused) and
+//     --noClosingGU, --noLonelyPairs; --use-alifold is refused) and
 //     averages alignment rows as the reference does
 //     (common/bpmatrix.cpp:306-342).  BPMatrix::Options::fold plugs in any
 //     other folder (e.g. ViennaRNA itself, or skc::synthetic_fold);

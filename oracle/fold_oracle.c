@@ -75,12 +75,50 @@ typedef struct {
   int n;
   int *s;  /* base codes */
   int no_gu, no_closing_gu;
+  unsigned char *lp;  /* --noLonelyPairs: lp[i*n+j] = the pair survives the filter (NULL: off) */
 } fold_in;
 
-static int ptype(const fold_in *F, int i, int j) {
+static int ptype_raw(const fold_in *F, int i, int j) {
   int t = pair_type(F->s[i], F->s[j]);
   if (F->no_gu && (t == 3 || t == 4)) return 0;
   return t;
+}
+static int ptype(const fold_in *F, int i, int j) {
+  int t = ptype_raw(F, i, j);
+  if (t && F->lp && !F->lp[(size_t)i * F->n + j]) return 0;
+  return t;
+}
+
+/* --noLonelyPairs (common/bpmatrix.cpp:56-58, 149: Vienna::noLonelyPairs
+ * before pf_fold).  The legacy ViennaRNA partition function (1.8,
+ * part_func.c make_ptypes; not vendored, restated from its published
+ * source) applies it only through the pair-type table: walking each chain of
+ * pairs (i, j), (i-1, j+1), ... outward from its innermost pair, a pair
+ * whose inner neighbour was removed or cannot pair, and whose outer
+ * neighbour cannot pair, is removed (it "can only form isolated pairs").  As
+ * written there the outer-neighbour type is only re-read while i > 1 and
+ * j < n (1-based), so at a chain's outermost pair it still holds that
+ * pair's own type: such a pair is kept whenever it can pair (unless it is
+ * also the chain's innermost pair).  Chains start at j - i = 4 and 5
+ * (0-based: hairpins of 3 and 4). */
+static void lonely_filter(fold_in *F) {
+  int n = F->n;
+  F->lp = (unsigned char *)calloc((size_t)(n ? n : 1) * (n ? n : 1), 1);
+  for (int k = 0; k < n; ++k)
+    for (int l = 1; l <= 2; ++l) {
+      int i = k, j = k + 3 + l, otype = 0, ntype = 0, type;
+      if (j >= n) continue;
+      type = ptype_raw(F, i, j);
+      while (i >= 0 && j < n) {
+        if (i > 0 && j < n - 1) ntype = ptype_raw(F, i - 1, j + 1);
+        if (!otype && !ntype) type = 0;
+        F->lp[(size_t)i * n + j] = type != 0;
+        otype = type;
+        type = ntype;
+        --i;
+        ++j;
+      }
+    }
 }
 static int is_gu(int t) { return t == 3 || t == 4; }
 static double au(int t) { return t > 2 ? (double)TerminalAU : 0.0; }
@@ -117,13 +155,21 @@ static double e_ext_branch(const fold_in *F, int p, int q) { return au(ptype(F, 
 
 static double boltz(double e) { return e >= ORC_INF ? 0.0 : exp(-e / kT); }
 
+/* flags bit 0 no_gu, 1 no_closing_gu, 2 no_lonely_pairs (the library's
+ * SK_FOLD_* bits); the older two-flag entry points pass no_closing_gu alone */
 static int setup(fold_in *F, const char *seq, int no_gu, int no_closing_gu) {
   F->n = (int)strlen(seq);
   F->s = (int *)malloc(sizeof(int) * (F->n ? F->n : 1));
   for (int k = 0; k < F->n; ++k) F->s[k] = base_code(seq[k]);
   F->no_gu = no_gu;
-  F->no_closing_gu = no_closing_gu;
+  F->no_closing_gu = no_closing_gu & 1;
+  F->lp = NULL;
+  if (no_closing_gu & 2) lonely_filter(F);
   return F->n;
+}
+static void teardown(fold_in *F) {
+  free(F->s);
+  free(F->lp);
 }
 
 static size_t tri(int n, int i, int j) { return (size_t)i * n - (size_t)i * (i + 1) / 2 + (size_t)(j - i - 1); }
@@ -137,7 +183,7 @@ double orc_fold_mccaskill(const char *seq, int no_gu, int no_closing_gu, double 
   fold_in F;
   int n = setup(&F, seq, no_gu, no_closing_gu);
   if (n == 0) {
-    free(F.s);
+    teardown(&F);
     return 0.0;
   }
   size_t N2 = (size_t)n * n;
@@ -218,7 +264,7 @@ double orc_fold_mccaskill(const char *seq, int no_gu, int no_closing_gu, double 
     }
   }
 #undef A
-  free(Qb); free(Qm); free(Qm1); free(Hb); free(Hm); free(Hm1); free(Q5); free(H5); free(F.s);
+  free(Qb); free(Qm); free(Qm1); free(Hb); free(Hm); free(Hm1); free(Q5); free(H5); teardown(&F);
   return log(Z);
 }
 
@@ -267,11 +313,11 @@ double orc_fold_structure_energy(const char *seq, const int *pt, int no_gu, int 
   setup(&F, seq, no_gu, no_closing_gu);
   for (int i = 0; i < F.n; ++i)
     if (pt[i] > i && !ptype(&F, i, pt[i])) {
-      free(F.s);
+      teardown(&F);
       return ORC_INF;
     }
   double e = struct_energy(&F, pt);
-  free(F.s);
+  teardown(&F);
   return e;
 }
 
@@ -336,6 +382,6 @@ double orc_fold_enum(const char *seq, int no_gu, int no_closing_gu, double *bpp,
     for (size_t k = 0; k < (size_t)n * (n - 1) / 2; ++k) bpp[k] /= E.Z;
   if (n_struct) *n_struct = E.count;
   free(E.pt);
-  free(F.s);
+  teardown(&F);
   return log(E.Z);
 }

@@ -289,21 +289,26 @@ def _fold_lib():
     return L
 
 
-def fold_mccaskill(seq: str, no_gu=False, no_closing_gu=False):
+def _fl(no_closing_gu, no_lp):
+    """fold_oracle.c's third argument: bit 0 --noClosingGU, bit 1 --noLonelyPairs."""
+    return int(bool(no_closing_gu)) | (2 if no_lp else 0)
+
+
+def fold_mccaskill(seq: str, no_gu=False, no_closing_gu=False, no_lp=False):
     """(ln Z, packed bpp) of the restated McCaskill DP (fold_oracle.c)."""
     n = len(seq)
     bpp = np.zeros(max(n * (n - 1) // 2, 1))
-    lz = _fold_lib().orc_fold_mccaskill(seq.encode(), int(no_gu), int(no_closing_gu),
+    lz = _fold_lib().orc_fold_mccaskill(seq.encode(), int(no_gu), _fl(no_closing_gu, no_lp),
                                         bpp.ctypes.data_as(_D))
     return lz, bpp[: n * (n - 1) // 2]
 
 
-def fold_enum(seq: str, no_gu=False, no_closing_gu=False):
+def fold_enum(seq: str, no_gu=False, no_closing_gu=False, no_lp=False):
     """(ln Z, packed bpp, number of structures) by exhaustive enumeration."""
     n = len(seq)
     bpp = np.zeros(max(n * (n - 1) // 2, 1))
     cnt = C.c_long()
-    lz = _fold_lib().orc_fold_enum(seq.encode(), int(no_gu), int(no_closing_gu),
+    lz = _fold_lib().orc_fold_enum(seq.encode(), int(no_gu), _fl(no_closing_gu, no_lp),
                                    bpp.ctypes.data_as(_D), C.byref(cnt))
     return lz, bpp[: n * (n - 1) // 2], cnt.value
 

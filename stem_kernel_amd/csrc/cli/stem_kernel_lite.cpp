@@ -17,7 +17,7 @@
 //
 // Differences, by necessity: base-pairing probabilities come from the
 // engine's GPU McCaskill (sk_fold_mccaskill) instead of ViennaRNA;
-// --noLonelyPairs and --use-alifold are refused; .bz2 output goes through the
+// --use-alifold is refused; .bz2 output goes through the
 // system's libbz2.so.1 (loaded at run time: the image has the library but not
 // its headers).  The
 // reference's default kernel (SuStemStr without --log) only estimates memory
@@ -98,7 +98,7 @@ const char* kUsage =
     "Folding Options:\n"
     "  --noGU                      disallow GU wobble base-pairs\n"
     "  --noClosingGU               disallow closing GU base-pairs\n"
-    "  --noLonelyPairs             disallow lonely base-pairs (not supported by the engine)\n"
+    "  --noLonelyPairs             disallow lonely base-pairs\n"
     "  --use-alifold               use pf_alifold (not supported by the engine)\n"
     "  --pf-scale                  calculate appropriciate pf_scales using MFE (no effect)\n";
 
@@ -571,7 +571,6 @@ int main(int argc, char** argv) {
   try {
     if (o.predict_output.size() > o.trained_model_file.size())
       throw "--predict: every prediction file needs the --model of the same position";
-    if (o.bp.no_LonelyPairs) throw "--noLonelyPairs is not supported by the engine's fold";
     if (o.bp.alifold) throw "--use-alifold is not supported by the engine's fold";
     if (o.predict_mode && !o.trained_model_file.empty()) load_sv_index(o.sv_index, o.trained_model_file);
     // kernel choice: main.cpp:166-214

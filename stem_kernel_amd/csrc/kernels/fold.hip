@@ -80,8 +80,10 @@ __global__ void __launch_bounds__(256) sk_fold_kernel(FoldLaunch P) {
   T.mli = P.tab[P.o_ml + 1];
   const double* scp = T.scp;
   const bool ngu = P.no_gu != 0, ncg = P.no_closing_gu != 0;
+  const uint8_t* __restrict__ lp = P.lp ? P.lp + sq.lp_off : nullptr;
   auto ptype = [&](int i, int j) {
     const int t = pair_raw(c[i], c[j]);
+    if (lp && !lp[(size_t)i * n + j]) return 0;  // --noLonelyPairs (host table)
     return (ngu && is_gu(t)) ? 0 : t;
   };
 

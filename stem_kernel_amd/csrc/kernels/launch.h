@@ -269,6 +269,7 @@ struct FoldSeq {
   int64_t seq_off = 0;   // into codes
   int64_t work_off = 0;  // into work: 10 n^2 + 2 (n + 1) doubles
   int64_t out_off = 0;   // into out: n (n - 1) / 2 packed probabilities
+  int64_t lp_off = 0;    // into lp (--noLonelyPairs): n x n pair filter
   int32_t n = 0, pad = 0;
 };
 struct FoldLaunch {
@@ -278,6 +279,7 @@ struct FoldLaunch {
   int32_t o_st = 0, o_hp = 0, o_bu = 0, o_in = 0, o_ni = 0, o_au = 0, o_ml = 0, o_scp = 0;
   double log_sc = 0.0;            // ln of the per-nucleotide scale
   int32_t no_gu = 0, no_closing_gu = 0;
+  const uint8_t* lp = nullptr;    // --noLonelyPairs pair filter (nullptr: off)
   double* work = nullptr;
   double* out = nullptr;
   double* log_z = nullptr;        // per sequence of the launch (nullptr: not wanted)

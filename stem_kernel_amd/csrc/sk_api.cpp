@@ -3471,11 +3471,42 @@ int8_t fold_code(char ch) {
 
 }  // namespace
 
+// --noLonelyPairs (common/bpmatrix.cpp:56-58, 149, Vienna::noLonelyPairs):
+// the legacy ViennaRNA partition function applies it through its pair-type
+// table only (1.8 part_func.c make_ptypes; not vendored).  Walking each chain
+// (i, j), (i-1, j+1), ... outward from its innermost pair (j - i = 4 or 5),
+// a pair is dropped when its inner neighbour was dropped or cannot pair and
+// its outer neighbour cannot pair; the outer type is re-read only inside the
+// sequence, so a chain's outermost pair compares against its own type.
+// lp[i*n + j] = 1 where the pair survives (codes: fold_code, -1 never pairs).
+void lonely_pair_table(const int8_t* c, int n, bool no_gu, uint8_t* lp) {
+  static const int8_t pt[16] = {0, 0, 0, 5, 0, 0, 1, 0, 0, 2, 0, 4, 6, 0, 3, 0};
+  auto raw = [&](int i, int j) {
+    const int t = (c[i] < 0 || c[j] < 0) ? 0 : pt[c[i] * 4 + c[j]];
+    return (no_gu && (t == 3 || t == 4)) ? 0 : t;
+  };
+  std::fill(lp, lp + (size_t)n * n, (uint8_t)0);
+  for (int k = 0; k < n; ++k)
+    for (int l = 1; l <= 2; ++l) {
+      int i = k, j = k + 3 + l, otype = 0, ntype = 0;
+      if (j >= n) continue;
+      int type = raw(i, j);
+      for (; i >= 0 && j < n; --i, ++j) {
+        if (i > 0 && j < n - 1) ntype = raw(i - 1, j + 1);
+        if (!otype && !ntype) type = 0;
+        lp[(size_t)i * n + j] = type != 0;
+        otype = type;
+        type = ntype;
+      }
+    }
+}
+
 int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32_t flags,
                       double* out, double* log_z) {
   if (!ctx || n < 0 || (n > 0 && (!seqs || !out))) return fail(ctx, SK_ERR_INVALID, "null argument");
-  if (flags & ~(SK_FOLD_NO_GU | SK_FOLD_NO_CLOSING_GU))
-    return fail(ctx, SK_ERR_UNSUPPORTED, "fold: only SK_FOLD_NO_GU / SK_FOLD_NO_CLOSING_GU");
+  if (flags & ~(SK_FOLD_NO_GU | SK_FOLD_NO_CLOSING_GU | SK_FOLD_NO_LONELY_PAIRS))
+    return fail(ctx, SK_ERR_UNSUPPORTED, "fold: unknown flag");
+  const bool no_lp = (flags & SK_FOLD_NO_LONELY_PAIRS) != 0;
   if (n == 0) return SK_OK;
   std::vector<int> len(n);
   int max_len = 0;
@@ -3498,6 +3529,7 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
     // batch: sequences whose tables fit the budget (at least one)
     std::vector<sk::FoldSeq> sq;
     std::vector<int8_t> codes;
+    std::vector<uint8_t> lp;  // --noLonelyPairs tables
     size_t work = 0, outn = 0;
     int32_t b1 = b0;
     for (; b1 < n; ++b1) {
@@ -3510,13 +3542,18 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
       f.out_off = (int64_t)outn;
       f.n = (int32_t)nn;
       for (size_t a = 0; a < nn; ++a) codes.push_back(fold_code(seqs[b1][a]));
+      if (no_lp) {
+        f.lp_off = (int64_t)lp.size();
+        lp.resize(lp.size() + nn * nn);
+        lonely_pair_table(codes.data() + f.seq_off, (int)nn, L.no_gu != 0, lp.data() + f.lp_off);
+      }
       work += w;
       outn += nn > 1 ? nn * (nn - 1) / 2 : 0;
       sq.push_back(f);
     }
     const int nb = b1 - b0;
-    size_t need = sq.size() * sizeof(sk::FoldSeq) + codes.size() + tab.size() * 8 +
-                  (outn + nb) * 8 + 6 * 256;
+    size_t need = sq.size() * sizeof(sk::FoldSeq) + codes.size() + lp.size() + tab.size() * 8 +
+                  (outn + nb) * 8 + 7 * 256;
     int rc = ensure_work(ctx, need);
     if (rc) return rc;
     rc = ensure_scratch(ctx, std::max<size_t>(work * 8, 64));
@@ -3527,6 +3564,10 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
     double* d_tab = A.take<double>(tab.size());
     double* d_out = A.take<double>(std::max<size_t>(outn, 1));
     double* d_lz = A.take<double>(nb);
+    uint8_t* d_lp = no_lp ? A.take<uint8_t>(std::max<size_t>(lp.size(), 1)) : nullptr;
+    if (no_lp && !lp.empty())
+      SK_HIP(ctx, hipMemcpyAsync(d_lp, lp.data(), lp.size(), hipMemcpyHostToDevice, S));
+    L.lp = d_lp;
     SK_HIP(ctx, hipMemcpyAsync(d_sq, sq.data(), sq.size() * sizeof(sk::FoldSeq), hipMemcpyHostToDevice, S));
     if (!codes.empty())
       SK_HIP(ctx, hipMemcpyAsync(d_codes, codes.data(), codes.size(), hipMemcpyHostToDevice, S));

@@ -348,7 +348,7 @@ class Dataset:
 
     @classmethod
     def folded(cls, ctx: "Context", alns, labels=None, th: float = 0.01, no_gu: bool = False,
-               no_closing_gu: bool = False, threads: int = 0):
+               no_closing_gu: bool = False, threads: int = 0, no_lonely_pairs: bool = False):
         """Examples whose rows are folded on ctx's GPU (sk_fold_mccaskill, the
         engine's McCaskill in place of Vienna pf_fold) and built on host
         threads (sk_dataset_add_folded).  ``alns``: sequences or alignments
@@ -362,7 +362,7 @@ class Dataset:
         flat = [r.encode() for a in alns for r in a]
         rarr = (C.c_char_p * max(len(flat), 1))(*flat)
         larr = None if labels is None else (C.c_char_p * n)(*[l.encode() for l in labels])
-        flags = (1 if no_gu else 0) | (2 if no_closing_gu else 0)
+        flags = (1 if no_gu else 0) | (2 if no_closing_gu else 0) | (4 if no_lonely_pairs else 0)
         ctx._chk(lib().sk_dataset_add_folded(ctx.handle, ds._h, n, nr, rarr, larr, C.c_float(th),
                                              flags, threads))
         return ds
@@ -441,7 +441,7 @@ class Context:
         return check(rc, self._h)
 
     def fold(self, seqs: Sequence[str], no_gu: bool = False, no_closing_gu: bool = False,
-             log_z: bool = False):
+             log_z: bool = False, no_lonely_pairs: bool = False):
         """McCaskill base-pairing probabilities of every sequence on this GPU
         (sk_fold_mccaskill): a list of packed upper triangles, plus ln Z per
         sequence when ``log_z``."""
@@ -451,7 +451,7 @@ class Context:
         out = np.zeros(max(sum(sizes), 1))
         lz = np.zeros(max(n, 1))
         sarr = (C.c_char_p * max(n, 1))(*[s.encode() for s in seqs])
-        flags = (1 if no_gu else 0) | (2 if no_closing_gu else 0)
+        flags = (1 if no_gu else 0) | (2 if no_closing_gu else 0) | (4 if no_lonely_pairs else 0)
         self._chk(lib().sk_fold_mccaskill(self._h, n, sarr, flags,
                                           out.ctypes.data_as(C.POINTER(C.c_double)),
                                           lz.ctypes.data_as(C.POINTER(C.c_double))))

@@ -53,8 +53,7 @@ def test_usage_without_arguments():
         assert flag in r.stdout
 
 
-@pytest.mark.parametrize("flag,msg", [("--noLonelyPairs", "noLonelyPairs"),
-                                      ("--use-alifold", "use-alifold")])
+@pytest.mark.parametrize("flag,msg", [("--use-alifold", "use-alifold")])
 def test_refused_folding_options(tmp_path, flag, msg):
     _write_fa(tmp_path / "a.fa", ["GGGGAAACCCC"])
     r = _run([tmp_path / "o.txt", "+1", tmp_path / "a.fa", flag])
@@ -125,6 +124,20 @@ def test_cli_train_gz_and_options(gpu_ctx, fa_files):
     labels, got = _parse_libsvm(gzip.open(out, "rt").read())
     ds = ska.Dataset.folded(gpu_ctx, pos, th=0.02, no_gu=True)
     ref = gpu_ctx.gram(ds, ska.SuStemStrKernel(beta=0.4, loop_gap=0.3, gap=0.7, len_band=8))
+    assert np.max(np.abs(got - ref) / np.abs(ref)) < 1e-5
+
+
+@pytest.mark.gpu
+def test_cli_no_lonely_pairs(gpu_ctx, fa_files):
+    """--noLonelyPairs (common/bpmatrix.cpp:56-58, 149) reaches the fold: the
+    Gram is the one of examples folded with SK_FOLD_NO_LONELY_PAIRS."""
+    d, pos, neg, _ = fa_files
+    out = d / "gram_nolp.txt"
+    r = _run(["--noLonelyPairs", out, "+1", d / "pos.fa"])
+    assert r.returncode == 0, r.stdout + r.stderr
+    _, got = _parse_libsvm(out.read_text())
+    ds = ska.Dataset.folded(gpu_ctx, pos, no_lonely_pairs=True)
+    ref = gpu_ctx.gram(ds, ska.SuStemStrKernel())
     assert np.max(np.abs(got - ref) / np.abs(ref)) < 1e-5
 
 

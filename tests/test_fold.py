@@ -6,7 +6,8 @@ Parity against ViennaRNA is unpinned (its parameter files are absent; the
 model is the Turner-1999 core).  Pinned here instead:
 * the oracle's DP (oracle/fold_oracle.c) equals the Boltzmann sum over every
   secondary structure (exhaustive enumeration) -- Z and every p(i,j) -- for
-  random short sequences, with and without --noGU / --noClosingGU;
+  random short sequences, with and without --noGU / --noClosingGU /
+  --noLonelyPairs (the legacy ViennaRNA pair-type filter, restated);
 * the GPU fold equals the oracle's DP (1e-9 absolute on probabilities, 1e-12
   relative on ln Z) up to L = 400, single sequences and batches;
 * probabilities are a distribution per base (sum_j p(i,j) <= 1), and the
@@ -23,13 +24,16 @@ def _rand_seq(rng, L, alphabet="ACGU"):
     return "".join(rng.choice(list(alphabet), L))
 
 
-@pytest.mark.parametrize("flags", [(0, 0), (1, 0), (0, 1)])
+@pytest.mark.parametrize("flags", [(0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 1)])
 def test_oracle_dp_equals_enumeration(flags):
-    rng = np.random.default_rng(11 + flags[0] + 2 * flags[1])
+    """(no_gu, no_closing_gu, no_lonely_pairs); --noLonelyPairs is ViennaRNA
+    1.8's pair-type filter (oracle/fold_oracle.c lonely_filter), under which
+    the enumeration sums the structures of the filtered pairs."""
+    rng = np.random.default_rng(11 + flags[0] + 2 * flags[1] + 4 * flags[2])
     for _ in range(25):
         s = _rand_seq(rng, int(rng.integers(6, 17)))
-        a, pa = po.fold_mccaskill(s, *flags)
-        b, pb, cnt = po.fold_enum(s, *flags)
+        a, pa = po.fold_mccaskill(s, flags[0], flags[1], no_lp=bool(flags[2]))
+        b, pb, cnt = po.fold_enum(s, flags[0], flags[1], no_lp=bool(flags[2]))
         assert abs(a - b) < 1e-12 * max(1.0, abs(b)), s
         assert np.max(np.abs(pa - pb), initial=0.0) < 1e-12, s
 
@@ -115,9 +119,20 @@ def test_folded_dataset_gram(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_fold_rejects_no_lonely_pairs(gpu_ctx):
-    import ctypes as C
-    arr = (C.c_char_p * 1)(b"GGGAAACCC")
-    out = np.zeros(36)
-    rc = ska.lib().sk_fold_mccaskill(gpu_ctx.handle, 1, arr, 4, out.ctypes.data_as(C.POINTER(C.c_double)), None)
-    assert rc == -6
+@pytest.mark.parametrize("no_gu", [False, True])
+def test_gpu_fold_no_lonely_pairs(gpu_ctx, no_gu):
+    """--noLonelyPairs: the GPU fold equals the restatement with the same
+    pair-type filter (which equals enumeration, test above); short ones
+    against the enumeration directly, and the filter changes the result."""
+    rng = np.random.default_rng(404 + no_gu)
+    seqs = [_rand_seq(rng, L) for L in (5, 9, 14, 17, 40, 75, 128, 200, 301)]
+    got, lz = gpu_ctx.fold(seqs, no_gu=no_gu, log_z=True, no_lonely_pairs=True)
+    plain = gpu_ctx.fold(seqs, no_gu=no_gu)
+    for s, p, z, q in zip(seqs, got, lz, plain):
+        ref_z, ref_p = po.fold_mccaskill(s, no_gu, False, no_lp=True)
+        assert abs(z - ref_z) <= 1e-12 * max(1.0, abs(ref_z)), (len(s), z, ref_z)
+        assert np.max(np.abs(p - ref_p), initial=0.0) < 1e-9, len(s)
+        if len(s) <= 17:
+            b, pb, _ = po.fold_enum(s, no_gu, False, no_lp=True)
+            assert abs(z - b) < 1e-12 * max(1.0, abs(b)) and np.max(np.abs(p - pb), initial=0.0) < 1e-12
+    assert any(np.max(np.abs(p - q)) > 1e-6 for p, q in zip(got[4:], plain[4:]))

@@ -10,3 +10,7 @@ timeout -k 10 300 python3 -u bench.py --config c3 > $OUT/c3_col.log 2>&1 || { ta
 line $OUT/c3_col.log "c3 col"
 SK4_NO_COL=1 timeout -k 10 300 python3 -u bench.py --config c3 --no-cpu-baseline > $OUT/c3_pre.log 2>&1 || { tail -20 $OUT/c3_pre.log; exit 1; }
 line $OUT/c3_pre.log "c3 pre"
+timeout -k 10 400 python3 -u bench.py --config ns --no-cpu-baseline > $OUT/ns_async.log 2>&1 || { tail -20 $OUT/ns_async.log; exit 1; }
+line $OUT/ns_async.log "ns async"
+timeout -k 10 400 python3 -u bench.py --config ns --no-cpu-baseline --sync > $OUT/ns_sync.log 2>&1 || { tail -20 $OUT/ns_sync.log; exit 1; }
+line $OUT/ns_sync.log "ns sync"
