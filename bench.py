@@ -148,8 +148,9 @@ def components(kern):
     kernel (StringKernel) with the composition's own parameters, so each DP is
     checked on its own -- in a plain sum the stem term is invisible."""
     import stem_kernel_amd as ska
+    from stem_kernel_amd import _lib
     p = kern.params
-    if p.kind in (ska.SU_STEM_STR, ska.LSU_STEM_STR):
+    if p.kind in (_lib.SU_STEM_STR, _lib.LSU_STEM_STR):
         return {"stem": ska.SuStemKernel(loop_gap=p.loop_gap, beta=p.beta, len_band=p.len_band),
                 "string": ska.StringKernel(gap=p.gap, alpha=p.alpha)}
     return {}
@@ -161,10 +162,10 @@ def compose(kind, p, stem, string):
     in oracle/pyoracle.py kernel_value's operation order."""
     import math
 
-    import stem_kernel_amd as ska
-    if kind == ska.SU_STEM_STR:
+    from stem_kernel_amd import _lib
+    if kind == _lib.SU_STEM_STR:
         return stem + string
-    if kind == ska.LSU_STEM_STR:
+    if kind == _lib.LSU_STEM_STR:
         return (p.beta * math.log(stem) + 0.0) + (p.alpha * math.log(string) + 0.0)
     raise ValueError(kind)
 
