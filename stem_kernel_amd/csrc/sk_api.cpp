@@ -523,7 +523,11 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     return !is_gamma(X, v);
   };
   std::vector<uint64_t> phi_raw;  // child gamma key:32 | code:16 | len:16 (sorted: by child key)
-  const int nthr = (int)std::max<size_t>(1, std::min<size_t>({(size_t)n / 8 + 1, (size_t)16,
+  // host threads of the packing passes (SK_PACK_THREADS caps them: the
+  // packed arrays do not depend on it, tests/test_pack_threads.py)
+  const size_t pcap = std::getenv("SK_PACK_THREADS") ? (size_t)std::max(1, std::atoi(std::getenv("SK_PACK_THREADS")))
+                                                     : (size_t)16;
+  const int nthr = (int)std::max<size_t>(1, std::min<size_t>({(size_t)n / 8 + 1, pcap,
                                                               (size_t)std::max(1u, std::thread::hardware_concurrency())}));
   {  // every example's keys (host threads, one slice each), then one sorted set
     std::vector<std::vector<uint32_t>> tk(nthr);
@@ -1301,7 +1305,7 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
   const double tp2 = tnow();
   {
     std::vector<YOut> yo(yjobs.size());
-    const int nthr = (int)std::max<size_t>(1, std::min<size_t>({yjobs.size() / 8 + 1, (size_t)16,
+    const int nthr = (int)std::max<size_t>(1, std::min<size_t>({yjobs.size() / 8 + 1, pcap,
                                                                 (size_t)std::max(1u, std::thread::hardware_concurrency())}));
     std::atomic<size_t> next{0};
     auto work = [&]() {
