@@ -805,8 +805,9 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      land during the sweep; this row itself, when a child of the next,
     //      is added from registers in D.
     // rows prefetched per row: two where the register budget allows
-    constexpr int NPF = ((MAXK <= 12 && SK_NPF12 == 2) || (MAXK == 16 && SK_NPF16 == 2) ||
-                         (MAXK == 20 && SK_W20 == 8 && SK_NPF20 == 2)) ? 2 : 1;
+    constexpr int NPF = (MAXK == 16 && SK_NPF16 == 0) ? 0
+                        : ((MAXK <= 12 && SK_NPF12 == 2) || (MAXK == 16 && SK_NPF16 == 2) ||
+                           (MAXK == 20 && SK_W20 == 8 && SK_NPF20 == 2)) ? 2 : 1;
     uint32_t nxt_done = 0;
     double egd = 0.0, egt0 = 0.0, egt1 = 0.0;
     double T0[MAXK], T1[MAXK];
@@ -837,7 +838,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
           }
         }
       }
-      if (npf >= 1) {
+      if (NPF >= 1 && npf >= 1) {
         const __amdgpu_buffer_rsrc_t r0 = row_rsrc(child_row(pf0, slab, gamtab, phitab, stride), NLy);
 #pragma unroll
         for (int k = 0; k < MAXK; ++k) T0[k] = row_ld(r0, lane, k);

@@ -13,4 +13,5 @@ run c3_pre SK4_NO_COL=1 python3 -u bench.py --config c3 --no-cpu-baseline
 run ns_async python3 -u bench.py --config ns
 run ns_sync python3 -u bench.py --config ns --no-cpu-baseline --sync
 run ns_w12 SK_LIB_PATH=$PWD/build/libsk_w12.so python3 -u bench.py --config ns --no-cpu-baseline
+run ns_w12n SK_LIB_PATH=$PWD/build/libsk_w12n.so python3 -u bench.py --config ns --no-cpu-baseline
 run c2 python3 -u bench.py --config c2 --no-cpu-baseline
