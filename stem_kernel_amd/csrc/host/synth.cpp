@@ -43,49 +43,65 @@ void fold_nussinov(const char* seq, int n, bool no_gu, double* out) {
   if (n < 2) return;
   const double s = 2.0, inv_s = 1.0 / s, inv_s2 = inv_s * inv_s;
   const int hp = 3;
-  // Q(i,j) for 0<=i<=j<n; empty spans (j=i-1) are 1.
+  // Q(i,j) for 0<=i<=j<n; empty spans (j=i-1) are 1.  Q is kept in both
+  // layouts (QT[j][i] = Q[i][j]) and B, P transposed, so every k loop below
+  // walks memory contiguously; each value is formed by the same operations
+  // in the same order as the row-major loops (bit-identical output).
   auto at = [n](int i, int j) { return (size_t)i * n + j; };
   // per-thread workspace: repeated folds reuse already-faulted pages
-  thread_local std::vector<double> Q, O, B, P;
+  thread_local std::vector<double> Q, QT, O, BT, PT;
   Q.assign((size_t)n * n, 0.0);
+  QT.assign((size_t)n * n, 0.0);
   O.assign((size_t)n * n, 0.0);
-  B.assign((size_t)n * n, 0.0);
+  BT.assign((size_t)n * n, 0.0);  // BT[j][k] = B(k, j)
   auto q = [&](int i, int j) -> double { return j < i ? 1.0 : Q[at(i, j)]; };
   for (int i = 0; i < n; ++i)
-    for (int j = i + hp + 1; j < n; ++j) B[at(i, j)] = pair_weight(seq[i], seq[j], no_gu) * inv_s2;
+    for (int j = i + hp + 1; j < n; ++j) BT[at(j, i)] = pair_weight(seq[i], seq[j], no_gu) * inv_s2;
   for (int d = 0; d < n; ++d) {
     for (int i = 0; i + d < n; ++i) {
-      int j = i + d;
+      const int j = i + d;
       double v = q(i, j - 1) * inv_s;
-      for (int k = i; k <= j - hp - 1; ++k) {
-        double b = B[at(k, j)];
-        if (b != 0.0) v += q(i, k - 1) * b * q(k + 1, j - 1);
-      }
+      const double* __restrict__ bj = &BT[at(j, 0)];
+      const double* __restrict__ qi = &Q[at(i, 0)];
+      const double* __restrict__ qtj = &QT[at(j - 1 >= 0 ? j - 1 : 0, 0)];
+      // k = i (left span empty), then the rest; a pair that cannot form
+      // adds an exact +0 (v > 0), so no branch is needed on b
+      // (inner = q(k+1, j-1) always has k+1 <= j-3)
+      if (i <= j - hp - 1) v += 1.0 * bj[i] * qtj[i + 1];
+      for (int k = i + 1; k <= j - hp - 1; ++k) v += qi[k - 1] * bj[k] * qtj[k + 1];
       Q[at(i, j)] = v;
+      QT[at(j, i)] = v;
     }
   }
   const double Z = Q[at(0, n - 1)];
   O[at(0, n - 1)] = 1.0;
-  P.assign((size_t)n * n, 0.0);
+  PT.assign((size_t)n * n, 0.0);  // PT[j][k] = P(k, j)
   for (int d = n - 1; d >= 0; --d) {
     for (int i = 0; i + d < n; ++i) {
-      int j = i + d;
-      double o = O[at(i, j)];
+      const int j = i + d;
+      const double o = O[at(i, j)];
       if (o == 0.0) continue;
       if (j - 1 >= i) O[at(i, j - 1)] += o * inv_s;
+      const double* __restrict__ bj = &BT[at(j, 0)];
+      const double* __restrict__ qi = &Q[at(i, 0)];
+      const double* __restrict__ qtj = &QT[at(j - 1 >= 0 ? j - 1 : 0, 0)];
+      double* __restrict__ pj = &PT[at(j, 0)];
+      // (every term of a pair that cannot form is an exact +0: no branch;
+      // inner = q(k+1, j-1) always has k+1 <= j-3)
+      double* __restrict__ oi = &O[at(i, 0)];
       for (int k = i; k <= j - hp - 1; ++k) {
-        double b = B[at(k, j)];
-        if (b == 0.0) continue;
-        double left = q(i, k - 1), inner = q(k + 1, j - 1);
-        if (k - 1 >= i) O[at(i, k - 1)] += o * b * inner;
+        const double b = bj[k];
+        const double left = k - 1 >= i ? qi[k - 1] : 1.0;
+        const double inner = qtj[k + 1];
+        if (k - 1 >= i) oi[k - 1] += o * b * inner;
         O[at(k + 1, j - 1)] += o * b * left;
-        P[at(k, j)] += o * left * b * inner;
+        pj[k] += o * left * b * inner;
       }
     }
   }
   size_t t = 0;
   for (int i = 0; i < n; ++i)
-    for (int j = i + 1; j < n; ++j) out[t++] = P[at(i, j)] / Z;
+    for (int j = i + 1; j < n; ++j) out[t++] = PT[at(j, i)] / Z;
 }
 
 void random_sequence(uint64_t& state, int len, char* out) {

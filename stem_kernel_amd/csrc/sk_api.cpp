@@ -406,12 +406,12 @@ int fail(sk_context* ctx, int code, const std::string& msg) {
 // the emptiest slots.
 static void assign_sweep_lanes(const std::vector<int>& take, const std::vector<uint32_t>& er, int nl,
                                uint32_t lanes[64]) {
-  int n = (int)take.size();
-  std::vector<int> cntp(n, 0);
+  const int n = (int)take.size();  // <= 64: fixed arrays, no allocation per chunk
+  int cntp[64];
   {
-    std::vector<std::pair<uint32_t, int>> pp(n);
+    std::pair<uint32_t, int> pp[64];
     for (int i = 0; i < n; ++i) pp[i] = {(er[take[i]] >> 11) & 0x7ff, i};
-    std::sort(pp.begin(), pp.end());
+    std::sort(pp, pp + n);
     for (int a = 0; a < n;) {
       int b = a;
       while (b < n && pp[b].first == pp[a].first) ++b;
@@ -419,9 +419,9 @@ static void assign_sweep_lanes(const std::vector<int>& take, const std::vector<u
       a = b;
     }
   }
-  std::vector<int> ord(n);
-  std::iota(ord.begin(), ord.end(), 0);
-  std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cntp[a] > cntp[b]; });
+  int ord[64];
+  std::iota(ord, ord + n, 0);
+  std::stable_sort(ord, ord + n, [&](int a, int b) { return cntp[a] > cntp[b]; });
   int fill[4] = {0, 0, 0, 0};
   int at[4][16];         // group -> parent slot load
   uint32_t rd[2][32][4];  // half -> child slot -> distinct children (up to 4 kept)
@@ -446,7 +446,8 @@ static void assign_sweep_lanes(const std::vector<int>& take, const std::vector<u
     at[g][q & 15]++;
     lanes[16 * g + fill[g]++] = r;
   };
-  for (int i : ord) {
+  for (int oi = 0; oi < n; ++oi) {
+    const int i = ord[oi];
     const uint32_t r = er[take[i]];
     const uint32_t c = r & 0x7ff, q = (r >> 11) & 0x7ff;
     int best = -1, bc = 1 << 30;
@@ -632,31 +633,38 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
       } else {
         std::vector<uint32_t> er;       // records child:11 | parent:11 | gaps:10
         std::vector<int> epar, ech;
-        std::vector<std::vector<int>> by_child(nl), parents(nl);
         for (int k = 0; k < nl; ++k) {
           const uint32_t a = P.nd_a[nb0 + k];
           const uint32_t ne = (a >> 16) & 0xff, el = a & 0xffff;
           for (uint32_t t = 0; t < ne; ++t) {
             const uint2 rec = P.ed[ebase + el + t];  // {child | gaps<<16, parent}
             const int c = pos[rec.x & 0xffff], q = pos[k];
-            by_child[c].push_back((int)er.size());
-            parents[c].push_back(q);
             epar.push_back(q);
             ech.push_back(c);
             er.push_back((uint32_t)c | ((uint32_t)q << 11) | ((rec.x >> 16) << 22));
           }
         }
         const int ne_all = (int)er.size();
+        // a child's edges in edge order (CSR: one allocation, not one per node)
+        std::vector<int> cb(nl + 1, 0), by_child(ne_all);
+        for (int f = 0; f < ne_all; ++f) cb[ech[f] + 1]++;
+        for (int i = 0; i < nl; ++i) cb[i + 1] += cb[i];
+        {
+          std::vector<int> fillc(cb.begin(), cb.end() - 1);
+          for (int f = 0; f < ne_all; ++f) by_child[fillc[ech[f]]++] = f;
+        }
         // sorted ids: a parent is strictly longer, so it has a larger id
         std::vector<int> h(nl, 0), rem(nl, 0);
         for (int i = nl - 1; i >= 0; --i)
-          for (int q : parents[i]) h[i] = std::max(h[i], h[q] + 1);
+          for (int t = cb[i]; t < cb[i + 1]; ++t) h[i] = std::max(h[i], h[epar[by_child[t]]] + 1);
         for (int f = 0; f < ne_all; ++f) rem[epar[f]]++;
         typedef std::pair<std::pair<int, int>, int> Key;  // {{-height, child len}, edge}
         std::priority_queue<Key, std::vector<Key>, std::greater<Key>> ready;
         auto push_edges_of = [&](int c) {
-          for (int f : by_child[c])
+          for (int t = cb[c]; t < cb[c + 1]; ++t) {
+            const int f = by_child[t];
             ready.push({{-h[epar[f]], (int)(P.nd_b[nb0 + srt[c]] & 0xffff)}, f});
+          }
         };
         for (int c = 0; c < nl; ++c)
           if (rem[c] == 0) push_edges_of(c);
