@@ -182,10 +182,12 @@ def dag_bytes(shapes, x, y):
 def col_waves(lens, y):
     """Waves per pair of the 4-D column kernel, as run_stem4d picks them for a
     batch: the class's register budget (CPL 1-2: 16, 4: 12, 8: 8), at most
-    m - 2 (the smallest y of the batch; one batch per bench step)."""
+    m - F - 1 (the smallest y of the batch; F = 8 steps between full
+    barriers, 1 for short y; one batch per bench step)."""
     m = lens[y]
     cpl = 1 if m.max() + 1 <= 64 else 2 if m.max() + 1 <= 128 else 4 if m.max() + 1 <= 256 else 8
-    return int(max(1, min({1: 16, 2: 16, 4: 12, 8: 8}[cpl], int(m.min()) - 2)))
+    F = 8 if int(m.min()) - 9 >= 4 else 1
+    return int(max(1, min({1: 16, 2: 16, 4: 12, 8: 8}[cpl], int(m.min()) - F - 1)))
 
 
 def stem4d_cells(lens, x, y):

@@ -233,6 +233,8 @@ struct Stem4dLaunch {
   // the ring; 0 = the four-state planes; 2 = the same planes with each plane's
   // G1 pre-combined by the plane (i+1, j) (sk_stem4d_pre_kernel, one k tile)
   int32_t gsum = 0;
+  // column kernel: steps between full (global-memory) barriers (stem4d.hip)
+  int32_t col_f = 1;
 };
 
 int stem4d_cpl(int m);

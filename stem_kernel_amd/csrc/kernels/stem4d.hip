@@ -790,15 +790,23 @@ __global__ void __launch_bounds__(256) sk_stem4d_pre_kernel(Stem4dLaunch P) {
 // K = 1 + the waves' lane-reduced sums in wave order.
 constexpr int SK4C_PF = 2;
 
-__device__ __forceinline__ int s4c_cols(int j) { return j > SK4C_PF + 1 ? j : SK4C_PF + 1; }
+// Barriers: between steps only the LDS B' rows need to be visible, so most
+// barriers wait for LDS traffic alone (lgkmcnt) -- a workgroup release of
+// global memory would wait for every outstanding vector memory op (vmcnt:
+// the prefetched rows too), i.e. pay the HBM latency every step.  Every F-th
+// barrier (P.col_f; the one before step t, t % F == 0) is a full one, so a
+// global store of step u is visible from the first multiple of F above u
+// on: readers of global data need a lag of F + PF steps -- column j holds
+// c_j = max(j, F + 2) positions, and W <= m - F - 1 (the round wrap).
+__device__ __forceinline__ int s4c_cols(int j, int F) { return j > F + SK4C_PF ? j : F + SK4C_PF; }
 
 // position -> plane of the column schedule; advance() moves on by W positions
 struct S4cPos {
   int j = 1, off = 0;  // column, offset in the column (i = j - 1 - off; off >= j: bubble)
-  __device__ void advance(int W, int n) {
+  __device__ void advance(int W, int n, int F) {
     off += W;
-    while (j <= n && off >= s4c_cols(j)) {
-      off -= s4c_cols(j);
+    while (j <= n && off >= s4c_cols(j, F)) {
+      off -= s4c_cols(j, F);
       ++j;
     }
   }
@@ -832,6 +840,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   const double* gpow = P.gpow;
   const float bound = P.bp_bound;
   const double g = P.gap, stk = P.stack, sub = P.subst;
+  const int F = max(P.col_f, 1);
   // links: wave w writes link w (slot t & 1), wave w+1 reads it a step later
   double* link_out = s4c_lds + (int64_t)w * 2 * TW;
   const double* link_in = s4c_lds + (int64_t)(w - 1) * 2 * TW;
@@ -839,7 +848,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
 
   // steps: T(last position) + R
   int64_t np = 0;
-  for (int j = 1; j <= n; ++j) np += s4c_cols(j);
+  for (int j = 1; j <= n; ++j) np += s4c_cols(j, F);
   const int64_t total = np > 0 ? ((np - 1) / W) * R + (np - 1) % W + R : 0;
 
   // per-plane constants of the plane at a position
@@ -912,7 +921,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
 
   // this wave's position (p = w) and the fetch cursor PF rows ahead
   S4cPos cur;
-  cur.advance(w, n);  // from position 0
+  cur.advance(w, n, F);  // from position 0
   Plane dc = describe(cur);
   S4cPos fpos = cur;
   Plane df = dc;
@@ -922,7 +931,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     fetch(r, df, fs);
     if (++fs == R) {
       fs = 0;
-      fpos.advance(W, n);
+      fpos.advance(W, n, F);
       df = describe(fpos);
     }
   };
@@ -933,8 +942,16 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   int s = 0;
 
   for (int64_t t = 0; t < total; ++t) {
-    if (t > 0) __syncthreads();
-    if (!cur.valid(n)) continue;  // (every wave takes every barrier)
+    if (t > 0) {  // (every wave takes every barrier)
+      if (t % F == 0) {
+        __syncthreads();
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      }
+    }
+    if (!cur.valid(n)) continue;
     if (t < w) {
       if (t == w - 2) fetch_next(r0);
       if (t == w - 1) fetch_next(r1);
@@ -1010,7 +1027,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     }
     if (++s == R) {
       s = 0;
-      cur.advance(W, n);
+      cur.advance(W, n, F);
       dc = describe(cur);
     }
   }

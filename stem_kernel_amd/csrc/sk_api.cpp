@@ -1843,7 +1843,10 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       // (the schedule's R >= W + PF + 1) and the class's register budget
       int min_m = INT32_MAX;
       for (const auto& p : prs) min_m = std::min(min_m, p.m);
-      const int W = std::max(1, std::min(sk::stem4d_col_max_waves(cpl), min_m - 2));
+      // W <= m - F - 1 (the round wrap's lag, stem4d.hip); full barriers every
+      // F = 8 steps where the y's are long enough, else every step
+      const int F = min_m - 9 >= 4 ? 8 : 1;
+      const int W = std::max(1, std::min(sk::stem4d_col_max_waves(cpl), min_m - F - 1));
       rc = ensure_scratch(ctx, ring_bytes + 64);
       if (rc) return rc;
       if (Bt.cap_pairs < prs.size()) {
@@ -1868,6 +1871,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       L.bp_bound = (float)kp->bp_bound;
       L.out = out_dev;
       L.gsum = 3;
+      L.col_f = F;
       SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
       SK_HIP(ctx, sk::lev_mark(ctx, S));
       SK_HIP(ctx, sk::launch_stem4d_col(L, (int64_t)prs.size(), cpl, W, S));

@@ -17,18 +17,18 @@ from oracle import pyoracle as po
 PF = 2
 
 
-def cols(j):
-    return max(j, PF + 1)
+def cols(j, F):
+    return max(j, F + PF)
 
 
 class Pos:
     def __init__(self):
         self.j, self.off = 1, 0
 
-    def advance(self, W, n):
+    def advance(self, W, n, F):
         self.off += W
-        while self.j <= n and self.off >= cols(self.j):
-            self.off -= cols(self.j)
+        while self.j <= n and self.off >= cols(self.j, F):
+            self.off -= cols(self.j, F)
             self.j += 1
 
     def copy(self):
@@ -57,7 +57,9 @@ def bpdiag(seq, bpp):
     return np.array(out, np.float32)
 
 
-def emulate(x, bx, y, by, W, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None):
+def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None):
+    """F: steps between full barriers -- a global store of step u is seen
+    from the first multiple of F above u on; LDS stores from the next step."""
     n, m = len(x), len(y)
     R = m + 1
     TW = 64 * (CPL or max(1, -(-(m + 1) // 64)))
@@ -70,7 +72,7 @@ def emulate(x, bx, y, by, W, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None)
     bpx, bpy = bpdiag(x, bx), bpdiag(y, by)
     cp = row_off(m, m + 1)
     mem = {"planes": np.full(max(n, 1) * cp + cp, np.nan), "lds": np.full((W, 2, TW), np.nan)}
-    np_ = sum(cols(j) for j in range(1, n + 1))
+    np_ = sum(cols(j, F) for j in range(1, n + 1))
     total = ((np_ - 1) // W) * R + (np_ - 1) % W + R if np_ else 0
     k = np.arange(TW)
     yk = np.array([y[kk] if kk < m else "\0" for kk in k])
@@ -95,7 +97,7 @@ def emulate(x, bx, y, by, W, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None)
     for w in range(W):
         v = Wave()
         v.cur = Pos()
-        v.cur.advance(w, n)
+        v.cur.advance(w, n, F)
         v.dc = describe(v.cur)
         v.fpos, v.df, v.fs = v.cur.copy(), dict(v.dc), 0
         v.rows = []
@@ -127,7 +129,7 @@ def emulate(x, bx, y, by, W, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None)
         v.fs += 1
         if v.fs == R:
             v.fs = 0
-            v.fpos.advance(W, n)
+            v.fpos.advance(W, n, F)
             v.df = describe(v.fpos)
         return r
 
@@ -139,7 +141,16 @@ def emulate(x, bx, y, by, W, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None)
     snap = {kk: vv.copy() for kk, vv in mem.items()}
     for v_i, v in enumerate(waves):  # first rows: PF steps before the wave's first step
         v.rows = [fetch(v, snap, v_i) for _ in range(max(0, PF - v_i))]
+    pending = []  # global stores not yet visible: (first visible step, index, values)
     for t in range(total):
+        # global stores become visible at the full barriers (before steps t % F == 0)
+        keep = []
+        for vis, idx, val in pending:
+            if vis <= t:
+                mem["planes"][idx] = val
+            else:
+                keep.append((vis, idx, val))
+        pending = keep
         snap = {kk: vv.copy() for kk, vv in mem.items()}
         writes = []
         for w, v in enumerate(waves):
@@ -193,16 +204,20 @@ def emulate(x, bx, y, by, W, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None)
             v.s += 1
             if v.s == R:
                 v.s = 0
-                v.cur.advance(W, n)
+                v.cur.advance(W, n, F)
                 v.dc = describe(v.cur)
         for name, idx, val in writes:
-            mem[name][idx] = val
+            if name == "lds":
+                mem[name][idx] = val
+            else:
+                pending.append(((t // F + 1) * F, idx, val))
     return 1.0 + sum(float(v.ksrc.sum()) for v in waves)
 
 
-@pytest.mark.parametrize("n,m,W", [(9, 11, 3), (12, 7, 5), (6, 14, 12), (1, 5, 3), (0, 6, 2),
-                                   (10, 4, 2), (7, 9, 1), (13, 13, 11)])
-def test_column_schedule_equals_oracle(n, m, W):
+@pytest.mark.parametrize("n,m,W,F", [(9, 11, 3, 1), (12, 7, 5, 1), (6, 14, 12, 1), (1, 5, 3, 1),
+                                     (0, 6, 2, 1), (10, 4, 2, 1), (7, 9, 1, 1), (13, 13, 11, 1),
+                                     (12, 17, 4, 8), (10, 21, 12, 8), (16, 13, 4, 8), (5, 30, 12, 8)])
+def test_column_schedule_equals_oracle(n, m, W, F):
     seqs = ska.random_sequences(2, max(n, m, 1), 0x5EED0C01 + n * 31 + m)
     x, y = seqs[0][:n].lower(), seqs[1][:m].lower()
     # dense base-pair probabilities (every cell a stacking source), so that any
@@ -210,8 +225,8 @@ def test_column_schedule_equals_oracle(n, m, W):
     rng = np.random.default_rng(n * 1000 + m)
     bx = rng.uniform(0.05, 0.6, n * (n - 1) // 2)
     by = rng.uniform(0.05, 0.6, m * (m - 1) // 2)
-    assert W <= max(1, m - 2)  # the host's limit (R >= W + PF + 1)
-    got = emulate(x, bx, y, by, W)
+    assert W <= max(1, m - F - 1)  # the host's limit (the round wrap's lag)
+    got = emulate(x, bx, y, by, W, F)
     f = lambda v: float(np.float32(v))  # the CLI's float options, as StemKernel4D rounds them
     ref = po.stem4d(x, bx, y, by, f(0.8), f(1.0), f(0.5), 0.0)
     assert abs(got - ref) <= 1e-12 * abs(ref), (got, ref)
@@ -228,3 +243,5 @@ def test_emulation_sees_a_broken_schedule():
     assert abs(emulate(x, bx, y, by, 9) - ref) <= 1e-12 * ref
     bad = emulate(x, bx, y, by, 11)
     assert not abs(bad - ref) <= 1e-12 * ref
+    # with full barriers every F = 8 steps, W = m - 2 is past the limit m - F - 1
+    assert not abs(emulate(x, bx, y, by, 9, F=8) - ref) <= 1e-12 * ref
