@@ -197,6 +197,13 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_NODEW_MIN  // the narrowest class whose sweep weights are per node (LDS for waves)
 #define SK_NODEW_MIN 20
 #endif
+#ifndef SK_M16  // the MAXK 16 class: 0 = 8 waves; 1 = 12 waves (3 per SIMD: phases A / D in
+#define SK_M16 0  // halves, 128-node MATCH passes, per-node sweep weights); 2 = 1 without the
+#endif            // prefetched child row
+template <int MAXK>
+constexpr bool m16_wide() {
+  return MAXK == 16 && SK_M16 != 0;
+}
 // Sweep weights per y node (gap^2 w(q), 8 B per node; the widest classes
 // w(q) itself, the float, 4 B) instead of per schedule slot (8 B per slot of
 // (nch + 2) x 64): a third of the schedule's LDS, for one more LDS read per
@@ -206,7 +213,7 @@ __device__ __forceinline__ void wave_sync() {
 // trade; MAXK 16 holds 8 waves either way (VGPRs).
 template <int MAXK>
 constexpr bool node_weights() {
-  return MAXK >= SK_NODEW_MIN;
+  return MAXK >= SK_NODEW_MIN || m16_wide<MAXK>();
 }
 #ifndef SK_NODEF_MIN  // the narrowest class whose node weights are the floats w(q)
 #define SK_NODEF_MIN 24
@@ -222,8 +229,11 @@ constexpr bool node_weights_f32() {
 // per-wave accumulator is 64 * PW doubles of LDS)
 template <int MAXK>
 constexpr int pass_width() {
-  return MAXK >= SK_PW2_MIN ? 2 : SK_PW;
+  return (MAXK >= SK_PW2_MIN || m16_wide<MAXK>()) ? 2 : SK_PW;
 }
+// host mirror of pass_width (stem_lds_bytes)
+static inline int pass_width_of(int maxk) { return (maxk >= SK_PW2_MIN || (maxk == 16 && SK_M16 != 0)) ? 2 : SK_PW; }
+static inline bool node_weights_of(int maxk) { return maxk >= SK_NODEW_MIN || (maxk == 16 && SK_M16 != 0); }
 #ifndef SK_EDG_MIN  // the narrowest class whose MATCH reads the node-major edges from L2, not LDS
 #define SK_EDG_MIN 64  // off: C5 100.7k against 102.3k pairs/s (r03 A/B; MATCH 14.4k against 9.9k cycles per row)
 #endif
@@ -311,7 +321,7 @@ template <int MAXK>
 __device__ __forceinline__ void add_rows2(double (&S)[MAXK], __amdgpu_buffer_rsrc_t r0,
                                           __amdgpu_buffer_rsrc_t r1, double eg0, double eg1,
                                           int lane) {
-  constexpr int H = MAXK > SK_HALF_A ? MAXK / 2 : MAXK;
+  constexpr int H = (MAXK > SK_HALF_A || m16_wide<MAXK>()) ? MAXK / 2 : MAXK;
 #pragma unroll
   for (int h0 = 0; h0 < MAXK; h0 += H) {
     double a[H], b[H];
@@ -805,7 +815,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      land during the sweep; this row itself, when a child of the next,
     //      is added from registers in D.
     // rows prefetched per row: two where the register budget allows
-    constexpr int NPF = (MAXK == 16 && SK_NPF16 == 0) ? 0
+    constexpr int NPF = (MAXK == 16 && (SK_NPF16 == 0 || SK_M16 == 2)) ? 0
                         : ((MAXK <= 12 && SK_NPF12 == 2) || (MAXK == 16 && SK_NPF16 == 2) ||
                            (MAXK == 20 && SK_W20 == 8 && SK_NPF20 == 2)) ? 2 : 1;
     uint32_t nxt_done = 0;
@@ -882,7 +892,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // per-thread program order makes it visible: no fence.  A row nobody
     // reads (a root) is not stored; it is no child of the next row either.
     // (the widest classes read G1 back in two halves: fewer live registers)
-    constexpr int HD = MAXK > SK_HALF_D ? MAXK / 2 : MAXK;
+    constexpr int HD = (MAXK > SK_HALF_D || m16_wide<MAXK>()) ? MAXK / 2 : MAXK;
     if (pslot == 0xffffu) {
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) S[k] = egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
@@ -950,7 +960,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 
 template <int MAXK>
 struct StemWaves {
-  static constexpr int value = MAXK <= 12 ? 12 : MAXK <= 16 ? SK_W16 : MAXK <= 20 ? SK_W20 : 8;
+  static constexpr int value = MAXK <= 12 ? 12 : MAXK <= 16 ? (SK_M16 ? 12 : SK_W16) : MAXK <= 20 ? SK_W20 : 8;
 };
 
 template <int MAXK>
@@ -1211,9 +1221,9 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   b += 256 * 8;
   b += (size_t)P.n_gpow_pad * 8;
   b += (size_t)nwaves * P.lds_max_nl * 8;          // one row per wave
-  b += (size_t)nwaves * 64 * (stem_maxk(P.lds_max_nl) >= SK_PW2_MIN ? 2 : SK_PW) * 8;  // MATCH accumulators
+  b += (size_t)nwaves * 64 * pass_width_of(stem_maxk(P.lds_max_nl)) * 8;  // MATCH accumulators
   const int maxk = stem_maxk(P.lds_max_nl);
-  if (maxk >= SK_NODEW_MIN)                        // sweep schedule: records, node weights
+  if (node_weights_of(maxk))                       // sweep schedule: records, node weights
     b += (size_t)P.lds_max_nch * 64 * 4 + (size_t)P.lds_max_nl * (maxk >= SK_NODEF_MIN ? 4 : 8);
   else                                             // sweep schedule: weights + records
     b += (size_t)P.lds_max_nch * 64 * 12;
