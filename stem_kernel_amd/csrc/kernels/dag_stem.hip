@@ -197,9 +197,14 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_NODEW_MIN  // the narrowest class whose sweep weights are per node (LDS for waves)
 #define SK_NODEW_MIN 20
 #endif
-#ifndef SK_M16  // the MAXK 16 class: 0 = 8 waves; 1 = 12 waves (3 per SIMD: phases A / D in
-#define SK_M16 0  // halves, 128-node MATCH passes, per-node sweep weights); 2 = 1 without the
-#endif            // prefetched child row
+// The MAXK 16 class: 1 = 12 waves (3 per SIMD at 168 VGPRs: phases A / D in
+// halves, 128-node MATCH passes, per-node sweep weights; 7 VGPRs spilled),
+// NS 198.1k against 190.5k pairs/s with 0 (8 waves, one prefetched child row,
+// 196 VGPRs) over two alternating rounds (r04c); 2 = 1 without the
+// prefetched row (no spills): 196.0k.
+#ifndef SK_M16
+#define SK_M16 1
+#endif
 template <int MAXK>
 constexpr bool m16_wide() {
   return MAXK == 16 && SK_M16 != 0;

@@ -788,7 +788,9 @@ __global__ void __launch_bounds__(256) sk_stem4d_pre_kernel(Stem4dLaunch P) {
 // The K chain is summed (sk_stem4d_gsum_kernel): every lane keeps one running
 // sum of its consumers' stacking sources over all its planes; the pair's
 // K = 1 + the waves' lane-reduced sums in wave order.
-constexpr int SK4C_PF = 2;
+#ifndef SK4C_PF
+#define SK4C_PF 2  // rows fetched ahead
+#endif
 
 // Barriers: between steps only the LDS B' rows need to be visible, so most
 // barriers wait for LDS traffic alone (lgkmcnt) -- a workgroup release of
@@ -816,9 +818,12 @@ struct S4cPos {
 };
 
 // waves per workgroup at most: 4, 3 and 2 per SIMD (the register budget)
+#ifndef SK4C_W4  // waves per workgroup of the CPL 4 class (12: 3 per SIMD; 16 needs SK4C_PF 1)
+#define SK4C_W4 12
+#endif
 template <int CPL>
 constexpr int s4c_max_waves() {
-  return CPL <= 2 ? 16 : CPL == 4 ? 12 : 8;
+  return CPL <= 2 ? 16 : CPL == 4 ? SK4C_W4 : 8;
 }
 
 template <int CPL>
@@ -881,7 +886,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   struct Row {
     double A[CPL], Bw[CPL];
     float bp[CPL];
-    uint8_t yl[CPL];
+    uint32_t ylm;  // bit c: y[l-1] == x[j-1] of the consumer, slot c
   };
   auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
     const int kmax = m - s;
@@ -890,30 +895,32 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
     const double* Ai = planes + (int64_t)d.i * cp + ro;
     const bool wrap_in = w == 0 && !d.first;
+    r.ylm = 0u;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = lane + 64 * c;
       r.A[c] = 0.0;
       r.Bw[c] = 0.0;
       r.bp[c] = 0.0f;
-      r.yl[c] = 0;
+
       if (d.on && s >= 1 && k <= kmax) {
         r.A[c] = d.first ? gpow[s] : Ai[k];  // G0(j-1, j-1) = g^(l-k)
         if (wrap_in) r.Bw[c] = wrapb[ro + k];
         if (d.stack) {
           r.bp[c] = bpy[ye + k];
-          r.yl[c] = ys[k + s - 1];
+          r.ylm |= (ys[k + s - 1] == d.xcj ? 1u : 0u) << c;
         }
       }
     }
   };
 
-  uint8_t yk[CPL];
+  uint32_t yk = 0;  // y[k] of slot c in byte c (CPL <= 4), else reread per plane
 #pragma unroll
-  for (int c = 0; c < CPL; ++c) {
+  for (int c = 0; c < CPL && c < 4; ++c) {
     const int k = lane + 64 * c;
-    yk[c] = k < m ? ys[k] : 0;
+    yk |= (uint32_t)(k < m ? ys[k] : 0) << (8 * c);
   }
+  uint32_t xkm = 0;  // bit c: y[k] == x[i-1] of the consumer (per plane)
   double ksrc = 0.0;
   double Am1[CPL], Am2[CPL], G2c[CPL], G3c[CPL];
 #pragma unroll
@@ -926,7 +933,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   S4cPos fpos = cur;
   Plane df = dc;
   int fs = 0;  // fetch cursor: (fpos, fs)
-  Row r0, r1;
+  Row rq[SK4C_PF];  // rows fetched ahead, oldest first
   auto fetch_next = [&](Row& r) __attribute__((always_inline)) {
     fetch(r, df, fs);
     if (++fs == R) {
@@ -937,8 +944,9 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   };
   // a wave's first rows are fetched PF steps before its first step (t = w),
   // not earlier: their A rows may be written in the steps before
-  if (w == 0) fetch_next(r0);
-  if (w <= 1) fetch_next(w == 0 ? r1 : r0);
+#pragma unroll
+  for (int q = 0; q < SK4C_PF; ++q)
+    if (w - SK4C_PF + q < 0) fetch_next(rq[q]);
   int s = 0;
 
   for (int64_t t = 0; t < total; ++t) {
@@ -953,16 +961,25 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     }
     if (!cur.valid(n)) continue;
     if (t < w) {
-      if (t == w - 2) fetch_next(r0);
-      if (t == w - 1) fetch_next(r1);
+#pragma unroll
+      for (int q = 0; q < SK4C_PF; ++q)
+        if (t == w - SK4C_PF + q) fetch_next(rq[q]);
       continue;
     }
-    const Row cr = r0;
-    r0 = r1;
-    fetch_next(r1);
+    const Row cr = rq[0];
+#pragma unroll
+    for (int q = 0; q + 1 < SK4C_PF; ++q) rq[q] = rq[q + 1];
+    fetch_next(rq[SK4C_PF - 1]);
     if (dc.on) {
       const int kmax = m - s;
       if (s == 0) {  // cells (l, l): G0 = g^(j-i), never stored; chain registers reset
+        xkm = 0u;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const int k = lane + 64 * c;
+          const uint32_t ykc = c < 4 ? (yk >> (8 * (c & 3))) & 0xffu : (k < m ? ys[k] : 0u);
+          xkm |= (dc.stack && ykc == dc.xci ? 1u : 0u) << c;
+        }
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
           const int k = lane + 64 * c;
@@ -975,17 +992,16 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
         const bool wrap_in = w == 0;
         const double* lin = link_in + ((t - 1) & 1) * TW;
         double* lout = dc.cons && w + 1 < W ? link_out + (t & 1) * TW : nullptr;
-        // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at (k+1, l-1)
-        double G3n[CPL], A2[CPL];
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
+          // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
+          // (k+1, l-1): the next lane's, or the next slot's lane 0 -- formed
+          // here, before slot c's update, while slot c+1's is still the old
+          // row's (short live ranges: the registers of 4 waves per SIMD)
           const double hg = c + 1 < CPL ? bcast_lane0(G3c[c + 1 < CPL ? c + 1 : c]) : 0.0;
           const double ha = c + 1 < CPL ? bcast_lane0(Am2[c + 1 < CPL ? c + 1 : c]) : 0.0;
-          G3n[c] = wave_shl1(G3c[c], hg);
-          A2[c] = wave_shl1(Am2[c], ha);
-        }
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
+          const double G3n = wave_shl1(G3c[c], hg);
+          const double A2 = wave_shl1(Am2[c], ha);
           const int k = lane + 64 * c;
           if (k <= kmax) {
             // this plane: G1 = B' (formed by the plane (i+1, j)), G0 (:85-111)
@@ -994,12 +1010,12 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
             G0 += G1;
             out[k] = G0;
             if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
-              double g3 = G3n[c] * g;
+              double g3 = G3n * g;
               if (dc.stack && s >= 2) {
                 const float bp_kl = cr.bp[c];
                 if (bp_kl > bound) {
-                  const double g0 = A2[c];
-                  if (dc.xci == yk[c] && dc.xcj == cr.yl[c]) {
+                  const double g0 = A2;
+                  if (((xkm & cr.ylm) >> c) & 1u) {
                     ksrc += g0 * stk * (double)dc.bp_c * (double)bp_kl;
                     g3 += g0;
                   } else {

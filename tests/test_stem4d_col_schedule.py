@@ -17,18 +17,18 @@ from oracle import pyoracle as po
 PF = 2
 
 
-def cols(j, F):
-    return max(j, F + PF)
+def cols(j, F, pf=PF):
+    return max(j, F + pf)
 
 
 class Pos:
     def __init__(self):
         self.j, self.off = 1, 0
 
-    def advance(self, W, n, F):
+    def advance(self, W, n, F, pf=PF):
         self.off += W
-        while self.j <= n and self.off >= cols(self.j, F):
-            self.off -= cols(self.j, F)
+        while self.j <= n and self.off >= cols(self.j, F, pf):
+            self.off -= cols(self.j, F, pf)
             self.j += 1
 
     def copy(self):
@@ -57,7 +57,7 @@ def bpdiag(seq, bpp):
     return np.array(out, np.float32)
 
 
-def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None):
+def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None, pf=PF):
     """F: steps between full barriers -- a global store of step u is seen
     from the first multiple of F above u on; LDS stores from the next step."""
     n, m = len(x), len(y)
@@ -72,7 +72,7 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
     bpx, bpy = bpdiag(x, bx), bpdiag(y, by)
     cp = row_off(m, m + 1)
     mem = {"planes": np.full(max(n, 1) * cp + cp, np.nan), "lds": np.full((W, 2, TW), np.nan)}
-    np_ = sum(cols(j, F) for j in range(1, n + 1))
+    np_ = sum(cols(j, F, pf) for j in range(1, n + 1))
     total = ((np_ - 1) // W) * R + (np_ - 1) % W + R if np_ else 0
     k = np.arange(TW)
     yk = np.array([y[kk] if kk < m else "\0" for kk in k])
@@ -97,7 +97,7 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
     for w in range(W):
         v = Wave()
         v.cur = Pos()
-        v.cur.advance(w, n, F)
+        v.cur.advance(w, n, F, pf)
         v.dc = describe(v.cur)
         v.fpos, v.df, v.fs = v.cur.copy(), dict(v.dc), 0
         v.rows = []
@@ -129,7 +129,7 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
         v.fs += 1
         if v.fs == R:
             v.fs = 0
-            v.fpos.advance(W, n, F)
+            v.fpos.advance(W, n, F, pf)
             v.df = describe(v.fpos)
         return r
 
@@ -140,7 +140,7 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
 
     snap = {kk: vv.copy() for kk, vv in mem.items()}
     for v_i, v in enumerate(waves):  # first rows: PF steps before the wave's first step
-        v.rows = [fetch(v, snap, v_i) for _ in range(max(0, PF - v_i))]
+        v.rows = [fetch(v, snap, v_i) for _ in range(max(0, pf - v_i))]
     pending = []  # global stores not yet visible: (first visible step, index, values)
     for t in range(total):
         # global stores become visible at the full barriers (before steps t % F == 0)
@@ -157,7 +157,7 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
             if not v.cur.j <= n:
                 continue
             if t < w:
-                if t >= w - PF:
+                if t >= w - pf:
                     v.rows.append(fetch(v, snap, w))
                 continue
             cr = v.rows.pop(0)
@@ -204,7 +204,7 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
             v.s += 1
             if v.s == R:
                 v.s = 0
-                v.cur.advance(W, n, F)
+                v.cur.advance(W, n, F, pf)
                 v.dc = describe(v.cur)
         for name, idx, val in writes:
             if name == "lds":
@@ -217,7 +217,8 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
 @pytest.mark.parametrize("n,m,W,F", [(9, 11, 3, 1), (12, 7, 5, 1), (6, 14, 12, 1), (1, 5, 3, 1),
                                      (0, 6, 2, 1), (10, 4, 2, 1), (7, 9, 1, 1), (13, 13, 11, 1),
                                      (12, 17, 4, 8), (10, 21, 12, 8), (16, 13, 4, 8), (5, 30, 12, 8)])
-def test_column_schedule_equals_oracle(n, m, W, F):
+@pytest.mark.parametrize("pf", [2, 1])
+def test_column_schedule_equals_oracle(n, m, W, F, pf):
     seqs = ska.random_sequences(2, max(n, m, 1), 0x5EED0C01 + n * 31 + m)
     x, y = seqs[0][:n].lower(), seqs[1][:m].lower()
     # dense base-pair probabilities (every cell a stacking source), so that any
@@ -226,7 +227,7 @@ def test_column_schedule_equals_oracle(n, m, W, F):
     bx = rng.uniform(0.05, 0.6, n * (n - 1) // 2)
     by = rng.uniform(0.05, 0.6, m * (m - 1) // 2)
     assert W <= max(1, m - F - 1)  # the host's limit (the round wrap's lag)
-    got = emulate(x, bx, y, by, W, F)
+    got = emulate(x, bx, y, by, W, F, pf=pf)
     f = lambda v: float(np.float32(v))  # the CLI's float options, as StemKernel4D rounds them
     ref = po.stem4d(x, bx, y, by, f(0.8), f(1.0), f(0.5), 0.0)
     assert abs(got - ref) <= 1e-12 * abs(ref), (got, ref)
