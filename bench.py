@@ -73,7 +73,12 @@ CONFIGS = {
     # slice whose launch fill and tail would dominate ("whole": steps repeat it)
     "c2": dict(kernel="ss", n=256, L=150, slices=1, whole=True, cid=1, cpu_pairs=12288),
     "c3": dict(kernel="stem4d", n=1024, L=200, slices=2050, cid=2, cpu_pairs=32),
-    "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=16, cid=3, cpu_pairs=196608),
+    # async: step t+1 planned while step t runs (sk_set_async): C4 +3.6 % (its
+    # 7 ms steps had 0.6-0.9 ms host gaps); the DAG configs gain <1 % and
+    # their two concurrent class launches would then overlap fully, which
+    # doubles each launch's duration (the per-launch roofline) -- kept
+    # synchronous
+    "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=16, cid=3, cpu_pairs=196608, async_calls=True),
     "c5": dict(kernel="stem", n=8192, L=300, slices=128, cid=4, cpu_pairs=4096),
 }
 
@@ -88,8 +93,9 @@ def parse():
     ap.add_argument("--length", type=int, default=None)
     ap.add_argument("--slices", type=int, default=None)
     ap.add_argument("--full", action="store_true", help="time every slice (whole Gram)")
-    ap.add_argument("--sync", action="store_true",
-                    help="synchronous compute calls (default: sk_set_async, step t+1 planned while step t runs)")
+    ap.add_argument("--sync", action="store_true", help="synchronous compute calls for every config")
+    ap.add_argument("--async", dest="async_calls", action="store_true",
+                    help="asynchronous compute calls (sk_set_async) for every config (default: C4 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-pairs", type=int, default=None, help="pairs in the CPU sample")
     ap.add_argument("--pmc-json", default=None, help="traffic profile (default profiles/<kind>_traffic.json)")
@@ -496,7 +502,7 @@ class GpuEngine:
         self.kern = make_kernel(cfg["kernel"], cfg.get("cls"))
         # asynchronous calls: the host plans step t+1 while the GPU runs step
         # t; timings are collected over the timed steps (totals())
-        self.async_on = not a.sync
+        self.async_on = not a.sync and bool(a.async_calls or cfg.get("async_calls"))
         self.ctx.set_async(self.async_on)
         if self.dist_on:
             shard.rccl_init(self.ctx)
