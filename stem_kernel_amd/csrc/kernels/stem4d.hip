@@ -800,6 +800,41 @@ __global__ void __launch_bounds__(256) sk_stem4d_pre_kernel(Stem4dLaunch P) {
 // global store of step u is visible from the first multiple of F above u
 // on: readers of global data need a lag of F + PF steps -- column j holds
 // c_j = max(j, F + 2) positions, and W <= m - F - 1 (the round wrap).
+//
+// Between the full barriers the waves need not run in lockstep (SK4C_P2P):
+// wave w publishes in LDS the number of steps it has completed, and waits
+// only for what it touches -- its producer's step t-1 before it reads link
+// slot (t-1) % D, its consumer's step t-D+1 before it overwrites slot t % D
+// -- so a wave held up by a late row delays its consumers alone and not the
+// whole workgroup.  Every wait is on a strictly earlier step, so there is no
+// cycle; a wait that runs past ~0.5 s gives up and the pair's K is NaN.
+#ifndef SK4C_P2P
+#define SK4C_P2P 1
+#endif
+#ifndef SK4C_D  // link slots per wave (a power of 2; 2 when lockstep)
+#define SK4C_D (SK4C_P2P ? 4 : 2)
+#endif
+static_assert(SK4C_D >= 2 && (SK4C_D & (SK4C_D - 1)) == 0, "SK4C_D: a power of 2");
+
+__device__ __forceinline__ void s4c_publish(int* done, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(done, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void s4c_wait_ge(const int* done, int v, bool& bad) {
+  if (bad) return;
+  int it = 0;
+  while (__builtin_amdgcn_readfirstlane(
+             __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < v) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++it > (1 << 23)) {
+      bad = true;
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ int s4c_cols(int j, int F) { return j > F + SK4C_PF ? j : F + SK4C_PF; }
 
 // position -> plane of the column schedule; advance() moves on by W positions
@@ -846,10 +881,13 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   const float bound = P.bp_bound;
   const double g = P.gap, stk = P.stack, sub = P.subst;
   const int F = max(P.col_f, 1);
-  // links: wave w writes link w (slot t & 1), wave w+1 reads it a step later
-  double* link_out = s4c_lds + (int64_t)w * 2 * TW;
-  const double* link_in = s4c_lds + (int64_t)(w - 1) * 2 * TW;
-  double* red = s4c_lds + (int64_t)W * 2 * TW;  // W per-wave sums
+  // links: wave w writes link w (slot t % D), wave w+1 reads it a step later
+  constexpr int D = SK4C_D;
+  double* link_out = s4c_lds + (int64_t)w * D * TW;
+  const double* link_in = s4c_lds + (int64_t)(w - 1) * D * TW;
+  double* red = s4c_lds + (int64_t)W * D * TW;  // W per-wave sums
+  int* done = reinterpret_cast<int*>(red + W);  // W step counters (SK4C_P2P)
+  bool bad = false;
 
   // steps: T(last position) + R
   int64_t np = 0;
@@ -886,7 +924,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   struct Row {
     double A[CPL], Bw[CPL];
     float bp[CPL];
-    uint32_t ylm;  // bit c: y[l-1] == x[j-1] of the consumer, slot c
+    uint8_t yl[CPL];  // y[l-1], compared at the row's step: an operation on a
+                      // loaded value here would wait for the load (no prefetch)
   };
   auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
     const int kmax = m - s;
@@ -895,20 +934,20 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
     const double* Ai = planes + (int64_t)d.i * cp + ro;
     const bool wrap_in = w == 0 && !d.first;
-    r.ylm = 0u;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = lane + 64 * c;
       r.A[c] = 0.0;
       r.Bw[c] = 0.0;
       r.bp[c] = 0.0f;
+      r.yl[c] = 0;
 
       if (d.on && s >= 1 && k <= kmax) {
         r.A[c] = d.first ? gpow[s] : Ai[k];  // G0(j-1, j-1) = g^(l-k)
         if (wrap_in) r.Bw[c] = wrapb[ro + k];
         if (d.stack) {
           r.bp[c] = bpy[ye + k];
-          r.ylm |= (ys[k + s - 1] == d.xcj ? 1u : 0u) << c;
+          r.yl[c] = ys[k + s - 1];
         }
       }
     }
@@ -948,12 +987,16 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   for (int q = 0; q < SK4C_PF; ++q)
     if (w - SK4C_PF + q < 0) fetch_next(rq[q]);
   int s = 0;
+#if SK4C_P2P
+  done[w] = cur.valid(n) ? 0 : INT_MAX;
+  __syncthreads();
+#endif
 
   for (int64_t t = 0; t < total; ++t) {
     if (t > 0) {  // (every wave takes every barrier)
       if (t % F == 0) {
         __syncthreads();
-      } else {
+      } else if (!SK4C_P2P) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -964,6 +1007,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
 #pragma unroll
       for (int q = 0; q < SK4C_PF; ++q)
         if (t == w - SK4C_PF + q) fetch_next(rq[q]);
+      if (SK4C_P2P) s4c_publish(done + w, (int)t + 1);
       continue;
     }
     const Row cr = rq[0];
@@ -990,8 +1034,12 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
         const int ro = row_off(m, s);
         double* __restrict__ out = planes + (int64_t)dc.i * cp + ro;
         const bool wrap_in = w == 0;
-        const double* lin = link_in + ((t - 1) & 1) * TW;
-        double* lout = dc.cons && w + 1 < W ? link_out + (t & 1) * TW : nullptr;
+        const double* lin = link_in + ((t - 1) & (D - 1)) * TW;
+        double* lout = dc.cons && w + 1 < W ? link_out + (t & (D - 1)) * TW : nullptr;
+        if (SK4C_P2P) {
+          if (!dc.first && !wrap_in) s4c_wait_ge(done + w - 1, (int)t, bad);
+          if (lout) s4c_wait_ge(done + w + 1, (int)t - D + 2, bad);
+        }
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
           // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
@@ -1015,7 +1063,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
                 const float bp_kl = cr.bp[c];
                 if (bp_kl > bound) {
                   const double g0 = A2;
-                  if (((xkm & cr.ylm) >> c) & 1u) {
+                  if (((xkm >> c) & 1u) && cr.yl[c] == dc.xcj) {
                     ksrc += g0 * stk * (double)dc.bp_c * (double)bp_kl;
                     g3 += g0;
                   } else {
@@ -1046,9 +1094,10 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       cur.advance(W, n, F);
       dc = describe(cur);
     }
+    if (SK4C_P2P) s4c_publish(done + w, cur.valid(n) ? (int)t + 1 : INT_MAX);
   }
   for (int off = 32; off > 0; off >>= 1) ksrc += __shfl_xor(ksrc, off, 64);
-  if (lane == 0) red[w] = ksrc;
+  if (lane == 0) red[w] = bad ? __builtin_nan("") : ksrc;
   __syncthreads();
   if (threadIdx.x == 0) {
     double K = 0.0;
@@ -1062,7 +1111,7 @@ int stem4d_col_max_waves(int cpl) {
 }
 
 size_t stem4d_col_lds_bytes(int cpl, int waves) {
-  return ((size_t)waves * 2 * 64 * cpl + waves) * sizeof(double);
+  return ((size_t)waves * SK4C_D * 64 * cpl + 2 * waves) * sizeof(double);
 }
 
 hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves,
