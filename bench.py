@@ -212,7 +212,7 @@ def algorithmic(kind, shapes, x, y):
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
                 72.0 * stem4d_cells(lens, x, y)
-        if not (os.environ.get("SK4_NO_PRE") or os.environ.get("SK4_NO_COL")) and int(lens[y].max()) + 1 <= 512:
+        if os.environ.get("SK4_COL") and not os.environ.get("SK4_NO_PRE") and int(lens[y].max()) + 1 <= 512:
             # column-pipelined full_dp (stem4d.hip sk_stem4d_col_kernel): G0 of
             # (i,j-1) read and G0 of (i,j) written (16 B); every W-th plane's
             # pre-combined G1 crosses the round wrap through HBM (+16 B)
@@ -765,7 +765,7 @@ def main():
             rf["kernel"] = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
                             "stem4d": "sk_stem4d_kernel" if os.environ.get("SK4_NO_GSUM") else
                             "sk_stem4d_gsum_kernel" if os.environ.get("SK4_NO_PRE") else
-                            "sk_stem4d_pre_kernel" if os.environ.get("SK4_NO_COL") else "sk_stem4d_col_kernel",
+                            "sk_stem4d_col_kernel" if os.environ.get("SK4_COL") else "sk_stem4d_pre_kernel",
                             "bpla": "sk_bpla_fast_kernel"}[kind]
         cpu, parity = None, None
         if not a.no_cpu_baseline and world == 1 and not a.cpu_stub:  # rank 0 at N=1 only

@@ -573,8 +573,15 @@ __global__ void __launch_bounds__(256) sk_stem4d_gsum_kernel(Stem4dLaunch P) {
 // go to its own accumulator acc[i].  Single k tile (|y| < 512; the host runs
 // the K-sum kernel otherwise).  Plane layout: G0 at 0, B' (for the plane
 // (i-1, j)) at cp.
+// SK4P_WPE (build-time): ask the register allocator for that many waves per
+// SIMD (4: <= 128 VGPRs)
+#ifdef SK4P_WPE
+#define SK4P_ATTR __attribute__((amdgpu_waves_per_eu(SK4P_WPE)))
+#else
+#define SK4P_ATTR
+#endif
 template <int CPL>
-__global__ void __launch_bounds__(256) sk_stem4d_pre_kernel(Stem4dLaunch P) {
+__global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaunch P) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t it = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;

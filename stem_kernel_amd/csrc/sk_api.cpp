@@ -1799,10 +1799,11 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   const bool banded = ali_phmm || (!ali && kp->len_band > 0);
   const bool gsum = !banded && !std::getenv("SK4_NO_GSUM");
   const size_t nst = gsum ? 2 : 4;
-  // full_dp with one k tile: the column-pipelined kernel (one workgroup per
-  // pair, B' handed on through LDS; stem4d.hip sk_stem4d_col_kernel) unless
-  // SK4_NO_COL / SK4_NO_PRE (A/B: the span kernels)
-  const bool colk = gsum && !ktiles && !std::getenv("SK4_NO_COL") && !std::getenv("SK4_NO_PRE");
+  // full_dp with one k tile: the pre-combined span kernel; SK4_COL=1 runs the
+  // column-pipelined kernel instead (one workgroup per pair, B' handed on
+  // through LDS; stem4d.hip sk_stem4d_col_kernel): half the bytes, but slower
+  // on MI355X (r04) -- kept as an option and tested
+  const bool colk = gsum && !ktiles && std::getenv("SK4_COL") && !std::getenv("SK4_NO_PRE");
   double total_ms = 0.0;
   int launches = 0;
   Stem4dBatch& Bt = ctx->s4d;

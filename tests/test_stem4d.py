@@ -83,21 +83,25 @@ def test_stem4d_gram_matches_oracle(gpu_ctx, model, bound):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("no_pre", [False, True])
-def test_stem4d_ksum_equals_four_state(gpu_ctx, monkeypatch, no_pre):
+@pytest.mark.parametrize("mode", ["pre", "col", "ksum"])
+def test_stem4d_ksum_equals_four_state(gpu_ctx, monkeypatch, mode):
     """full_dp with the K chain summed (K0(0,n,0,m) = 1 + the sum of every
     stacking source) against the four-state planes
     (SK4_NO_GSUM=1): equal up to the association of non-negative sums, CPL
     1-4, empty and one-residue sequences included, both against the oracle.
-    no_pre=False runs the pre-combined kernel (sk_stem4d_pre_kernel, the
-    default for |y| < 512), no_pre=True the K-sum kernel
-    (sk_stem4d_gsum_kernel) on the same short sequences (SK4_NO_PRE=1)."""
+    "pre" runs the pre-combined kernel (sk_stem4d_pre_kernel, the default for
+    |y| < 512), "col" the column-pipelined kernel (SK4_COL=1), "ksum" the
+    K-sum kernel (sk_stem4d_gsum_kernel) on the same short sequences
+    (SK4_NO_PRE=1)."""
     seqs = _seqs() + ["", "G"] + ska.random_sequences(2, 130, 0x5EED0043)
     ds, _ = make_examples(seqs)
     kern = ska.StemKernel4D()
-    if no_pre:
+    if mode == "ksum":
         monkeypatch.setenv("SK4_NO_PRE", "1")
+    if mode == "col":
+        monkeypatch.setenv("SK4_COL", "1")
     a = gpu_ctx.gram(ds, kern)
+    assert bool(gpu_ctx.last_classes()["stem4d_col"]) == (mode == "col")
     monkeypatch.setenv("SK4_NO_GSUM", "1")
     b = gpu_ctx.gram(ds, kern)
     assert rel_err(a, b) < 1e-12
