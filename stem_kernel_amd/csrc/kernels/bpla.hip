@@ -719,7 +719,9 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
       // to the same pair; they go to the pair's sum when the pair changes
       const double h = accA + (okB ? accB : 0.0);
       const bool cont = okA && okan && pn == p;
-      if (okA && !cont) ksum[p] += h;
+      // (an LDS add without return: no read round trip inside the window;
+      // one lane, this wave's own sums, so the order of additions is kept)
+      if (okA && !cont) __hip_atomic_fetch_add(&ksum[p], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       accA = cont ? h : 0.0;
       accB = 0.0;
       xA = xnA;
