@@ -39,69 +39,102 @@ static double pair_weight(char a, char b, bool no_gu) {
 // Inside/outside over the grammar  S(i,j) -> S(i,j-1) | S(i,k-1) (k S(k+1,j-1) j)
 // with spans scaled by s^-(len) to stay in range.  Output: p(i,j), i<j, 0-based,
 // packed strict upper triangle.
-void fold_nussinov(const char* seq, int n, bool no_gu, double* out) {
+//
+// Layout: every table is stored by diagonal, X(i, i+e) at D[e+1][i] (e = -1
+// holds the empty spans, Q = 1), so for four neighbouring cells (i..i+3, j =
+// i + d) each term of the k loop -- Q(i, k-1), B(k, j), Q(k+1, j-1), and in
+// the outside pass the updates of O(i, k-1), O(k+1, j-1), P(k, j) -- is one
+// contiguous 4-wide access.  Four cells of a diagonal run side by side: each
+// cell's value is formed by the same operations in the same order as the
+// scalar loop (bit-identical output; fp contraction off), four independent
+// add chains instead of one.  In the outside pass the four cells' updates
+// never hit one element (two cells i < i' of a diagonal share a target only
+// when i' - i >= hp + 1 = 4), so updating them side by side keeps the
+// scalar loop's order per element.
+// (an unaligned 4-double vector: plain dereferences, no vector-valued
+// functions, so the AVX2 clone and the baseline one share one source)
+typedef double sk_v4d __attribute__((vector_size(32), aligned(8)));
+#define v4_ld(p) (*reinterpret_cast<const sk_v4d*>(p))
+#define v4_st(p, v) (*reinterpret_cast<sk_v4d*>(p) = (v))
+
+// AVX2 where the host has it (no FMA: the products and sums stay separate)
+__attribute__((target_clones("avx2", "default"))) void fold_nussinov(const char* seq, int n, bool no_gu, double* out) {
+#pragma STDC FP_CONTRACT OFF
   if (n < 2) return;
   const double s = 2.0, inv_s = 1.0 / s, inv_s2 = inv_s * inv_s;
   const int hp = 3;
-  // Q(i,j) for 0<=i<=j<n; empty spans (j=i-1) are 1.  Q is kept in both
-  // layouts (QT[j][i] = Q[i][j]) and B, P transposed, so every k loop below
-  // walks memory contiguously; each value is formed by the same operations
-  // in the same order as the row-major loops (bit-identical output).
-  auto at = [n](int i, int j) { return (size_t)i * n + j; };
-  // per-thread workspace: repeated folds reuse already-faulted pages
-  thread_local std::vector<double> Q, QT, O, BT, PT;
-  Q.assign((size_t)n * n, 0.0);
-  QT.assign((size_t)n * n, 0.0);
-  O.assign((size_t)n * n, 0.0);
-  BT.assign((size_t)n * n, 0.0);  // BT[j][k] = B(k, j)
-  auto q = [&](int i, int j) -> double { return j < i ? 1.0 : Q[at(i, j)]; };
-  for (int i = 0; i < n; ++i)
-    for (int j = i + hp + 1; j < n; ++j) BT[at(j, i)] = pair_weight(seq[i], seq[j], no_gu) * inv_s2;
+  // diagonal e (-1 .. n-1) starts at off[e + 1]; n - e cells (n + 1 for e = -1)
+  thread_local std::vector<size_t> off;
+  off.assign((size_t)n + 2, 0);
+  for (int e = -1; e < n; ++e) off[e + 2] = off[e + 1] + (size_t)(e < 0 ? n + 1 : n - e) + 4;  // +4: vector tails
+  const size_t tot = off[n + 1];
+  thread_local std::vector<double> Q, O, B, P;
+  Q.assign(tot, 0.0);
+  O.assign(tot, 0.0);
+  B.assign(tot, 0.0);
+  P.assign(tot, 0.0);
+  auto D = [&](std::vector<double>& X, int e) { return X.data() + off[e + 1]; };
+  for (int i = 0; i <= n; ++i) D(Q, -1)[i] = 1.0;
+  for (int e = hp + 1; e < n; ++e)
+    for (int i = 0; i + e < n; ++i) D(B, e)[i] = pair_weight(seq[i], seq[i + e], no_gu) * inv_s2;
   for (int d = 0; d < n; ++d) {
-    for (int i = 0; i + d < n; ++i) {
-      const int j = i + d;
-      double v = q(i, j - 1) * inv_s;
-      const double* __restrict__ bj = &BT[at(j, 0)];
-      const double* __restrict__ qi = &Q[at(i, 0)];
-      const double* __restrict__ qtj = &QT[at(j - 1 >= 0 ? j - 1 : 0, 0)];
-      // k = i (left span empty), then the rest; a pair that cannot form
-      // adds an exact +0 (v > 0), so no branch is needed on b
-      // (inner = q(k+1, j-1) always has k+1 <= j-3)
-      if (i <= j - hp - 1) v += 1.0 * bj[i] * qtj[i + 1];
-      for (int k = i + 1; k <= j - hp - 1; ++k) v += qi[k - 1] * bj[k] * qtj[k + 1];
-      Q[at(i, j)] = v;
-      QT[at(j, i)] = v;
+    const int m = n - d;  // cells of diagonal d
+    const double* qd1 = D(Q, d - 1);
+    double* qd = D(Q, d);
+    int i = 0;
+    for (; i + 4 <= m; i += 4) {
+      sk_v4d v = v4_ld(qd1 + i) * inv_s;
+      for (int t = 0; t <= d - hp - 1; ++t) v += v4_ld(D(Q, t - 1) + i) * v4_ld(D(B, d - t) + i + t) * v4_ld(D(Q, d - t - 2) + i + t + 1);
+      v4_st(qd + i, v);
+    }
+    for (; i < m; ++i) {
+      double v = qd1[i] * inv_s;
+      for (int t = 0; t <= d - hp - 1; ++t) v += D(Q, t - 1)[i] * D(B, d - t)[i + t] * D(Q, d - t - 2)[i + t + 1];
+      qd[i] = v;
     }
   }
-  const double Z = Q[at(0, n - 1)];
-  O[at(0, n - 1)] = 1.0;
-  PT.assign((size_t)n * n, 0.0);  // PT[j][k] = P(k, j)
+  const double Z = D(Q, n - 1)[0];
+  D(O, n - 1)[0] = 1.0;
   for (int d = n - 1; d >= 0; --d) {
-    for (int i = 0; i + d < n; ++i) {
-      const int j = i + d;
-      const double o = O[at(i, j)];
+    const int m = n - d;
+    const double* od = D(O, d);
+    double* od1 = D(O, d - 1);  // (d = 0: the e = -1 row, written and never read)
+    int i = 0;
+    for (; i + 4 <= m; i += 4) {
+      const sk_v4d o = v4_ld(od + i);
+      if (o[0] == 0.0 && o[1] == 0.0 && o[2] == 0.0 && o[3] == 0.0) continue;
+      if (d >= 1) v4_st(od1 + i, v4_ld(od1 + i) + o * inv_s);
+      for (int t = 0; t <= d - hp - 1; ++t) {
+        const sk_v4d b = v4_ld(D(B, d - t) + i + t);
+        const sk_v4d left = v4_ld(D(Q, t - 1) + i);
+        const sk_v4d inner = v4_ld(D(Q, d - t - 2) + i + t + 1);
+        if (t >= 1) {
+          double* orow = D(O, t - 1) + i;
+          v4_st(orow, v4_ld(orow) + o * b * inner);
+        }
+        double* ocol = D(O, d - t - 2) + i + t + 1;
+        v4_st(ocol, v4_ld(ocol) + o * b * left);
+        double* pp = D(P, d - t) + i + t;
+        v4_st(pp, v4_ld(pp) + o * left * b * inner);
+      }
+    }
+    for (; i < m; ++i) {
+      const double o = od[i];
       if (o == 0.0) continue;
-      if (j - 1 >= i) O[at(i, j - 1)] += o * inv_s;
-      const double* __restrict__ bj = &BT[at(j, 0)];
-      const double* __restrict__ qi = &Q[at(i, 0)];
-      const double* __restrict__ qtj = &QT[at(j - 1 >= 0 ? j - 1 : 0, 0)];
-      double* __restrict__ pj = &PT[at(j, 0)];
-      // (every term of a pair that cannot form is an exact +0: no branch;
-      // inner = q(k+1, j-1) always has k+1 <= j-3)
-      double* __restrict__ oi = &O[at(i, 0)];
-      for (int k = i; k <= j - hp - 1; ++k) {
-        const double b = bj[k];
-        const double left = k - 1 >= i ? qi[k - 1] : 1.0;
-        const double inner = qtj[k + 1];
-        if (k - 1 >= i) oi[k - 1] += o * b * inner;
-        O[at(k + 1, j - 1)] += o * b * left;
-        pj[k] += o * left * b * inner;
+      if (d >= 1) od1[i] += o * inv_s;
+      for (int t = 0; t <= d - hp - 1; ++t) {
+        const double b = D(B, d - t)[i + t];
+        const double left = D(Q, t - 1)[i];
+        const double inner = D(Q, d - t - 2)[i + t + 1];
+        if (t >= 1) D(O, t - 1)[i] += o * b * inner;
+        D(O, d - t - 2)[i + t + 1] += o * b * left;
+        D(P, d - t)[i + t] += o * left * b * inner;
       }
     }
   }
   size_t t = 0;
   for (int i = 0; i < n; ++i)
-    for (int j = i + 1; j < n; ++j) out[t++] = PT[at(j, i)] / Z;
+    for (int j = i + 1; j < n; ++j) out[t++] = D(P, j - i)[i] / Z;
 }
 
 void random_sequence(uint64_t& state, int len, char* out) {

@@ -3081,6 +3081,8 @@ int sk_dataset_add_synthetic_rows(sk_dataset* ds, int32_t n, int32_t n_rows,
   int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
   nt = std::max(1, std::min(nt, std::max<int32_t>(n, 1)));
   std::atomic<int32_t> next(0), status(SK_OK);
+  static const bool stats = std::getenv("SK_HOST_STATS") != nullptr;
+  std::atomic<int64_t> ns_fold(0), ns_build(0);
   auto work = [&]() {
     std::vector<std::vector<double>> bpp(n_rows);
     std::vector<const double*> bptr(n_rows);
@@ -3088,6 +3090,7 @@ int sk_dataset_add_synthetic_rows(sk_dataset* ds, int32_t n, int32_t n_rows,
       const int32_t i = next.fetch_add(1);
       if (i >= n || status.load() != SK_OK) return;
       try {
+        const auto t0 = std::chrono::steady_clock::now();
         const char* const* ex_rows = rows + (size_t)i * n_rows;
         for (int32_t r = 0; r < n_rows; ++r) {
           const char* s = ex_rows[r];
@@ -3100,7 +3103,13 @@ int sk_dataset_add_synthetic_rows(sk_dataset* ds, int32_t n, int32_t n_rows,
           sk::fold_nussinov(row.c_str(), (int)row.size(), false, bpp[r].data());
           bptr[r] = bpp[r].data();
         }
+        const auto t1 = std::chrono::steady_clock::now();
         sk::build_example(ds->ex[base + i], n_rows, ex_rows, bptr.data(), th, true);
+        if (stats) {
+          const auto t2 = std::chrono::steady_clock::now();
+          ns_fold += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+          ns_build += std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+        }
       } catch (...) {
         status.store(SK_ERR_INVALID);
       }
@@ -3110,6 +3119,9 @@ int sk_dataset_add_synthetic_rows(sk_dataset* ds, int32_t n, int32_t n_rows,
   for (int t = 1; t < nt; ++t) pool.emplace_back(work);
   work();
   for (auto& t : pool) t.join();
+  if (stats)
+    std::fprintf(stderr, "[sk] synthetic examples: %d on %d threads, fold %.3f s, build %.3f s (thread-seconds)\n", n,
+                 nt, ns_fold.load() * 1e-9, ns_build.load() * 1e-9);
   if (status.load() != SK_OK) {
     ds->ex.resize(base);
     ds->labels.resize(base);
