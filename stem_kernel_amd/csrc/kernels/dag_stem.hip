@@ -399,13 +399,18 @@ __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int
   A.rv = R[A.rec & 0x7ff];
   int c = c0;
   const int nch = Y.nch;
-  // chunk X now, Y next, Z after: false after the last chunk
+  // chunk X now, Y next, Z after: false after the last chunk.  SK_SWEEP_GAP
+  // 2: the host never puts an edge into the chunk right after the one that
+  // completes its child, so chunk Y's R reads are issued before chunk X's
+  // atomics -- two chunks' reads in flight, one LDS round trip per two
+  // chunks (1: each chunk's reads after the previous chunk's atomics)
   auto step = [&](Ck& X, Ck& Yc, Ck& Z) __attribute__((always_inline)) -> bool {
     Z.rec = rp[128];
     Yc.w = NW ? nweight(Yc.rec) : wp[64];
+    if (SK_SWEEP_GAP >= 2) Yc.rv = R[Yc.rec & 0x7ff];
     __hip_atomic_fetch_add(&R[(X.rec >> 11) & 0x7ff], X.rv * X.w, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WAVEFRONT);
-    Yc.rv = R[Yc.rec & 0x7ff];
+    if (SK_SWEEP_GAP < 2) Yc.rv = R[Yc.rec & 0x7ff];
     rp += 64;
     wp += 64;
     return ++c < nch;

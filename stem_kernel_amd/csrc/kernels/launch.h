@@ -9,6 +9,17 @@
 
 namespace sk {
 
+// IY sweep schedule: an edge goes into a chunk at least SK_SWEEP_GAP chunks
+// after the one that completes its child (the host's list schedule,
+// sk_api.cpp); at 2 the kernel issues a chunk's R reads before the previous
+// chunk's atomics (dag_stem.hip iy_sweep).  Off: the NS y DAGs' sweeps are
+// bound by their height, not their width -- gap 2 takes 78.3 chunks per y
+// against 45.6 (1,024 L = 200 examples, tools/pack_compare.cpp), so two
+// reads in flight would buy nothing
+#ifndef SK_SWEEP_GAP
+#define SK_SWEEP_GAP 1
+#endif
+
 struct StemLaunch {
   DevSet xset;        // row examples (x role)
   DevSet yset;        // column examples (y role); may equal xset

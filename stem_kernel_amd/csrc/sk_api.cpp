@@ -670,8 +670,11 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
           if (rem[c] == 0) push_edges_of(c);
         std::vector<int32_t> cm;  // prefix maximum of the children's lengths
         int32_t run = -1, placed = 0;
-        std::vector<int> take, done;
-        while (!ready.empty()) {
+        // done: parents completed by the chunk just formed; their edges are
+        // ready SK_SWEEP_GAP chunks on (pend holds the ones in between; a
+        // chunk with nothing ready is all dummies, so the gap holds)
+        std::vector<int> take, done, pend;
+        while (!ready.empty() || !pend.empty()) {
           take.clear();
           done.clear();
           while (!ready.empty() && (int)take.size() < 64) {
@@ -695,7 +698,12 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
           }
           placed += (int)take.size();
           cm.push_back(run);
-          for (int q : done) push_edges_of(q);  // ready from the next chunk on
+          if (SK_SWEEP_GAP >= 2) {
+            for (int q : pend) push_edges_of(q);  // completed the chunk before: ready from the next on
+            pend.swap(done);
+          } else {
+            for (int q : done) push_edges_of(q);  // ready from the next chunk on
+          }
         }
         if (placed != ne_all) {
           Y.err = "IY sweep schedule: DAG has a cycle";
@@ -1362,8 +1370,13 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
     copy();
     for (auto& t : th) t.join();
 #undef SK_YBIG
-    if (tstats) fprintf(stderr, "[sk pack] y-role %.1f ms (%d threads) + append %.1f ms\n", ty1 - tp2, nthr,
-                        tnow() - ty1);
+    if (tstats) {
+      long tch = 0;
+      for (int32_t c : P.ex_nch) tch += c;
+      fprintf(stderr, "[sk pack] y-role %.1f ms (%d threads) + append %.1f ms; sweep chunks %ld (%.2f per y, gap %d)\n",
+              ty1 - tp2, nthr, tnow() - ty1, tch, P.ex_nch.empty() ? 0.0 : (double)tch / P.ex_nch.size(),
+              SK_SWEEP_GAP);
+    }
   }
   return SK_OK;
 }
