@@ -225,8 +225,13 @@ struct sk_context {
     size_t blk = 0, off = 0;
     hipEvent_t ev = nullptr;
     bool recorded = false;
+    // device copy of a call's inputs uploaded on the copy stream (up_reserve)
+    char* dbuf = nullptr;
+    size_t dcap = 0;
+    hipEvent_t uev = nullptr;
   };
   Stage stage[2];
+  hipStream_t cps = nullptr;  // copy stream of the asynchronous uploads
   uint64_t ncalls = 0;
   double last_launch_ms_sum = 0.0;
   int32_t last_launch_n = 0;
@@ -348,6 +353,38 @@ hipError_t h2d(sk_context* ctx, void* dst, const void* src, size_t bytes, hipStr
   G.off += need;
   std::memcpy(p, src, bytes);
   return hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s);
+}
+
+// Asynchronous calls (BPLA): the call's host inputs go to a device buffer of
+// the call's parity on a copy stream that the call's stream then waits for,
+// so the upload overlaps the previous call's kernels instead of following
+// them.  The buffer's last user is the call two back, which call_begin has
+// waited for.
+hipError_t up_reserve(sk_context* ctx, size_t bytes, char** dst) {
+  sk_context::Stage& G = ctx->stage[(ctx->ncalls - 1) & 1];
+  hipError_t r;
+  if (G.dcap < bytes) {
+    if (G.dbuf && (r = hipFree(G.dbuf)) != hipSuccess) return r;
+    G.dbuf = nullptr;
+    G.dcap = 0;
+    const size_t cap = bytes + bytes / 4 + 4096;
+    void* p = nullptr;
+    if ((r = hipMalloc(&p, cap)) != hipSuccess) return r;
+    G.dbuf = static_cast<char*>(p);
+    G.dcap = cap;
+  }
+  *dst = G.dbuf;
+  return hipSuccess;
+}
+
+hipError_t up_copy(sk_context* ctx, const void* src, size_t bytes, hipStream_t s) {
+  sk_context::Stage& G = ctx->stage[(ctx->ncalls - 1) & 1];
+  hipError_t r;
+  if (!ctx->cps && (r = hipStreamCreateWithFlags(&ctx->cps, hipStreamNonBlocking)) != hipSuccess) return r;
+  if (!G.uev && (r = hipEventCreateWithFlags(&G.uev, hipEventDisableTiming)) != hipSuccess) return r;
+  if ((r = h2d(ctx, G.dbuf, src, bytes, ctx->cps)) != hipSuccess) return r;  // (pinned staging)
+  if ((r = hipEventRecord(G.uev, ctx->cps)) != hipSuccess) return r;
+  return hipStreamWaitEvent(s, G.uev, 0);
 }
 
 // End of a compute call whose span events (ev0/ev1: stem, ev2/ev3: string)
@@ -1566,31 +1603,54 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   int rc = ensure_work(ctx, 16 * 8 + nb * 8 + (permute ? nb * 8 : 0) + ntab * sizeof(sk::BplaPos) +
                                 items.size() * sizeof(int2) + 8192);
   if (rc) return rc;
-  Arena A{static_cast<char*>(ctx->work), 0, ctx->work_bytes};
   // the call's host inputs and zeroed counters are laid out as on the device
   // and go up in ONE copy (separate small copies and a memset cost the
-  // stream ~0.1 ms of gaps per call)
-  double* d_tb = A.take<double>(16);
-  unsigned long long* d_ctr = A.take<unsigned long long>(8);
-  int32_t* d_px = A.take<int32_t>(nb);
-  int32_t* d_py = A.take<int32_t>(nb);
-  int64_t* d_oidx = permute ? A.take<int64_t>(nb) : nullptr;
-  int2* d_items = items.empty() ? nullptr : A.take<int2>(items.size());
-  const size_t up_bytes = A.off;
+  // stream ~0.1 ms of gaps per call); asynchronous calls upload them on the
+  // copy stream into a buffer of their own (up_reserve), overlapping the
+  // previous call's kernels
+  double* d_tb;
+  unsigned long long* d_ctr;
+  int32_t *d_px, *d_py;
+  int64_t* d_oidx;
+  int2* d_items;
+  auto lay = [&](Arena& U) {
+    d_tb = U.take<double>(16);
+    d_ctr = U.take<unsigned long long>(8);
+    d_px = U.take<int32_t>(nb);
+    d_py = U.take<int32_t>(nb);
+    d_oidx = permute ? U.take<int64_t>(nb) : nullptr;
+    d_items = items.empty() ? nullptr : U.take<int2>(items.size());
+  };
+  Arena A{static_cast<char*>(ctx->work), 0, ctx->work_bytes};
+  Arena U{nullptr, 0, 0};
+  lay(U);  // (sizes only)
+  const size_t up_bytes = U.off;
+  if (ctx->async) {
+    char* ub = nullptr;
+    SK_HIP(ctx, sk::up_reserve(ctx, up_bytes, &ub));
+    U = Arena{ub, 0, up_bytes};
+    lay(U);
+  } else {
+    lay(A);
+    U.base = A.base;
+  }
   sk::BplaPos* d_tab = ntab ? A.take<sk::BplaPos>(ntab) : nullptr;
   hipStream_t S = ctx->stream;
   {
     thread_local std::vector<char> hb;
     hb.assign(up_bytes, 0);
     auto put = [&](const void* dptr, const void* src, size_t bytes) {
-      if (bytes) std::memcpy(hb.data() + (static_cast<const char*>(dptr) - A.base), src, bytes);
+      if (bytes) std::memcpy(hb.data() + (static_cast<const char*>(dptr) - U.base), src, bytes);
     };
     put(d_tb, kp->score_table, 16 * 8);
     put(d_px, x, nb * 4);
     put(d_py, y, nb * 4);
     if (permute) put(d_oidx, oidx.data(), nb * 8);
     if (d_items) put(d_items, items.data(), items.size() * sizeof(int2));
-    SK_HIP(ctx, sk::h2d(ctx, A.base, hb.data(), up_bytes, S));
+    if (ctx->async)
+      SK_HIP(ctx, sk::up_copy(ctx, hb.data(), up_bytes, S));
+    else
+      SK_HIP(ctx, sk::h2d(ctx, U.base, hb.data(), up_bytes, S));
   }
   sk::BplaLaunch T;
   T.xset = xs_->dev;
@@ -3040,8 +3100,11 @@ int sk_close(sk_context* ctx) {
   }
   for (auto& G : ctx->stage) {
     if (G.ev) (void)hipEventDestroy(G.ev);
+    if (G.uev) (void)hipEventDestroy(G.uev);
+    if (G.dbuf) (void)hipFree(G.dbuf);
     for (auto& b : G.blocks) (void)hipHostFree(b.first);
   }
+  if (ctx->cps) (void)hipStreamDestroy(ctx->cps);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SK_OK;
