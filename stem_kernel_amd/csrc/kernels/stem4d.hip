@@ -815,8 +815,8 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 // -- so a wave held up by a late row delays its consumers alone and not the
 // whole workgroup.  Every wait is on a strictly earlier step, so there is no
 // cycle; a wait that runs past ~0.5 s gives up and the pair's K is NaN.
-#ifndef SK4C_P2P
-#define SK4C_P2P 1
+#ifndef SK4C_P2P  // off: 278 against 305 pairs/s lockstep on C3 (r04e)
+#define SK4C_P2P 0
 #endif
 #ifndef SK4C_D  // link slots per wave (a power of 2; 2 when lockstep)
 #define SK4C_D (SK4C_P2P ? 4 : 2)
