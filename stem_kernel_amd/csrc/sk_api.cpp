@@ -36,6 +36,7 @@ namespace {
 
 struct DeviceBuffers {
   std::vector<void*> ptrs;
+  size_t bytes = 0;  // (SK_HOST_STATS)
   ~DeviceBuffers() { release(); }
   void release() {
     for (void* p : ptrs) (void)hipFree(p);
@@ -50,6 +51,7 @@ hipError_t upload(DeviceBuffers& db, const V& v, const T** out) {
   hipError_t e = hipMalloc(&p, bytes);
   if (e != hipSuccess) return e;
   db.ptrs.push_back(p);
+  db.bytes += bytes;
   if (!v.empty()) e = hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
   *out = static_cast<const T*>(p);
   return e;
@@ -3292,8 +3294,10 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   if (!ctx || !ds) return SK_ERR_INVALID;
   if (ds->uploaded) return ds->device == ctx->device ? SK_OK : fail(ctx, SK_ERR_INVALID, "dataset bound to another device");
   std::string err;
+  const auto tu0 = std::chrono::steady_clock::now();
   int rc = pack_dataset(ds, err);
   if (rc) return fail(ctx, rc, err);
+  const auto tu1 = std::chrono::steady_clock::now();
   SK_HIP(ctx, hipSetDevice(ctx->device));
   HostPack& P = ds->pack;
   P.xr_ch.insert(P.xr_ch.end(), 8, 0u);  // the kernel prefetches 4 records past a row
@@ -3387,6 +3391,12 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   D.total_nodes = (int64_t)P.nd_a.size();
   ds->device = ctx->device;
   ds->uploaded = true;
+  if (std::getenv("SK_HOST_STATS")) {
+    const auto tu2 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[sk upload] pack %.1f ms, %zu arrays %.1f MB to the device %.1f ms\n",
+                 std::chrono::duration<double, std::milli>(tu1 - tu0).count(), B.ptrs.size(), B.bytes / 1e6,
+                 std::chrono::duration<double, std::milli>(tu2 - tu1).count());
+  }
   return SK_OK;
 }
 
