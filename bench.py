@@ -192,7 +192,8 @@ def col_waves(lens, y):
     barriers, 1 for short y; one batch per bench step)."""
     m = lens[y]
     cpl = 1 if m.max() + 1 <= 64 else 2 if m.max() + 1 <= 128 else 4 if m.max() + 1 <= 256 else 8
-    F = 8 if int(m.min()) - 9 >= 4 else 1
+    f_env = max(1, int(os.environ.get("SK4C_F", "8")))
+    F = f_env if int(m.min()) - f_env - 1 >= 4 else 1
     return int(max(1, min({1: 16, 2: 16, 4: 12, 8: 8}[cpl], int(m.min()) - F - 1)))
 
 

@@ -1931,7 +1931,9 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       for (const auto& p : prs) min_m = std::min(min_m, p.m);
       // W <= m - F - 1 (the round wrap's lag, stem4d.hip); full barriers every
       // F = 8 steps where the y's are long enough, else every step
-      const int F = min_m - 9 >= 4 ? 8 : 1;
+      // (SK4C_F: another interval, A/B)
+      static const int f_env = std::getenv("SK4C_F") ? std::max(1, std::atoi(std::getenv("SK4C_F"))) : 8;
+      const int F = min_m - f_env - 1 >= 4 ? f_env : 1;
       const int W = std::max(1, std::min(sk::stem4d_col_max_waves(cpl), min_m - F - 1));
       rc = ensure_scratch(ctx, ring_bytes + 64);
       if (rc) return rc;
