@@ -216,7 +216,8 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
 
 @pytest.mark.parametrize("n,m,W,F", [(9, 11, 3, 1), (12, 7, 5, 1), (6, 14, 12, 1), (1, 5, 3, 1),
                                      (0, 6, 2, 1), (10, 4, 2, 1), (7, 9, 1, 1), (13, 13, 11, 1),
-                                     (12, 17, 4, 8), (10, 21, 12, 8), (16, 13, 4, 8), (5, 30, 12, 8)])
+                                     (12, 17, 4, 8), (10, 21, 12, 8), (16, 13, 4, 8), (5, 30, 12, 8),
+                                     (8, 30, 4, 16), (6, 40, 12, 24)])
 @pytest.mark.parametrize("pf", [2, 1])
 def test_column_schedule_equals_oracle(n, m, W, F, pf):
     seqs = ska.random_sequences(2, max(n, m, 1), 0x5EED0C01 + n * 31 + m)

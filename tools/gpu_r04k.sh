@@ -18,3 +18,7 @@ run c4 python3 -u bench.py --config c4 --no-cpu-baseline
 run c3 python3 -u bench.py --config c3 --no-cpu-baseline
 run c2 python3 -u bench.py --config c2 --no-cpu-baseline
 run c5 python3 -u bench.py --config c5 --no-cpu-baseline
+# column kernel: full-barrier interval F (SK4C_F) sweep
+run c3col_f8 SK4_COL=1 python3 -u bench.py --config c3 --no-cpu-baseline
+run c3col_f16 SK4_COL=1 SK4C_F=16 python3 -u bench.py --config c3 --no-cpu-baseline
+run c3col_f32 SK4_COL=1 SK4C_F=32 python3 -u bench.py --config c3 --no-cpu-baseline
