@@ -918,10 +918,13 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     d.bp_c = 0.0f;
     d.xci = d.xcj = 0;
     if (d.cons) {  // the consumer (i-1, j): bp(i-1, j-1) (:320)
+      // (wave-uniform loads made uniform in SGPRs: the plane's branches on
+      // them are then scalar branches, not exec-mask juggling per slot)
       const int e = d.j - d.i;
-      d.bp_c = bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (d.i - 1)];
-      d.xci = xs[d.i - 1];
-      d.xcj = xs[d.j - 1];
+      d.bp_c = __uint_as_float(__builtin_amdgcn_readfirstlane(
+          __float_as_uint(bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (d.i - 1)])));
+      d.xci = (uint8_t)__builtin_amdgcn_readfirstlane(xs[d.i - 1]);
+      d.xcj = (uint8_t)__builtin_amdgcn_readfirstlane(xs[d.j - 1]);
     }
     d.stack = d.cons && d.bp_c > bound;
     return d;
