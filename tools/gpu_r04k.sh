@@ -22,3 +22,13 @@ run c5 python3 -u bench.py --config c5 --no-cpu-baseline
 run c3col_f8 SK4_COL=1 python3 -u bench.py --config c3 --no-cpu-baseline
 run c3col_f16 SK4_COL=1 SK4C_F=16 python3 -u bench.py --config c3 --no-cpu-baseline
 run c3col_f32 SK4_COL=1 SK4C_F=32 python3 -u bench.py --config c3 --no-cpu-baseline
+# C4 kernel trace: gaps between consecutive BPLA launches (uploads on the copy stream)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_c4 -o run --output-format csv -- python3 bench.py --config c4 --no-cpu-baseline > $OUT/prof_c4.log 2>&1 || { tail -20 $OUT/prof_c4.log; exit 1; }
+python3 - $OUT <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/prof_c4/**/*kernel_trace.csv", recursive=True)[0]
+rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+ks = [r for r in rows if "bpla_fast_items" in r["Kernel_Name"]]
+gaps = [(int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 for a, b in zip(ks, ks[1:])]
+print("C4 items-kernel gaps us:", [round(g, 1) for g in gaps])
+PY
