@@ -842,6 +842,17 @@ __device__ __forceinline__ void s4c_wait_ge(const int* done, int v, bool& bad) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// A range-checked buffer over `bytes` from `base` (wave-uniform): loads past
+// the range return 0, stores past it are dropped -- a row's slots need no
+// per-slot guard, so a step is straight-line code.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s4c_rsrc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
+}
+typedef unsigned int s4c_u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+
 __device__ __forceinline__ int s4c_cols(int j, int F) { return j > F + SK4C_PF ? j : F + SK4C_PF; }
 
 // position -> plane of the column schedule; advance() moves on by W positions
@@ -938,27 +949,42 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
                       // loaded value here would wait for the load (no prefetch)
   };
   auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
-    const int kmax = m - s;
+    // cells k <= m - s of the row; past them every load returns 0 (buffer
+    // range), the branches below are on wave-uniform values
+    const int nk = d.on && s >= 1 ? m - s + 1 : 0;
     const int ro = row_off(m, s);
     const int e2 = s - 1;
     const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
-    const double* Ai = planes + (int64_t)d.i * cp + ro;
-    const bool wrap_in = w == 0 && !d.first;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      const int k = lane + 64 * c;
-      r.A[c] = 0.0;
-      r.Bw[c] = 0.0;
+      r.A[c] = r.Bw[c] = 0.0;
       r.bp[c] = 0.0f;
       r.yl[c] = 0;
-
-      if (d.on && s >= 1 && k <= kmax) {
-        r.A[c] = d.first ? gpow[s] : Ai[k];  // G0(j-1, j-1) = g^(l-k)
-        if (wrap_in) r.Bw[c] = wrapb[ro + k];
-        if (d.stack) {
-          r.bp[c] = bpy[ye + k];
-          r.yl[c] = ys[k + s - 1];
-        }
+    }
+    if (nk == 0) return;
+    if (d.first) {  // G0(j-1, j-1) = g^(l-k)
+      const double gs = gpow[s];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) r.A[c] = lane + 64 * c < nk ? gs : 0.0;
+    } else {
+      const __amdgpu_buffer_rsrc_t ra = s4c_rsrc(planes + (int64_t)d.i * cp + ro, nk * 8);
+#pragma unroll
+      for (int c = 0; c < CPL; ++c)
+        r.A[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, lane * 8, c * 512, 0));
+      if (w == 0) {  // the round wrap's B'
+        const __amdgpu_buffer_rsrc_t rw = s4c_rsrc(wrapb + ro, nk * 8);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+          r.Bw[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rw, lane * 8, c * 512, 0));
+      }
+    }
+    if (d.stack) {
+      const __amdgpu_buffer_rsrc_t rb = s4c_rsrc(bpy + ye, nk * 4);
+      const __amdgpu_buffer_rsrc_t ry = s4c_rsrc(ys + s - 1, nk);
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        r.bp[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, lane * 4, c * 256, 0));
+        r.yl[c] = __builtin_amdgcn_raw_buffer_load_b8(ry, lane, c * 64, 0);
       }
     }
   };
@@ -1041,15 +1067,23 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           Am2[c] = G2c[c] = G3c[c] = 0.0;
         }
       } else {
+        // Straight-line slots: lanes past kmax compute values that are never
+        // stored (the output buffers' range ends at kmax) nor read by a valid
+        // cell of a later row (a cell reads k+1 of the row before, valid
+        // there), and add nothing to K (their bp loads are 0 and masked)
         const int ro = row_off(m, s);
-        double* __restrict__ out = planes + (int64_t)dc.i * cp + ro;
+        const int nk = kmax + 1;
+        const __amdgpu_buffer_rsrc_t ro_out = s4c_rsrc(planes + (int64_t)dc.i * cp + ro, nk * 8);
         const bool wrap_in = w == 0;
         const double* lin = link_in + ((t - 1) & (D - 1)) * TW;
         double* lout = dc.cons && w + 1 < W ? link_out + (t & (D - 1)) * TW : nullptr;
+        const __amdgpu_buffer_rsrc_t ro_wrap = s4c_rsrc(wrapb + ro, dc.cons && !lout ? nk * 8 : 0);
         if (SK4C_P2P) {
           if (!dc.first && !wrap_in) s4c_wait_ge(done + w - 1, (int)t, bad);
           if (lout) s4c_wait_ge(done + w + 1, (int)t - D + 2, bad);
         }
+        const bool stk_row = dc.stack && s >= 2;
+        const double bpc = (double)dc.bp_c;
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
           // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
@@ -1061,35 +1095,33 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           const double G3n = wave_shl1(G3c[c], hg);
           const double A2 = wave_shl1(Am2[c], ha);
           const int k = lane + 64 * c;
-          if (k <= kmax) {
-            // this plane: G1 = B' (formed by the plane (i+1, j)), G0 (:85-111)
-            const double G1 = dc.first ? 0.0 : wrap_in ? cr.Bw[c] : lin[k];
-            double G0 = cr.A[c] * g;
-            G0 += G1;
-            out[k] = G0;
-            if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
-              double g3 = G3n * g;
-              if (dc.stack && s >= 2) {
-                const float bp_kl = cr.bp[c];
-                if (bp_kl > bound) {
-                  const double g0 = A2;
-                  if (((xkm >> c) & 1u) && cr.yl[c] == dc.xcj) {
-                    ksrc += g0 * stk * (double)dc.bp_c * (double)bp_kl;
-                    g3 += g0;
-                  } else {
-                    ksrc += g0 * stk * sub * (double)dc.bp_c * (double)bp_kl;
-                  }
-                }
-              }
-              double g2 = G2c[c] * g;
-              g2 += g3;
-              double Bn = G1 * g;
-              Bn += g2;
-              if (lout) lout[k] = Bn;
-              else wrapb[ro + k] = Bn;
-              G2c[c] = g2;
-              G3c[c] = g3;
+          // this plane: G1 = B' (formed by the plane (i+1, j)), G0 (:85-111)
+          const double G1 = dc.first ? 0.0 : wrap_in ? cr.Bw[c] : lin[k];
+          double G0 = cr.A[c] * g;
+          G0 += G1;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, G0), ro_out, lane * 8, c * 512, 0);
+          if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
+            double g3 = G3n * g;
+            if (stk_row) {
+              const float bp_kl = cr.bp[c];
+              const bool src = bp_kl > bound && k <= kmax;
+              const bool match = ((xkm >> c) & 1u) && cr.yl[c] == dc.xcj;
+              const double g0 = A2;
+              // the reference's products in its order; +0 where no source
+              const double t0 = g0 * stk;
+              const double tm = match ? t0 : t0 * sub;
+              const double term = tm * bpc * (double)bp_kl;
+              ksrc += src ? term : 0.0;
+              g3 += src && match ? g0 : 0.0;
             }
+            double g2 = G2c[c] * g;
+            g2 += g3;
+            double Bn = G1 * g;
+            Bn += g2;
+            if (lout) lout[k] = Bn;
+            else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, Bn), ro_wrap, lane * 8, c * 512, 0);
+            G2c[c] = g2;
+            G3c[c] = g3;
           }
         }
 #pragma unroll
