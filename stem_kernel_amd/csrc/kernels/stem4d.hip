@@ -52,6 +52,17 @@ __device__ __forceinline__ int row_off(int m, int d2) {
   return r;
 }
 
+// A range-checked buffer over `bytes` from `base` (wave-uniform): loads past
+// the range return 0, stores past it are dropped -- a row's slots need no
+// per-slot guard, so a step is straight-line code.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s4c_rsrc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
+}
+typedef unsigned int s4c_u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+
 // BAND: partial_dp (stem_kernel.cpp:113-280) with the -b band constraints:
 // cells outside the band stay zero, K0 past c_high[j-1] and K1 below
 // c_low[i+1] take the reference's boundary approximations.
@@ -573,6 +584,11 @@ __global__ void __launch_bounds__(256) sk_stem4d_gsum_kernel(Stem4dLaunch P) {
 // go to its own accumulator acc[i].  Single k tile (|y| < 512; the host runs
 // the K-sum kernel otherwise).  Plane layout: G0 at 0, B' (for the plane
 // (i-1, j)) at cp.
+// SK4P_RANGE: the span kernel's rows as straight-line slots over
+// range-checked buffers (0: per-slot guards, A/B)
+#ifndef SK4P_RANGE
+#define SK4P_RANGE 1
+#endif
 // SK4P_WPE (build-time): ask the register allocator for that many waves per
 // SIMD (4: <= 128 VGPRs)
 #ifdef SK4P_WPE
@@ -631,11 +647,12 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
   const bool cons = i >= 1;
   float bp_c = 0.0f;
   uint8_t xci = 0, xcj = 0;
-  if (cons) {
+  if (cons) {  // (wave-uniform: into SGPRs)
     const int e = d1;
-    bp_c = bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (i - 1)];
-    xci = xs[i - 1];
-    xcj = xs[j - 1];
+    bp_c = __uint_as_float(__builtin_amdgcn_readfirstlane(
+        __float_as_uint(bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (i - 1)])));
+    xci = (uint8_t)__builtin_amdgcn_readfirstlane(xs[i - 1]);
+    xcj = (uint8_t)__builtin_amdgcn_readfirstlane(xs[j - 1]);
   }
   const bool stack_c = cons && bp_c > bound;
   const double stk = P.stack, sub = P.subst;
@@ -672,6 +689,29 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
     const int kmax = m - d2;
     const int e2 = d2 - 1;
     const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+#if SK4P_RANGE
+    // range-checked buffers: loads past kmax return 0, no per-slot guards
+    const int nk = kmax + 1;
+    const __amdgpu_buffer_rsrc_t ra = s4c_rsrc(A + Rd, nk * 8);
+    const __amdgpu_buffer_rsrc_t rb = s4c_rsrc(B + cp + Rd, nk * 8);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      r.A[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, lane * 8, c * 512, 0));
+      r.Bp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb, lane * 8, c * 512, 0));
+      r.bp[c] = 0.0f;
+      r.yl[c] = 0;
+    }
+    if (stack_c) {
+      const __amdgpu_buffer_rsrc_t rp = s4c_rsrc(bpy + ye, nk * 4);
+      const __amdgpu_buffer_rsrc_t ry = s4c_rsrc(ys + d2 - 1, nk);
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        r.bp[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, lane * 4, c * 256, 0));
+        r.yl[c] = __builtin_amdgcn_raw_buffer_load_b8(ry, lane, c * 64, 0);
+      }
+    }
+    return;
+#endif
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + 64 * c;
@@ -711,6 +751,54 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
       A2[c] = wave_shl1(Am2[c], ha);
     }
     const int kmax = m - d2;
+#if SK4P_RANGE
+    {  // straight-line slots (as in sk_stem4d_col_kernel): stores past kmax are
+       // dropped by the buffer range, lanes past it feed no valid cell and add
+       // nothing to K
+      const __amdgpu_buffer_rsrc_t rg = s4c_rsrc(cur + R, (kmax + 1) * 8);
+      const __amdgpu_buffer_rsrc_t rn = s4c_rsrc(cur + cp + R, (kmax + 1) * 8);
+      const bool stk_row = stack_c && d2 >= 2;
+      const double bpc = (double)bp_c;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int k = k0 + 64 * c;
+        const double G1 = cr.Bp[c];
+        double G0 = cr.A[c] * g;
+        G0 += G1;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, G0), rg, lane * 8, c * 512, 0);
+        if (cons) {
+          double g3 = G3n[c] * g;
+          if (stk_row) {
+            const float bp_kl = cr.bp[c];
+            const bool src = bp_kl > bound && k <= kmax;
+            const bool match = xci == yk[c] && xcj == cr.yl[c];
+            const double g0 = A2[c];
+            const double t0 = g0 * stk;
+            const double tm = match ? t0 : t0 * sub;
+            const double term = tm * bpc * (double)bp_kl;
+            ksrc += src ? term : 0.0;
+            g3 += src && match ? g0 : 0.0;
+          }
+          double g2 = G2c[c] * g;
+          g2 += g3;
+          double Bn = G1 * g;
+          Bn += g2;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, Bn), rn, lane * 8, c * 512, 0);
+          G2c[c] = g2;
+          G3c[c] = g3;
+        }
+      }
+    }
+    if (SK4P_RANGE) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        Am2[c] = Am1[c];
+        Am1[c] = cr.A[c];
+      }
+      R = Rn;
+      continue;
+    }
+#endif
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + 64 * c;
@@ -842,16 +930,6 @@ __device__ __forceinline__ void s4c_wait_ge(const int* done, int v, bool& bad) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// A range-checked buffer over `bytes` from `base` (wave-uniform): loads past
-// the range return 0, stores past it are dropped -- a row's slots need no
-// per-slot guard, so a step is straight-line code.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t s4c_rsrc(const void* base, int bytes) {
-  const uint64_t a = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
-}
-typedef unsigned int s4c_u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
 
 __device__ __forceinline__ int s4c_cols(int j, int F) { return j > F + SK4C_PF ? j : F + SK4C_PF; }
 

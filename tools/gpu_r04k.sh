@@ -16,6 +16,8 @@ run ns SK_HOST_STATS=1 python3 -u bench.py --config ns
 grep "\[sk" $OUT/ns.log | head -12
 run c4 python3 -u bench.py --config c4 --no-cpu-baseline
 run c3 python3 -u bench.py --config c3 --no-cpu-baseline
+run c3_prold SK_LIB_PATH=$PWD/build/libsk_prold.so python3 -u bench.py --config c3 --no-cpu-baseline
+run c3_b python3 -u bench.py --config c3 --no-cpu-baseline
 run c2 python3 -u bench.py --config c2 --no-cpu-baseline
 run c5 python3 -u bench.py --config c5 --no-cpu-baseline
 # column kernel: full-barrier interval F (SK4C_F) sweep
