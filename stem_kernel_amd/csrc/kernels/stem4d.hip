@@ -54,7 +54,8 @@ __device__ __forceinline__ int row_off(int m, int d2) {
 
 // A range-checked buffer over `bytes` from `base` (wave-uniform): loads past
 // the range return 0, stores past it are dropped -- a row's slots need no
-// per-slot guard, so a step is straight-line code.
+// per-slot guard, so a step is straight-line code.  The whole element offset
+// goes in the VGPR offset (the SGPR offset is not range-checked on gfx9).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t s4c_rsrc(const void* base, int bytes) {
   const uint64_t a = (uint64_t)base;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
@@ -696,8 +697,8 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
     const __amdgpu_buffer_rsrc_t rb = s4c_rsrc(B + cp + Rd, nk * 8);
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      r.A[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, lane * 8, c * 512, 0));
-      r.Bp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb, lane * 8, c * 512, 0));
+      r.A[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, (lane + 64 * c) * 8, 0, 0));
+      r.Bp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb, (lane + 64 * c) * 8, 0, 0));
       r.bp[c] = 0.0f;
       r.yl[c] = 0;
     }
@@ -706,8 +707,8 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
       const __amdgpu_buffer_rsrc_t ry = s4c_rsrc(ys + d2 - 1, nk);
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
-        r.bp[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, lane * 4, c * 256, 0));
-        r.yl[c] = __builtin_amdgcn_raw_buffer_load_b8(ry, lane, c * 64, 0);
+        r.bp[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, (lane + 64 * c) * 4, 0, 0));
+        r.yl[c] = __builtin_amdgcn_raw_buffer_load_b8(ry, lane + 64 * c, 0, 0);
       }
     }
     return;
@@ -765,7 +766,7 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
         const double G1 = cr.Bp[c];
         double G0 = cr.A[c] * g;
         G0 += G1;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, G0), rg, lane * 8, c * 512, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, G0), rg, (lane + 64 * c) * 8, 0, 0);
         if (cons) {
           double g3 = G3n[c] * g;
           if (stk_row) {
@@ -783,7 +784,7 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
           g2 += g3;
           double Bn = G1 * g;
           Bn += g2;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, Bn), rn, lane * 8, c * 512, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, Bn), rn, (lane + 64 * c) * 8, 0, 0);
           G2c[c] = g2;
           G3c[c] = g3;
         }
@@ -1048,12 +1049,12 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       const __amdgpu_buffer_rsrc_t ra = s4c_rsrc(planes + (int64_t)d.i * cp + ro, nk * 8);
 #pragma unroll
       for (int c = 0; c < CPL; ++c)
-        r.A[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, lane * 8, c * 512, 0));
+        r.A[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, (lane + 64 * c) * 8, 0, 0));
       if (w == 0) {  // the round wrap's B'
         const __amdgpu_buffer_rsrc_t rw = s4c_rsrc(wrapb + ro, nk * 8);
 #pragma unroll
         for (int c = 0; c < CPL; ++c)
-          r.Bw[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rw, lane * 8, c * 512, 0));
+          r.Bw[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rw, (lane + 64 * c) * 8, 0, 0));
       }
     }
     if (d.stack) {
@@ -1061,8 +1062,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       const __amdgpu_buffer_rsrc_t ry = s4c_rsrc(ys + s - 1, nk);
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
-        r.bp[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, lane * 4, c * 256, 0));
-        r.yl[c] = __builtin_amdgcn_raw_buffer_load_b8(ry, lane, c * 64, 0);
+        r.bp[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (lane + 64 * c) * 4, 0, 0));
+        r.yl[c] = __builtin_amdgcn_raw_buffer_load_b8(ry, lane + 64 * c, 0, 0);
       }
     }
   };
@@ -1177,7 +1178,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           const double G1 = dc.first ? 0.0 : wrap_in ? cr.Bw[c] : lin[k];
           double G0 = cr.A[c] * g;
           G0 += G1;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, G0), ro_out, lane * 8, c * 512, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, G0), ro_out, (lane + 64 * c) * 8, 0, 0);
           if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
             double g3 = G3n * g;
             if (stk_row) {
@@ -1197,7 +1198,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
             double Bn = G1 * g;
             Bn += g2;
             if (lout) lout[k] = Bn;
-            else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, Bn), ro_wrap, lane * 8, c * 512, 0);
+            else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, Bn), ro_wrap, (lane + 64 * c) * 8, 0, 0);
             G2c[c] = g2;
             G3c[c] = g3;
           }
