@@ -63,6 +63,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t s4c_rsrc(const void* base, int
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
 }
 typedef unsigned int s4c_u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+// slot c (elements 64c .. 64c + 63) of a row of nk valid elements: a
+// buffer per slot, lane offset in the VGPR (range-checked), so the slot
+// offset costs no VGPR
+template <class T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s4c_slot(const T* base, int nk, int c) {
+  return s4c_rsrc(base + 64 * c, (nk > 64 * c ? nk - 64 * c : 0) * (int)sizeof(T));
+}
+__device__ __forceinline__ double s4c_ld64(const double* base, int nk, int c, int lane) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(s4c_slot(base, nk, c), lane * 8, 0, 0));
+}
+__device__ __forceinline__ float s4c_ld32(const float* base, int nk, int c, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s4c_slot(base, nk, c), lane * 4, 0, 0));
+}
+__device__ __forceinline__ uint8_t s4c_ld8(const uint8_t* base, int nk, int c, int lane) {
+  return __builtin_amdgcn_raw_buffer_load_b8(s4c_slot(base, nk, c), lane, 0, 0);
+}
+__device__ __forceinline__ void s4c_st64(double* base, int nk, int c, int lane, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, v), s4c_slot(base, nk, c), lane * 8, 0, 0);
+}
 
 // BAND: partial_dp (stem_kernel.cpp:113-280) with the -b band constraints:
 // cells outside the band stay zero, K0 past c_high[j-1] and K1 below
@@ -693,22 +712,18 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 #if SK4P_RANGE
     // range-checked buffers: loads past kmax return 0, no per-slot guards
     const int nk = kmax + 1;
-    const __amdgpu_buffer_rsrc_t ra = s4c_rsrc(A + Rd, nk * 8);
-    const __amdgpu_buffer_rsrc_t rb = s4c_rsrc(B + cp + Rd, nk * 8);
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      r.A[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, (lane + 64 * c) * 8, 0, 0));
-      r.Bp[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rb, (lane + 64 * c) * 8, 0, 0));
+      r.A[c] = s4c_ld64(A + Rd, nk, c, lane);
+      r.Bp[c] = s4c_ld64(B + cp + Rd, nk, c, lane);
       r.bp[c] = 0.0f;
       r.yl[c] = 0;
     }
     if (stack_c) {
-      const __amdgpu_buffer_rsrc_t rp = s4c_rsrc(bpy + ye, nk * 4);
-      const __amdgpu_buffer_rsrc_t ry = s4c_rsrc(ys + d2 - 1, nk);
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
-        r.bp[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, (lane + 64 * c) * 4, 0, 0));
-        r.yl[c] = __builtin_amdgcn_raw_buffer_load_b8(ry, lane + 64 * c, 0, 0);
+        r.bp[c] = s4c_ld32(bpy + ye, nk, c, lane);
+        r.yl[c] = s4c_ld8(ys + d2 - 1, nk, c, lane);
       }
     }
     return;
@@ -756,8 +771,6 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
     {  // straight-line slots (as in sk_stem4d_col_kernel): stores past kmax are
        // dropped by the buffer range, lanes past it feed no valid cell and add
        // nothing to K
-      const __amdgpu_buffer_rsrc_t rg = s4c_rsrc(cur + R, (kmax + 1) * 8);
-      const __amdgpu_buffer_rsrc_t rn = s4c_rsrc(cur + cp + R, (kmax + 1) * 8);
       const bool stk_row = stack_c && d2 >= 2;
       const double bpc = (double)bp_c;
 #pragma unroll
@@ -766,7 +779,7 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
         const double G1 = cr.Bp[c];
         double G0 = cr.A[c] * g;
         G0 += G1;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, G0), rg, (lane + 64 * c) * 8, 0, 0);
+        s4c_st64(cur + R, kmax + 1, c, lane, G0);
         if (cons) {
           double g3 = G3n[c] * g;
           if (stk_row) {
@@ -784,7 +797,7 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
           g2 += g3;
           double Bn = G1 * g;
           Bn += g2;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, Bn), rn, (lane + 64 * c) * 8, 0, 0);
+          s4c_st64(cur + cp + R, kmax + 1, c, lane, Bn);
           G2c[c] = g2;
           G3c[c] = g3;
         }
@@ -1046,24 +1059,18 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
 #pragma unroll
       for (int c = 0; c < CPL; ++c) r.A[c] = lane + 64 * c < nk ? gs : 0.0;
     } else {
-      const __amdgpu_buffer_rsrc_t ra = s4c_rsrc(planes + (int64_t)d.i * cp + ro, nk * 8);
 #pragma unroll
-      for (int c = 0; c < CPL; ++c)
-        r.A[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, (lane + 64 * c) * 8, 0, 0));
+      for (int c = 0; c < CPL; ++c) r.A[c] = s4c_ld64(planes + (int64_t)d.i * cp + ro, nk, c, lane);
       if (w == 0) {  // the round wrap's B'
-        const __amdgpu_buffer_rsrc_t rw = s4c_rsrc(wrapb + ro, nk * 8);
 #pragma unroll
-        for (int c = 0; c < CPL; ++c)
-          r.Bw[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rw, (lane + 64 * c) * 8, 0, 0));
+        for (int c = 0; c < CPL; ++c) r.Bw[c] = s4c_ld64(wrapb + ro, nk, c, lane);
       }
     }
     if (d.stack) {
-      const __amdgpu_buffer_rsrc_t rb = s4c_rsrc(bpy + ye, nk * 4);
-      const __amdgpu_buffer_rsrc_t ry = s4c_rsrc(ys + s - 1, nk);
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
-        r.bp[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (lane + 64 * c) * 4, 0, 0));
-        r.yl[c] = __builtin_amdgcn_raw_buffer_load_b8(ry, lane + 64 * c, 0, 0);
+        r.bp[c] = s4c_ld32(bpy + ye, nk, c, lane);
+        r.yl[c] = s4c_ld8(ys + s - 1, nk, c, lane);
       }
     }
   };
@@ -1152,11 +1159,11 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
         // there), and add nothing to K (their bp loads are 0 and masked)
         const int ro = row_off(m, s);
         const int nk = kmax + 1;
-        const __amdgpu_buffer_rsrc_t ro_out = s4c_rsrc(planes + (int64_t)dc.i * cp + ro, nk * 8);
+        double* const gout = planes + (int64_t)dc.i * cp + ro;
         const bool wrap_in = w == 0;
         const double* lin = link_in + ((t - 1) & (D - 1)) * TW;
         double* lout = dc.cons && w + 1 < W ? link_out + (t & (D - 1)) * TW : nullptr;
-        const __amdgpu_buffer_rsrc_t ro_wrap = s4c_rsrc(wrapb + ro, dc.cons && !lout ? nk * 8 : 0);
+        const int nk_wrap = dc.cons && !lout ? nk : 0;
         if (SK4C_P2P) {
           if (!dc.first && !wrap_in) s4c_wait_ge(done + w - 1, (int)t, bad);
           if (lout) s4c_wait_ge(done + w + 1, (int)t - D + 2, bad);
@@ -1178,7 +1185,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           const double G1 = dc.first ? 0.0 : wrap_in ? cr.Bw[c] : lin[k];
           double G0 = cr.A[c] * g;
           G0 += G1;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, G0), ro_out, (lane + 64 * c) * 8, 0, 0);
+          s4c_st64(gout, nk, c, lane, G0);
           if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
             double g3 = G3n * g;
             if (stk_row) {
@@ -1198,7 +1205,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
             double Bn = G1 * g;
             Bn += g2;
             if (lout) lout[k] = Bn;
-            else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, Bn), ro_wrap, (lane + 64 * c) * 8, 0, 0);
+            else s4c_st64(wrapb + ro, nk_wrap, c, lane, Bn);
             G2c[c] = g2;
             G3c[c] = g3;
           }
