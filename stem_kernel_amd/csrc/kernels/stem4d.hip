@@ -917,6 +917,9 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 // -- so a wave held up by a late row delays its consumers alone and not the
 // whole workgroup.  Every wait is on a strictly earlier step, so there is no
 // cycle; a wait that runs past ~0.5 s gives up and the pair's K is NaN.
+#ifndef SK4C_RANGE  // the row step as straight-line slots over range-checked buffers (0: per-slot guards)
+#define SK4C_RANGE 1
+#endif
 #ifndef SK4C_P2P  // off: 278 against 305 pairs/s lockstep on C3 (r04e)
 #define SK4C_P2P 0
 #endif
@@ -1040,6 +1043,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     uint8_t yl[CPL];  // y[l-1], compared at the row's step: an operation on a
                       // loaded value here would wait for the load (no prefetch)
   };
+#if SK4C_RANGE
   auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
     // cells k <= m - s of the row; past them every load returns 0 (buffer
     // range), the branches below are on wave-uniform values
@@ -1074,6 +1078,33 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       }
     }
   };
+#else
+  auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
+    const int kmax = m - s;
+    const int ro = row_off(m, s);
+    const int e2 = s - 1;
+    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+    const double* Ai = planes + (int64_t)d.i * cp + ro;
+    const bool wrap_in = w == 0 && !d.first;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int k = lane + 64 * c;
+      r.A[c] = 0.0;
+      r.Bw[c] = 0.0;
+      r.bp[c] = 0.0f;
+      r.yl[c] = 0;
+
+      if (d.on && s >= 1 && k <= kmax) {
+        r.A[c] = d.first ? gpow[s] : Ai[k];  // G0(j-1, j-1) = g^(l-k)
+        if (wrap_in) r.Bw[c] = wrapb[ro + k];
+        if (d.stack) {
+          r.bp[c] = bpy[ye + k];
+          r.yl[c] = ys[k + s - 1];
+        }
+      }
+    }
+  };
+#endif
 
   uint32_t yk = 0;  // y[k] of slot c in byte c (CPL <= 4), else reread per plane
 #pragma unroll
@@ -1152,6 +1183,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           Am1[c] = (dc.stack && k <= m) ? gpow[dc.j - 1 - dc.i] : 0.0;  // G0(i, j-1, l, l)
           Am2[c] = G2c[c] = G3c[c] = 0.0;
         }
+#if SK4C_RANGE
       } else {
         // Straight-line slots: lanes past kmax compute values that are never
         // stored (the output buffers' range ends at kmax) nor read by a valid
@@ -1210,6 +1242,60 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
             G3c[c] = g3;
           }
         }
+#else
+      } else {
+        const int ro = row_off(m, s);
+        double* __restrict__ out = planes + (int64_t)dc.i * cp + ro;
+        const bool wrap_in = w == 0;
+        const double* lin = link_in + ((t - 1) & (D - 1)) * TW;
+        double* lout = dc.cons && w + 1 < W ? link_out + (t & (D - 1)) * TW : nullptr;
+        if (SK4C_P2P) {
+          if (!dc.first && !wrap_in) s4c_wait_ge(done + w - 1, (int)t, bad);
+          if (lout) s4c_wait_ge(done + w + 1, (int)t - D + 2, bad);
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
+          // (k+1, l-1): the next lane's, or the next slot's lane 0 -- formed
+          // here, before slot c's update, while slot c+1's is still the old
+          // row's (short live ranges: the registers of 4 waves per SIMD)
+          const double hg = c + 1 < CPL ? bcast_lane0(G3c[c + 1 < CPL ? c + 1 : c]) : 0.0;
+          const double ha = c + 1 < CPL ? bcast_lane0(Am2[c + 1 < CPL ? c + 1 : c]) : 0.0;
+          const double G3n = wave_shl1(G3c[c], hg);
+          const double A2 = wave_shl1(Am2[c], ha);
+          const int k = lane + 64 * c;
+          if (k <= kmax) {
+            // this plane: G1 = B' (formed by the plane (i+1, j)), G0 (:85-111)
+            const double G1 = dc.first ? 0.0 : wrap_in ? cr.Bw[c] : lin[k];
+            double G0 = cr.A[c] * g;
+            G0 += G1;
+            out[k] = G0;
+            if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
+              double g3 = G3n * g;
+              if (dc.stack && s >= 2) {
+                const float bp_kl = cr.bp[c];
+                if (bp_kl > bound) {
+                  const double g0 = A2;
+                  if (((xkm >> c) & 1u) && cr.yl[c] == dc.xcj) {
+                    ksrc += g0 * stk * (double)dc.bp_c * (double)bp_kl;
+                    g3 += g0;
+                  } else {
+                    ksrc += g0 * stk * sub * (double)dc.bp_c * (double)bp_kl;
+                  }
+                }
+              }
+              double g2 = G2c[c] * g;
+              g2 += g3;
+              double Bn = G1 * g;
+              Bn += g2;
+              if (lout) lout[k] = Bn;
+              else wrapb[ro + k] = Bn;
+              G2c[c] = g2;
+              G3c[c] = g3;
+            }
+          }
+        }
+#endif
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
           Am2[c] = Am1[c];

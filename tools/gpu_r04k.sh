@@ -22,6 +22,7 @@ run c2 python3 -u bench.py --config c2 --no-cpu-baseline
 run c5 python3 -u bench.py --config c5 --no-cpu-baseline
 # column kernel: full-barrier interval F (SK4C_F) sweep
 run c3col_f8 SK4_COL=1 python3 -u bench.py --config c3 --no-cpu-baseline
+run c3col_old SK4_COL=1 SK_LIB_PATH=$PWD/build/libsk_prold.so python3 -u bench.py --config c3 --no-cpu-baseline
 run c3col_f16 SK4_COL=1 SK4C_F=16 python3 -u bench.py --config c3 --no-cpu-baseline
 run c3col_f32 SK4_COL=1 SK4C_F=32 python3 -u bench.py --config c3 --no-cpu-baseline
 # C4 kernel trace: gaps between consecutive BPLA launches (uploads on the copy stream)
