@@ -605,9 +605,10 @@ __global__ void __launch_bounds__(256) sk_stem4d_gsum_kernel(Stem4dLaunch P) {
 // the K-sum kernel otherwise).  Plane layout: G0 at 0, B' (for the plane
 // (i-1, j)) at cp.
 // SK4P_RANGE: the span kernel's rows as straight-line slots over
-// range-checked buffers (0: per-slot guards, A/B)
+// range-checked buffers -- off: 318.5 / 315.8 against 336.5 pairs/s with the
+// per-slot guards on one box (r04k), although it fits 128 VGPRs
 #ifndef SK4P_RANGE
-#define SK4P_RANGE 1
+#define SK4P_RANGE 0
 #endif
 // SK4P_WPE (build-time): ask the register allocator for that many waves per
 // SIMD (4: <= 128 VGPRs)
@@ -917,8 +918,8 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 // -- so a wave held up by a late row delays its consumers alone and not the
 // whole workgroup.  Every wait is on a strictly earlier step, so there is no
 // cycle; a wait that runs past ~0.5 s gives up and the pair's K is NaN.
-#ifndef SK4C_RANGE  // the row step as straight-line slots over range-checked buffers (0: per-slot guards)
-#define SK4C_RANGE 1
+#ifndef SK4C_RANGE  // 1: the row step as straight-line slots over range-checked buffers
+#define SK4C_RANGE 0   // (off: 260 against 306 pairs/s with the per-slot guards, r04k)
 #endif
 #ifndef SK4C_P2P  // off: 278 against 305 pairs/s lockstep on C3 (r04e)
 #define SK4C_P2P 0
