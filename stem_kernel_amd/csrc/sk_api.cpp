@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <functional>
 #include <memory>
 #include <new>
 #include <numeric>
@@ -525,7 +526,7 @@ static void assign_sweep_lanes(const std::vector<int>& take, const std::vector<u
   } while (0)
 
 // --------------------------------------------------------------- packing
-int pack_dataset(sk_dataset* ds, std::string& err) {
+int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* after_x = nullptr) {
   HostPack& P = ds->pack;
   const bool tstats = std::getenv("SK_HOST_STATS") != nullptr;
   auto tnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -1357,6 +1358,9 @@ int pack_dataset(sk_dataset* ds, std::string& err) {
               s_nodes, s_rows, s_nost, s_slots, s_st, s_slab, s_gam, s_phi, s_reg);
     }
   }
+  // the x-role arrays are final: the caller may start uploading them while
+  // the y-role records are formed (sk_dataset_upload)
+  if (after_x) (*after_x)();
   const double tp2 = tnow();
   {
     std::vector<YOut> yo(yjobs.size());
@@ -3295,45 +3299,99 @@ int sk_dataset_bpla_weights(const sk_dataset* ds, int i, float* p_left, float* p
 int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   if (!ctx || !ds) return SK_ERR_INVALID;
   if (ds->uploaded) return ds->device == ctx->device ? SK_OK : fail(ctx, SK_ERR_INVALID, "dataset bound to another device");
-  std::string err;
-  const auto tu0 = std::chrono::steady_clock::now();
-  int rc = pack_dataset(ds, err);
-  if (rc) return fail(ctx, rc, err);
-  const auto tu1 = std::chrono::steady_clock::now();
   SK_HIP(ctx, hipSetDevice(ctx->device));
+  std::string err;
   HostPack& P = ds->pack;
-  P.xr_ch.insert(P.xr_ch.end(), 8, 0u);  // the kernel prefetches 4 records past a row
-  P.xg_ch.insert(P.xg_ch.end(), 8, 0u);
   DevSet& D = ds->dev;
   DeviceBuffers& B = ds->buf;
+  const bool stats = std::getenv("SK_HOST_STATS") != nullptr;
+  const auto tu0 = std::chrono::steady_clock::now();
+  // the x-role arrays go to the device on a second host thread while the
+  // y-role records are formed (pack_dataset calls after_x between the two)
+  std::thread xt;
+  hipError_t xe = hipSuccess;
+  double x_ms = 0.0;
+  auto up_x = [&]() -> hipError_t {
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return e;
+#define SK_UPX(f, d) \
+  if ((e = upload(B, P.f, &D.d)) != hipSuccess) return e;
+    SK_UPX(ex_nl, ex_nl)
+    SK_UPX(ex_node_base, ex_node_base)
+    SK_UPX(ex_edge_base, ex_edge_base)
+    SK_UPX(ex_bpf_base, ex_bpf_base)
+    SK_UPX(ex_lvl_base, ex_lvl_base)
+    SK_UPX(ex_nlev, ex_nlev)
+    SK_UPX(ex_nseqs, ex_nseqs)
+    SK_UPX(ex_len, ex_len)
+    SK_UPX(ex_pos_base, ex_pos_base)
+    SK_UPX(ex_has_w, ex_has_w)
+    SK_UPX(nd_a, nd_a)
+    SK_UPX(nd_b, nd_b)
+    SK_UPX(nd_c, nd_c)
+    SK_UPX(nd_w, nd_w)
+    SK_UPX(nd_nbp, nd_nbp)
+    SK_UPX(nd_P, nd_P)
+    SK_UPX(ed, ed)
+    SK_UPX(bpf_code, bpf_code)
+    SK_UPX(bpf_p, bpf_p)
+    SK_UPX(lvl, lvl)
+    SK_UPX(pos_prof, pos_prof)
+    SK_UPX(pos_w, pos_w)
+    SK_UPX(pos_chr, pos_chr)
+    SK_UPX(pos_lru, pos_lru)
+    SK_UPX(ex_nslots, ex_nslots)
+    SK_UPX(ex_xch_base, ex_xch_base)
+    SK_UPX(xrow, xrow)
+    SK_UPX(xr_node, xr_node)
+    SK_UPX(xr_ch, xr_ch)
+    SK_UPX(xgrow, xgrow)
+    SK_UPX(xg_node, xg_node)
+    SK_UPX(xg_ch, xg_ch)
+    SK_UPX(xg_clg, xg_clg)
+    SK_UPX(xg_cpf, xg_cpf)
+    SK_UPX(ex_xg_base, ex_xg_base)
+    SK_UPX(ex_nlxg, ex_nlxg)
+    SK_UPX(ex_xgch_base, ex_xgch_base)
+    SK_UPX(gr_info, gr_info)
+    SK_UPX(gr_pf, gr_pf)
+    SK_UPX(gr_P, gr_P)
+    SK_UPX(ex_gapless, ex_gapless)
+    SK_UPX(gam_key, gam_key)
+    SK_UPX(xg_cty, xg_cty)
+    SK_UPX(gra_gidx, gra_gidx)
+    SK_UPX(gra_row, gra_row)
+    SK_UPX(phk_idx, phk_idx)
+    SK_UPX(phi_al, phi_al)
+    SK_UPX(phi_g, phi_g)
+    {
+      std::vector<int32_t> grb = P.ex_gr_base;
+      grb.push_back((int32_t)P.gr_info.size());
+      if ((e = upload(B, grb, &D.ex_gr_base)) != hipSuccess) return e;
+      std::vector<int32_t> b1 = P.ex_gra_base, b2 = P.ex_phk_base;
+      b1.push_back((int32_t)P.gra_gidx.size());
+      b2.push_back((int32_t)P.phk_idx.size());
+      if ((e = upload(B, b1, &D.ex_gra_base)) != hipSuccess) return e;
+      if ((e = upload(B, b2, &D.ex_phk_base)) != hipSuccess) return e;
+    }
+#undef SK_UPX
+    return hipSuccess;
+  };
+  const std::function<void()> after_x = [&]() {
+    P.xr_ch.insert(P.xr_ch.end(), 8, 0u);  // the kernel prefetches 4 records past a row
+    P.xg_ch.insert(P.xg_ch.end(), 8, 0u);
+    xt = std::thread([&]() {
+      const auto t0 = std::chrono::steady_clock::now();
+      xe = up_x();
+      x_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+  };
+  int rc = pack_dataset(ds, err, &after_x);
+  if (xt.joinable()) xt.join();
+  if (rc) return fail(ctx, rc, err);
+  SK_HIP(ctx, xe);
+  const auto tu1 = std::chrono::steady_clock::now();
   D.n_examples = (int32_t)ds->ex.size();
-  SK_HIP(ctx, upload(B, P.ex_nl, &D.ex_nl));
-  SK_HIP(ctx, upload(B, P.ex_node_base, &D.ex_node_base));
-  SK_HIP(ctx, upload(B, P.ex_edge_base, &D.ex_edge_base));
-  SK_HIP(ctx, upload(B, P.ex_bpf_base, &D.ex_bpf_base));
-  SK_HIP(ctx, upload(B, P.ex_lvl_base, &D.ex_lvl_base));
-  SK_HIP(ctx, upload(B, P.ex_nlev, &D.ex_nlev));
-  SK_HIP(ctx, upload(B, P.ex_nseqs, &D.ex_nseqs));
-  SK_HIP(ctx, upload(B, P.ex_len, &D.ex_len));
-  SK_HIP(ctx, upload(B, P.ex_pos_base, &D.ex_pos_base));
-  SK_HIP(ctx, upload(B, P.ex_has_w, &D.ex_has_w));
-  SK_HIP(ctx, upload(B, P.nd_a, &D.nd_a));
-  SK_HIP(ctx, upload(B, P.nd_b, &D.nd_b));
-  SK_HIP(ctx, upload(B, P.nd_c, &D.nd_c));
-  SK_HIP(ctx, upload(B, P.nd_w, &D.nd_w));
-  SK_HIP(ctx, upload(B, P.nd_nbp, &D.nd_nbp));
-  SK_HIP(ctx, upload(B, P.nd_P, &D.nd_P));
-  SK_HIP(ctx, upload(B, P.ed, &D.ed));
-  SK_HIP(ctx, upload(B, P.bpf_code, &D.bpf_code));
-  SK_HIP(ctx, upload(B, P.bpf_p, &D.bpf_p));
-  SK_HIP(ctx, upload(B, P.lvl, &D.lvl));
-  SK_HIP(ctx, upload(B, P.pos_prof, &D.pos_prof));
-  SK_HIP(ctx, upload(B, P.pos_w, &D.pos_w));
-  SK_HIP(ctx, upload(B, P.pos_chr, &D.pos_chr));
-  SK_HIP(ctx, upload(B, P.pos_lru, &D.pos_lru));
-  SK_HIP(ctx, upload(B, P.ex_nslots, &D.ex_nslots));
-  SK_HIP(ctx, upload(B, P.ex_xch_base, &D.ex_xch_base));
-  SK_HIP(ctx, upload(B, P.xrow, &D.xrow));
   SK_HIP(ctx, upload(B, P.yn_a, &D.yn_a));
   SK_HIP(ctx, upload(B, P.yn_b, &D.yn_b));
   SK_HIP(ctx, upload(B, P.yn_w, &D.yn_w));
@@ -3348,40 +3406,7 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   SK_HIP(ctx, upload(B, P.ex_ysc_base, &D.ex_ysc_base));
   SK_HIP(ctx, upload(B, P.ex_nch, &D.ex_nch));
   SK_HIP(ctx, upload(B, P.ex_ycs_base, &D.ex_ycs_base));
-  SK_HIP(ctx, upload(B, P.xr_node, &D.xr_node));
-  SK_HIP(ctx, upload(B, P.xr_ch, &D.xr_ch));
-  SK_HIP(ctx, upload(B, P.xgrow, &D.xgrow));
-  SK_HIP(ctx, upload(B, P.xg_node, &D.xg_node));
-  SK_HIP(ctx, upload(B, P.xg_ch, &D.xg_ch));
-  SK_HIP(ctx, upload(B, P.xg_clg, &D.xg_clg));
-  SK_HIP(ctx, upload(B, P.xg_cpf, &D.xg_cpf));
-  SK_HIP(ctx, upload(B, P.ex_xg_base, &D.ex_xg_base));
-  SK_HIP(ctx, upload(B, P.ex_nlxg, &D.ex_nlxg));
-  SK_HIP(ctx, upload(B, P.ex_xgch_base, &D.ex_xgch_base));
-  {
-    std::vector<int32_t> grb = P.ex_gr_base;
-    grb.push_back((int32_t)P.gr_info.size());
-    SK_HIP(ctx, upload(B, grb, &D.ex_gr_base));
-  }
-  SK_HIP(ctx, upload(B, P.gr_info, &D.gr_info));
-  SK_HIP(ctx, upload(B, P.gr_pf, &D.gr_pf));
-  SK_HIP(ctx, upload(B, P.gr_P, &D.gr_P));
-  SK_HIP(ctx, upload(B, P.ex_gapless, &D.ex_gapless));
-  SK_HIP(ctx, upload(B, P.gam_key, &D.gam_key));
   D.n_gam = (int32_t)P.gam_key.size();
-  SK_HIP(ctx, upload(B, P.xg_cty, &D.xg_cty));
-  {
-    std::vector<int32_t> b1 = P.ex_gra_base, b2 = P.ex_phk_base;
-    b1.push_back((int32_t)P.gra_gidx.size());
-    b2.push_back((int32_t)P.phk_idx.size());
-    SK_HIP(ctx, upload(B, b1, &D.ex_gra_base));
-    SK_HIP(ctx, upload(B, b2, &D.ex_phk_base));
-  }
-  SK_HIP(ctx, upload(B, P.gra_gidx, &D.gra_gidx));
-  SK_HIP(ctx, upload(B, P.gra_row, &D.gra_row));
-  SK_HIP(ctx, upload(B, P.phk_idx, &D.phk_idx));
-  SK_HIP(ctx, upload(B, P.phi_al, &D.phi_al));
-  SK_HIP(ctx, upload(B, P.phi_g, &D.phi_g));
   D.n_phi = (int32_t)P.phi_al.size();
   D.max_nl = P.max_nl;
   D.max_edges = P.max_edges;
@@ -3393,10 +3418,12 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   D.total_nodes = (int64_t)P.nd_a.size();
   ds->device = ctx->device;
   ds->uploaded = true;
-  if (std::getenv("SK_HOST_STATS")) {
+  if (stats) {
     const auto tu2 = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[sk upload] pack %.1f ms, %zu arrays %.1f MB to the device %.1f ms\n",
-                 std::chrono::duration<double, std::milli>(tu1 - tu0).count(), B.ptrs.size(), B.bytes / 1e6,
+    std::fprintf(stderr,
+                 "[sk upload] pack + x-role arrays %.1f ms (x-role transfer %.1f ms beside the y-role pack), %zu arrays "
+                 "%.1f MB in all, y-role transfer %.1f ms\n",
+                 std::chrono::duration<double, std::milli>(tu1 - tu0).count(), x_ms, B.ptrs.size(), B.bytes / 1e6,
                  std::chrono::duration<double, std::milli>(tu2 - tu1).count());
   }
   return SK_OK;
