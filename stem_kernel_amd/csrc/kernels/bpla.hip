@@ -310,6 +310,17 @@ template <bool BP, bool FULL>
 __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, const int4* ci, double* ksum,
                                                  int Ly, const BplaPos* ycol, double* bnd, const double* etab,
                                                  int lane);
+template <bool BP, bool FULL>
+__device__ __forceinline__ void bpla_fast_chunk3(const BplaLaunch& P, int np, const int4* ci, double* ksum,
+                                                 int Ly, const BplaPos* ycol, double* bnd, const double* etab,
+                                                 int lane);
+// rows per lane of the exp path (2 or 3) and a pair's rows padded to them
+#ifndef SK_BPLA_ROWS
+#define SK_BPLA_ROWS 2
+#endif
+__device__ __forceinline__ int bpla_pad_rows(int len) {
+  return SK_BPLA_ROWS == 3 ? len + (3 - len % 3) % 3 : len + (len & 1);
+}
 
 // A chunk of np pairs sharing y on one wavefront: their x rows are streamed
 // back to back as one sequence of rows (chunk row G = first row of pair p +
@@ -335,9 +346,11 @@ __device__ __forceinline__ void bpla_fast_chunk(const BplaLaunch& P, int np, con
                                                 double* bnd, const double* etab, int lane) {
   if (!SW) {  // the exp path runs two rows per lane
     if (Ly >= 64)
-      bpla_fast_chunk2<BP, true>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
+      SK_BPLA_ROWS == 3 ? bpla_fast_chunk3<BP, true>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane)
+                        : bpla_fast_chunk2<BP, true>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
     else
-      bpla_fast_chunk2<BP, false>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
+      SK_BPLA_ROWS == 3 ? bpla_fast_chunk3<BP, false>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane)
+                        : bpla_fast_chunk2<BP, false>(P, np, ci, ksum, Ly, ycol, bnd, etab, lane);
     return;
   }
   const double alpha = P.alpha, beta = P.beta, gap = P.gap, ext = P.ext;
@@ -822,6 +835,278 @@ __device__ __forceinline__ void bpla_fast_chunk2(const BplaLaunch& P, int np, co
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// SK_BPLA_ROWS 3: THREE rows per lane (rows A, B, C = 192s + 3l + 1 ..
+// + 3): the per-step shared work (y column, DPP shifts of the row above,
+// lane 63's boundary row, the window's per-lane control) is paid once per
+// three cells; pairs are padded to a multiple of three rows; row C is the
+// lane's last row (handed to lane l+1 and to the boundary row).  Same
+// operations per cell as the two-row schedule.
+template <bool BP, bool FULL>
+__device__ __forceinline__ void bpla_fast_chunk3(const BplaLaunch& P, int np, const int4* ci, double* ksum,
+                                                 int Ly, const BplaPos* ycol, double* bnd, const double* etab,
+                                                 int lane) {
+  const double ab = P.alpha * P.beta;
+  const double bg = P.beta_gap, be = P.beta_ext;
+  const int4 last = ci[np - 1];
+  const int Rt = __builtin_amdgcn_readfirstlane(last.z + bpla_pad_rows(last.y));  // padded rows
+  const int Lys = max(Ly, 64);
+  for (int j = lane; j < 3 * (Lys + 1); j += 64) bnd[j] = 0.0;  // row 0
+  if (lane < np) ksum[lane] = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (Rt == 0 || Ly == 0) return;  // no cells: K = 1
+  const int Rp = Rt / 3;           // row triples
+  const int nstrips = (Rp + 63) / 64;
+  const int T = (nstrips - 1) * Lys + ((Rp - 1) & 63) + Ly;  // steps
+  const char* ybase = reinterpret_cast<const char*>(ycol);
+
+  // row triple (chunk rows GA = 3 * Q + 1, GA + 1, GA + 2) -> pair,
+  // existence, fb, xtab index
+  auto map_pair = [&](int Q, int& pp, bool& oka, bool& okb, bool& okc, double& fbv, int& xi)
+                      __attribute__((always_inline)) {
+    const int G = 3 * Q + 1;
+    int q = 0;
+    for (int k = 1; k < np; ++k) q += G - 1 >= ci[k].z ? 1 : 0;
+    const int4 c = ci[q];
+    const int i = G - c.z;  // 1 mod 3, <= c.y when the row exists
+    oka = G <= Rt;
+    okb = oka && i + 1 <= c.y;
+    okc = oka && i + 2 <= c.y;
+    pp = q;
+    fbv = i == 1 ? 0.0 : 1.0;
+    xi = oka ? c.x + i - 1 : ci[0].x;
+  };
+  int pn, xi;
+  bool okan, okbn, okcn;
+  double fbn;
+  map_pair(lane, pn, okan, okbn, okcn, fbn, xi);
+  BplaPos xnA = P.xtab[xi], xnB = P.xtab[okbn ? xi + 1 : xi], xnC = P.xtab[okcn ? xi + 2 : xi];
+  BplaPos xA = xnA, xB = xnB, xC = xnC;
+  int p = 0;
+  bool okA = false, okB = false, okC = false;
+  double fb = 1.0, cbg = bg, cbe = be;  // row A's: 0 / 0 / 0 on a pair's first row
+  unsigned yofs = 0;
+  double aM = 0.0, aX = 0.0, aY = 0.0;  // row A at (., j-1)
+  double bY = 0.0;  // row B's Y at (., j-1) (its M + X: sB1)
+  double cM = 0.0, cX = 0.0, cY = 0.0;  // row C at (., j-1)
+  double accA = 0.0, accB = 0.0, accC = 0.0;
+
+  auto expo = [&](const BplaPos& xr, const BplaPos& yc) __attribute__((always_inline)) {
+    double s = xr.v[0] * yc.v[0];
+    s = __builtin_fma(xr.v[1], yc.v[1], s);
+    s = __builtin_fma(xr.v[2], yc.v[2], s);
+    s = __builtin_fma(xr.v[3], yc.v[3], s);
+    if (BP) {
+      // BPLAScore (bpla_kernel.cpp:55-60): float products as written
+      const float pp = f32_dot2(xr.pr, yc.pr, xr.pl, yc.pl);
+      const float uu = xr.pu * yc.pu;
+      s = __builtin_fma((double)uu, s, ab * (double)pp);
+    }
+    return fast_exp(s, etab);
+  };
+  // both cells of a step: dS = M + X + Y of the row above at (j-1) (lane
+  // l-1 sends its row B's sum, bS), u = row above at j (lane l-1's row B);
+  // c1: column 1 (left is column 0: zero).  A row's left sum M + X is
+  // shared by its Y recurrence and the diagonal sum it hands on.
+  // sB1 = bM + bX and sB2 = sB1 + bY of row B's latest outputs, carried from
+  // step to step: each is formed once per step (the row-B Y recurrence, the
+  // diagonal sum handed on, lane 63's boundary write), not once per use
+  // (three rows: row C is the lane's last -- its sums go down and to the
+  // boundary row; rows B and C take up and diagonal from the row before)
+  double sB1 = 0.0, sC1 = 0.0, sC2 = 0.0;
+  auto cells = [&](const BplaPos& yc, double dS, double uM, double uX, bool c1) __attribute__((always_inline)) {
+    const double eA = expo(xA, yc);
+    const double eB = expo(xB, yc);
+    const double eC = expo(xC, yc);
+    const double sA = aM + aX;
+    const double nMA = eA * __builtin_fma(fb, dS, 1.0);
+    const double nXA = cbg * uM + cbe * uX;
+    const double nYA = c1 ? 0.0 : bg * sA + be * aY;
+    const double nMB = __builtin_fma(eB, sA + aY, eB);  // diagonal: row A at j-1
+    const double nXB = bg * nMA + be * nXA;
+    const double nYB = c1 ? 0.0 : bg * sB1 + be * bY;
+    const double nMC = __builtin_fma(eC, sB1 + bY, eC);  // diagonal: row B at j-1
+    const double nXC = bg * nMB + be * nXB;
+    const double nYC = c1 ? 0.0 : bg * sC1 + be * cY;
+    aM = nMA;
+    aX = nXA;
+    aY = nYA;
+    bY = nYB;
+    cM = nMC;
+    cX = nXC;
+    cY = nYC;
+    accA += nMA;
+    accB += nMB;
+    accC += nMC;
+    sB1 = nMB + nXB;
+    sC1 = nMC + nXC;
+    sC2 = sC1 + nYC;
+    __asm__ volatile("" : "+v"(sC2));  // formed here, once, ahead of lane 63's write
+  };
+
+  // interior step: lane 0's column jb, every lane active
+  // (the boundary row holds {M, X, M + X + Y} of row B per column)
+  // Interior operands are read a step ahead (the y column and lane 0's
+  // boundary values of the next step land during this step's arithmetic):
+  // (yc, b*) this step's, (ycn, n*) the next step's.
+  auto iload = [&](int jb, BplaPos& yc, double& b0, double& b1, double& b2) __attribute__((always_inline)) {
+    yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+    const double* bj = bnd + 3 * jb;
+    b0 = bj[0];
+    b1 = bj[1];
+    b2 = bj[2];
+  };
+  auto interior = [&](int jb, double& dS, double& uS, const BplaPos& yc, double b0, double b1, double b2,
+                      BplaPos& ycn, double& n0, double& n1, double& n2) __attribute__((always_inline)) {
+    ycn = *reinterpret_cast<const BplaPos*>(ybase + yofs + (unsigned)sizeof(BplaPos));
+    {
+      const double* bj = bnd + 3 * (jb + 1);
+      n0 = bj[0];
+      n1 = bj[1];
+      n2 = bj[2];
+    }
+    const double uM = wave_shr1(cM, b0);
+    const double uX = wave_shr1(cX, b1);
+    uS = wave_shr1(sC2, b2);
+    cells(yc, dS, uM, uX, false);
+    if (lane == 63) {  // lane 63's column is jb - 63
+      double* bw = bnd + 3 * (jb - 63);
+      bw[0] = cM;
+      bw[1] = cX;
+      bw[2] = sC2;
+    }
+    yofs += (unsigned)sizeof(BplaPos);
+  };
+
+  // window step w of strip s: lane w starts its rows of strip s at column 1,
+  // handing its finished rows' sums to their pair (rows that exist only);
+  // lanes below are at column w - lane + 1 of strip s, lanes above at column
+  // Lys + w - lane + 1 of strip s-1
+  // FULL (Ly >= 64, so Lys = Ly): every lane computes every window step.
+  // The cells of lanes that have not started strip 0 yet are garbage that
+  // their wrap discards (sums and left / diagonal values reset, row B's left
+  // masked at column 1), and those of lanes past the last strip belong to
+  // rows that do not exist (dropped at the hand-off); lane 63's stray
+  // boundary writes in strip 0 land on columns it overwrites with the real
+  // values before lane 0 of strip 1 reads them.  Otherwise (Ly < 64: columns
+  // past Ly in every strip) the cells of columns past Ly are skipped.
+  auto window = [&](int s, int w, double& dM, double& dX, double& dS, double& uM, double& uX, double& uS)
+                    __attribute__((always_inline)) {
+    (void)dM;
+    (void)dX;
+    const bool wrap = lane == w;
+    if (wrap) {
+      // the finished rows' sums stay in the lane while its next rows belong
+      // to the same pair; they go to the pair's sum when the pair changes
+      const double h = accA + (okB ? accB : 0.0) + (okC ? accC : 0.0);
+      const bool cont = okA && okan && pn == p;
+      // (an LDS add without return: no read round trip inside the window;
+      // one lane, this wave's own sums, so the order of additions is kept)
+      if (okA && !cont) __hip_atomic_fetch_add(&ksum[p], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      accA = cont ? h : 0.0;
+      accB = accC = 0.0;
+      xA = xnA;
+      xB = xnB;
+      xC = xnC;
+      p = pn;
+      okA = okan;
+      okB = okbn;
+      okC = okcn;
+      fb = fbn;
+      cbg = bg * fbn;
+      cbe = be * fbn;
+      yofs = 0;
+      dS = 0.0;
+      aM = aX = aY = 0.0;  // row A's column 0 (row B's diagonal at column 1)
+    }
+    const int jb = w + 1;  // lane 0's column (strip s)
+    const double* bj = bnd + 3 * (jb <= Ly ? jb : 0);
+    uM = wave_shr1(cM, bj[0]);
+    uX = wave_shr1(cX, bj[1]);
+    uS = wave_shr1(sC2, bj[2]);
+    if (FULL) {
+      const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+      cells(yc, dS, uM, uX, wrap);
+      // lane 63's column: w - 62 once it wrapped (w = 63), else Lys + w - 62
+      const int j63 = w == 63 ? 1 : Lys + w - 62;
+      if (lane == 63) {
+        double* bw = bnd + 3 * j63;
+        bw[0] = cM;
+        bw[1] = cX;
+        bw[2] = sC2;
+      }
+    } else {
+      const int jl = lane <= w ? w - lane + 1 : Lys + w - lane + 1;
+      const bool on = jl <= Ly && (lane <= w ? s < nstrips : s > 0);
+      if (on) {
+        const BplaPos yc = *reinterpret_cast<const BplaPos*>(ybase + yofs);
+        cells(yc, dS, uM, uX, wrap);
+        if (lane == 63) {
+          double* bw = bnd + 3 * jl;
+          bw[0] = cM;
+          bw[1] = cX;
+          bw[2] = sC2;
+        }
+      }
+    }
+    yofs += (unsigned)sizeof(BplaPos);
+  };
+
+  // d* = values received a step earlier, u* = this step's; the unrolled
+  // pairs of steps swap their roles (no register copies)
+  double pM = 0.0, pX = 0.0, pY = 0.0, qM = 0.0, qX = 0.0, qY = 0.0;
+  for (int s = 0; s <= nstrips; ++s) {
+    const int Ws = s * Lys;
+    const int wend = min(64, T - Ws);
+    if (wend <= 0) break;
+    int w = 0;
+    for (; w + 1 < wend; w += 2) {
+      window(s, w, pM, pX, pY, qM, qX, qY);
+      window(s, w + 1, qM, qX, qY, pM, pX, pY);
+    }
+    if (w < wend) {
+      window(s, w, pM, pX, pY, qM, qX, qY);
+      pM = qM;
+      pX = qX;
+      pY = qY;
+    }
+    if (s + 1 < nstrips) {
+      map_pair(64 * (s + 1) + lane, pn, okan, okbn, okcn, fbn, xi);
+      xnA = P.xtab[xi];
+      xnB = P.xtab[okbn ? xi + 1 : xi];
+      xnC = P.xtab[okcn ? xi + 2 : xi];
+    } else {
+      // the drain: a lane that wraps past the last strip holds no rows (its
+      // cells there are computed, FULL, and must not be handed on)
+      okan = okbn = okcn = false;
+    }
+    const int tend = s < nstrips ? min(Ws + Lys, T) : 0;
+    int t = Ws + 64;
+    if (t < tend) {
+      BplaPos yc0, yc1;
+      double a0, a1, a2, c0, c1, c2;
+      iload(t - Ws + 1, yc0, a0, a1, a2);
+      for (; t + 1 < tend; t += 2) {
+        interior(t - Ws + 1, pY, qY, yc0, a0, a1, a2, yc1, c0, c1, c2);
+        interior(t - Ws + 2, qY, pY, yc1, c0, c1, c2, yc0, a0, a1, a2);
+      }
+      if (t < tend) {
+        interior(t - Ws + 1, pY, qY, yc0, a0, a1, a2, yc1, c0, c1, c2);
+        pY = qY;
+      }
+    }
+  }
+  // the rows still held
+  if (okA) {
+    const double h = accA + (okB ? accB : 0.0) + (okC ? accC : 0.0);
+    __hip_atomic_fetch_add(&ksum[p], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Pairs dealt one per wave: each wave stages its own y columns.
 template <bool SW, bool BP>
 __global__ void __launch_bounds__(256) sk_bpla_fast_kernel(BplaLaunch P) {
@@ -926,7 +1211,7 @@ __global__ void __launch_bounds__(64 * kBplaItemsWavesMax) SK_BPLA_ITEMS_ATTR
       int start = 0;
       for (int q = 0; q < np - 1; ++q) {
         const int lq = __shfl(len, q, 64);
-        start += lane > q ? (SW ? lq : lq + (lq & 1)) : 0;  // the exp path pads pairs to even rows
+        start += lane > q ? (SW ? lq : bpla_pad_rows(lq)) : 0;  // the exp path pads pairs (SK_BPLA_ROWS)
       }
       if (lane < np) ci[lane] = make_int4(pb, len, start, 0);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
