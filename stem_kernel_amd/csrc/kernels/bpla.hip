@@ -1019,6 +1019,7 @@ __device__ __forceinline__ void bpla_fast_chunk3(const BplaLaunch& P, int np, co
       yofs = 0;
       dS = 0.0;
       aM = aX = aY = 0.0;  // row A's column 0 (row B's diagonal at column 1)
+      sB1 = bY = 0.0;      // row B's column 0 (row C's diagonal at column 1)
     }
     const int jb = w + 1;  // lane 0's column (strip s)
     const double* bj = bnd + 3 * (jb <= Ly ? jb : 0);
