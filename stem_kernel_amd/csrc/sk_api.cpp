@@ -1590,35 +1590,13 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
         py[(size_t)d] = y[k];
         oidx[(size_t)d] = k;
       }
-      if (group) {  // runs of one y
+      if (group)  // runs of one y
         for (int64_t a = 0; a < n_fast;) {
           int64_t b = a;
           while (b < n_fast && py[(size_t)b] == py[(size_t)a] && b - a < item_max) ++b;
           items.push_back(make_int2((int)a, (int)(b - a)));
           a = b;
         }
-        // the launch's tail: workgroups pull items in list order, so the last
-        // round decides how long the last CUs run alone -- its items (one
-        // per CU) are split in two (SK_BPLA_TAIL=0: off)
-        static const bool tail = !(std::getenv("SK_BPLA_TAIL") && std::getenv("SK_BPLA_TAIL")[0] == '0');
-        if (tail && (int64_t)items.size() > 2 * (int64_t)ctx->n_cu) {
-          std::vector<int2> t;
-          t.reserve(items.size() + ctx->n_cu);
-          const size_t cut = items.size() - (size_t)ctx->n_cu;
-          t.insert(t.end(), items.begin(), items.begin() + (ptrdiff_t)cut);
-          for (size_t k = cut; k < items.size(); ++k) {
-            const int2 it = items[k];
-            const int h = it.y / 2;
-            if (h >= 8) {
-              t.push_back(make_int2(it.x, h));
-              t.push_back(make_int2(it.x + h, it.y - h));
-            } else {
-              t.push_back(it);
-            }
-          }
-          items.swap(t);
-        }
-      }
       x = px.data();
       y = py.data();
     }
