@@ -21,6 +21,7 @@
 #include <thread>
 #include <atomic>
 #include <string>
+#include <system_error>
 #include <vector>
 
 #include "../../include/stem_kernel.h"
@@ -3380,11 +3381,16 @@ int sk_dataset_upload(sk_context* ctx, sk_dataset* ds) {
   const std::function<void()> after_x = [&]() {
     P.xr_ch.insert(P.xr_ch.end(), 8, 0u);  // the kernel prefetches 4 records past a row
     P.xg_ch.insert(P.xg_ch.end(), 8, 0u);
-    xt = std::thread([&]() {
+    auto job = [&]() {
       const auto t0 = std::chrono::steady_clock::now();
       xe = up_x();
       x_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    });
+    };
+    try {
+      xt = std::thread(job);
+    } catch (const std::system_error&) {
+      job();  // no second thread: upload them here, before the y-role pack
+    }
   };
   int rc = pack_dataset(ds, err, &after_x);
   if (xt.joinable()) xt.join();
