@@ -3088,7 +3088,7 @@ int sk_close(sk_context* ctx) {
   // work may still be queued on any of the context's streams (e.g. after an
   // error part-way through a multi-stream call): drain them all before the
   // buffers they read are freed
-  for (hipStream_t st : {ctx->stream, ctx->side, ctx->cls, ctx->aux})
+  for (hipStream_t st : {ctx->stream, ctx->side, ctx->cls, ctx->aux, ctx->cps})
     if (st) (void)hipStreamSynchronize(st);
   sk::comm_destroy(ctx->comm);
   ctx->comm = nullptr;
