@@ -81,7 +81,10 @@ CONFIGS = {
     # their two concurrent class launches would then overlap fully, which
     # doubles each launch's duration (the per-launch roofline) -- kept
     # synchronous
-    "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=16, cid=3, cpu_pairs=196608, async_calls=True),
+    # C4: a step is 1/6 of the Gram (350k pairs): 20.5-20.8M against 18.5M
+    # pairs/s with 1/16 steps on one box (r04u / r04v: the launch's fill and
+    # last round of items amortized over 2.7x the work)
+    "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=6, cid=3, cpu_pairs=196608, async_calls=True),
     "c5": dict(kernel="stem", n=8192, L=300, slices=128, cid=4, cpu_pairs=4096),
 }
 
