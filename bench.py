@@ -85,7 +85,9 @@ CONFIGS = {
     # pairs/s with 1/16 steps on one box (r04u / r04v: the launch's fill and
     # last round of items amortized over 2.7x the work)
     "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=6, cid=3, cpu_pairs=196608, async_calls=True),
-    "c5": dict(kernel="stem", n=8192, L=300, slices=128, cid=4, cpu_pairs=4096),
+    # C5: 1/64 of the Gram per step (525k pairs; 110.2k against 109.0k pairs/s
+    # with 1/128 on one box, r04w2)
+    "c5": dict(kernel="stem", n=8192, L=300, slices=64, cid=4, cpu_pairs=4096),
 }
 
 
