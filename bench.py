@@ -72,10 +72,11 @@ CONFIGS = {
     # unit the reference computes per call (kernel_matrix.cpp:485-575), not a
     # slice whose launch fill and tail would dominate ("whole": steps repeat it)
     "c2": dict(kernel="ss", n=256, L=150, slices=1, whole=True, cid=1, cpu_pairs=12288),
-    # C3: 512 pairs per step (the batch's span launches twice as long: 349.7
-    # against 303.5 pairs/s with 256 on one box, r04t; 768 pairs exceed the
-    # 128 GB batch cap and split)
-    "c3": dict(kernel="stem4d", n=1024, L=200, slices=1025, cid=2, cpu_pairs=32),
+    # C3: 384 pairs per step (the batch's span launches longer: 349.7 against
+    # 303.5 pairs/s for 512 against 256 pairs on one box, r04t; 367.4 for 384
+    # against 360.4 for 512 and 345.2 for 640 on another, r04t2; 768 pairs
+    # exceed the 128 GB batch cap and split)
+    "c3": dict(kernel="stem4d", n=1024, L=200, slices=1367, cid=2, cpu_pairs=32),
     # async: step t+1 planned while step t runs (sk_set_async): C4 +3.6 % (its
     # 7 ms steps had 0.6-0.9 ms host gaps); the DAG configs gain <1 % and
     # their two concurrent class launches would then overlap fully, which
