@@ -194,16 +194,21 @@ def dag_bytes(shapes, x, y):
     return float(np.sum(32.0 * V[x] * V[y] + S[x] + S[y] + 8.0))
 
 
-def col_waves(lens, y):
-    """Waves per pair of the 4-D column kernel, as run_stem4d picks them for a
-    batch: the class's register budget (CPL 1-2: 16, 4: 12, 8: 8), at most
+# columns per group of the 4-D column kernel by class (stem4d.hip s4c_nb)
+COL_NB = {1: 4, 2: 4, 4: 2, 8: 1}
+
+
+def col_shape(lens, y):
+    """(NB, W) of the 4-D column kernel, as run_stem4d picks them for a batch:
+    NB columns per group by class, W = 8 waves at most (two per SIMD), at most
     m - F - 1 (the smallest y of the batch; F = 8 steps between full
     barriers, 1 for short y; one batch per bench step)."""
     m = lens[y]
     cpl = 1 if m.max() + 1 <= 64 else 2 if m.max() + 1 <= 128 else 4 if m.max() + 1 <= 256 else 8
     f_env = max(1, int(os.environ.get("SK4C_F", "8")))
     F = f_env if int(m.min()) - f_env - 1 >= 4 else 1
-    return int(max(1, min({1: 16, 2: 16, 4: 12, 8: 8}[cpl], int(m.min()) - F - 1)))
+    w_env = int(os.environ.get("SK4C_W", "0"))
+    return COL_NB[cpl], int(max(1, min(w_env or 8, 8, int(m.min()) - F - 1)))
 
 
 def stem4d_cells(lens, x, y):
@@ -222,15 +227,17 @@ def algorithmic(kind, shapes, x, y):
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
                 72.0 * stem4d_cells(lens, x, y)
-        if os.environ.get("SK4_COL") and not os.environ.get("SK4_NO_PRE") and int(lens[y].max()) + 1 <= 512:
-            # column-pipelined full_dp (stem4d.hip sk_stem4d_col_kernel): G0 of
-            # (i,j-1) read and G0 of (i,j) written (16 B); every W-th plane's
-            # pre-combined G1 crosses the round wrap through HBM (+16 B)
-            W = col_waves(lens, y)
+        col = not (os.environ.get("SK4_SPAN") or os.environ.get("SK4_NO_PRE"))
+        if col and int(lens[y].max()) + 1 <= 512:
+            # column groups (stem4d.hip sk_stem4d_col_kernel): G0 of (i, j_lo-1)
+            # read by a group's first chain and G0 of (i, j_hi) written by its
+            # last (16 B per NB columns); every W-th position's pre-combined G1
+            # crosses the round wrap through HBM (16 B)
+            NB, W = col_shape(lens, y)
             return "hbm", "GB/s", PEAK_HBM_GBS, \
-                f"16 B per (i,j,k,l) cell (G0 of (i,j-1) read, G0 of (i,j) written) + 16 B per cell of " \
-                f"every W-th plane (W = {W}: the pre-combined G1 across the round wrap), " \
-                "[n(n+1)/2][m(m+1)/2] cells", (16.0 + 16.0 / W) * stem4d_cells(lens, x, y)
+                f"16/NB B per (i,j,k,l) cell (G0 read by a group's first column, written by its last; " \
+                f"NB = {NB}) + 16/W B (W = {W}: every W-th position's pre-combined G1 across the round " \
+                "wrap), [n(n+1)/2][m(m+1)/2] cells", (16.0 / NB + 16.0 / W) * stem4d_cells(lens, x, y)
         if os.environ.get("SK4_NO_PRE") or int(lens[y].max()) + 1 > 512:
             # full_dp with the K chain summed (stem4d.hip): G0, G1 written once
             # (16 B), G0 of (i,j-1), G1 of (i+1,j) and the stacking G0 of
@@ -775,7 +782,7 @@ def main():
             rf["kernel"] = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
                             "stem4d": "sk_stem4d_kernel" if os.environ.get("SK4_NO_GSUM") else
                             "sk_stem4d_gsum_kernel" if os.environ.get("SK4_NO_PRE") else
-                            "sk_stem4d_col_kernel" if os.environ.get("SK4_COL") else "sk_stem4d_pre_kernel",
+                            "sk_stem4d_pre_kernel" if os.environ.get("SK4_SPAN") else "sk_stem4d_col_kernel",
                             "bpla": "sk_bpla_fast_kernel"}[kind]
         cpu, parity = None, None
         if not a.no_cpu_baseline and world == 1 and not a.cpu_stub:  # rank 0 at N=1 only

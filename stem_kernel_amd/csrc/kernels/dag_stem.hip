@@ -182,15 +182,6 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_SEGSUM_MAXK  // the widest class that sums runs per quad
 #define SK_SEGSUM_MAXK 20
 #endif
-#ifndef SK_SKIP_LOOPS  // cost experiment only (wrong results): loop rows (1) / rows with only gamma children (2) skip MATCH and the sweep
-#define SK_SKIP_LOOPS 0
-#endif
-#ifndef SK_PHI_EXP  // cost experiments only (wrong values): 1 phi rows load nothing, 2 no Phi tables
-#define SK_PHI_EXP 0
-#endif
-#ifndef SK_ROW_EXP  // cost experiments only (wrong values): child reads of gamma rows (1) / slab rows (2) all from one row
-#define SK_ROW_EXP 0
-#endif
 #ifndef SK_MU  // MATCH edge rounds: 64-edge groups whose reads are issued together
 #define SK_MU 3
 #endif
@@ -399,18 +390,14 @@ __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int
   A.rv = R[A.rec & 0x7ff];
   int c = c0;
   const int nch = Y.nch;
-  // chunk X now, Y next, Z after: false after the last chunk.  SK_SWEEP_GAP
-  // 2: the host never puts an edge into the chunk right after the one that
-  // completes its child, so chunk Y's R reads are issued before chunk X's
-  // atomics -- two chunks' reads in flight, one LDS round trip per two
-  // chunks (1: each chunk's reads after the previous chunk's atomics)
+  // chunk X now, Y next, Z after: false after the last chunk; each chunk's
+  // R reads after the previous chunk's atomics
   auto step = [&](Ck& X, Ck& Yc, Ck& Z) __attribute__((always_inline)) -> bool {
     Z.rec = rp[128];
     Yc.w = NW ? nweight(Yc.rec) : wp[64];
-    if (SK_SWEEP_GAP >= 2) Yc.rv = R[Yc.rec & 0x7ff];
     __hip_atomic_fetch_add(&R[(X.rec >> 11) & 0x7ff], X.rv * X.w, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if (SK_SWEEP_GAP < 2) Yc.rv = R[Yc.rec & 0x7ff];
+    Yc.rv = R[Yc.rec & 0x7ff];
     rp += 64;
     wp += 64;
     return ++c < nch;
@@ -428,12 +415,6 @@ __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int
 // component
 __device__ __forceinline__ const double* child_row(uint32_t c, const double* slab, const double* gamtab,
                                                    const double* phitab, int stride) {
-#if SK_ROW_EXP & 1
-  if (c & 0x8000u) c = 0x8000u;
-#endif
-#if SK_ROW_EXP & 2
-  if (!(c & 0xc000u)) c = 0u;
-#endif
   const double* base = (c & 0x8000u) ? gamtab : (c & 0x4000u) ? phitab : slab;
   return base + (size_t)(c & 0x3fffu) * stride;
 }
@@ -533,13 +514,6 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // a phi (combination) row: G0 = S, the weighted sum of its component
     // rows; no MATCH, no sweep (its K terms come with the y's Phi sums)
     const bool combo = (xc >> 31) != 0u;
-#if SK_SKIP_LOOPS == 2  // cost experiment: rows whose children are all gamma rows
-    bool skipr = gam && xne > 0 && xne <= 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) skipr = skipr && (j >= xne || (ch[j] & 0x8000u));
-#else
-    const bool skipr = xloop;
-#endif
     // MATCH node range [qa, qb): y nodes are numbered by length, so the
     // length band [xlen-band, xlen+band] is one index range; its first
     // pass's node records are requested now, ahead of the child rows
@@ -603,7 +577,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
         na += take ? 1 : 0;
       }
       for (int h = 0; h < 4; h += 2) {
-        if (na > h && !(SK_PHI_EXP == 1 && combo)) {
+        if (na > h) {
           const bool two = na > h + 1;
           const uint32_t c0 = c[h], c1 = two ? c[h + 1] : c[h];
           const double eg0 = w[h], eg1 = two ? w[h + 1] : 0.0;
@@ -619,7 +593,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
       cnt[0] += nl_ + (xne > 4 ? xne - 4 : 0);
     }
 #endif
-    for (int t = 4; t < xne && !(SK_PHI_EXP == 1 && combo); t += 2) {  // children past the fourth
+    for (int t = 4; t < xne; t += 2) {  // children past the fourth
       const uint32_t c0 = xch[chp_r + t];
       const bool two = t + 1 < xne;
       const uint32_t c1 = two ? xch[chp_r + t + 1] : c0;
@@ -652,7 +626,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #ifdef SK_STAMPS
     cnt[3] += qb > qa ? qb - qa : 0;
 #endif
-    if (!combo && qa < qb && !(SK_SKIP_LOOPS && skipr)) {
+    if (!combo && qa < qb) {
       // node records and path counts come from HBM (L2-resident per y),
       // the first pass's issued before A, each later pass's during the
       // pass before.  A pass covers NW = 64*PW nodes [q0, top], lane l
@@ -891,7 +865,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 #endif
     // a row nobody reads (a root: pslot 0xffff) needs only its MATCH terms
     // (K is the path sum of M), so it skips the sweep and the store
-    if (!combo && c0 < Y.nch && pslot != 0xffffu && !(SK_SKIP_LOOPS && skipr)) {
+    if (!combo && c0 < Y.nch && pslot != 0xffffu) {
       iy_sweep<node_weights<MAXK>(), node_weights_f32<MAXK>()>(Y, R, c0, lane);
       wave_sync();
     }
@@ -1119,7 +1093,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
       // the y stems q in len's band; Phi_t = its IY sweep; kappa_t = sum_q
       // M_t[q] P_y[q] (a phi row's MATCH row is pf_p sum_c w_c M_{t(c)} plus
       // its Gamma_{a,len} part)
-      if (P.phi_on && SK_PHI_EXP != 2) {
+      if (P.phi_on) {
         // the item's keys come sorted by gamma key: wave w takes the w-th
         // contiguous share, and H_g[q] = sum_{cy in ch(q)} g^gy Gamma_g[cy]
         // (independent of the key's code and length) is formed once per

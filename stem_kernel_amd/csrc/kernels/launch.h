@@ -9,17 +9,6 @@
 
 namespace sk {
 
-// IY sweep schedule: an edge goes into a chunk at least SK_SWEEP_GAP chunks
-// after the one that completes its child (the host's list schedule,
-// sk_api.cpp); at 2 the kernel issues a chunk's R reads before the previous
-// chunk's atomics (dag_stem.hip iy_sweep).  Off: the NS y DAGs' sweeps are
-// bound by their height, not their width -- gap 2 takes 78.3 chunks per y
-// against 45.6 (1,024 L = 200 examples, tools/pack_compare.cpp), so two
-// reads in flight would buy nothing
-#ifndef SK_SWEEP_GAP
-#define SK_SWEEP_GAP 1
-#endif
-
 struct StemLaunch {
   DevSet xset;        // row examples (x role)
   DevSet yset;        // column examples (y role); may equal xset
@@ -250,13 +239,14 @@ struct Stem4dLaunch {
 
 int stem4d_cpl(int m);
 hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st);
-// full_dp, column-pipelined (stem4d.hip sk_stem4d_col_kernel): one workgroup
-// of `waves` waves per pair (pairs[0..n_pairs)); per pair n planes of
-// plane_doubles (G0) and one B' plane at scratch_off; |y| < 512, and
-// m + 1 >= waves + 3
-size_t stem4d_col_lds_bytes(int cpl, int waves);
+// full_dp, column groups (stem4d.hip sk_stem4d_col_kernel): one workgroup of
+// `waves` waves per pair (pairs[0..n_pairs)); per pair n planes of
+// plane_doubles (G0) and stem4d_col_nb(cpl) B' planes (the round wrap) at
+// scratch_off; |y| < 512, and m + 1 >= waves + col_f + 2
+int stem4d_col_nb(int cpl);
+size_t stem4d_col_lds_bytes(int cpl, int waves, int max_m);
 int stem4d_col_max_waves(int cpl);
-hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves,
+hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves, int max_m,
                              hipStream_t st);
 
 // PairHMM alignment constraints of a 4-D batch (-a, stem_kernel.cpp:14-81):

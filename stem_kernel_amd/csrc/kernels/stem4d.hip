@@ -76,9 +76,6 @@ __device__ __forceinline__ double s4c_ld64(const double* base, int nk, int c, in
 __device__ __forceinline__ float s4c_ld32(const float* base, int nk, int c, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s4c_slot(base, nk, c), lane * 4, 0, 0));
 }
-__device__ __forceinline__ uint8_t s4c_ld8(const uint8_t* base, int nk, int c, int lane) {
-  return __builtin_amdgcn_raw_buffer_load_b8(s4c_slot(base, nk, c), lane, 0, 0);
-}
 __device__ __forceinline__ void s4c_st64(double* base, int nk, int c, int lane, double v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, v), s4c_slot(base, nk, c), lane * 8, 0, 0);
 }
@@ -604,12 +601,6 @@ __global__ void __launch_bounds__(256) sk_stem4d_gsum_kernel(Stem4dLaunch P) {
 // go to its own accumulator acc[i].  Single k tile (|y| < 512; the host runs
 // the K-sum kernel otherwise).  Plane layout: G0 at 0, B' (for the plane
 // (i-1, j)) at cp.
-// SK4P_RANGE: the span kernel's rows as straight-line slots over
-// range-checked buffers -- off: 318.5 / 315.8 against 336.5 pairs/s with the
-// per-slot guards on one box (r04k), although it fits 128 VGPRs
-#ifndef SK4P_RANGE
-#define SK4P_RANGE 0
-#endif
 // SK4P_WPE (build-time): ask the register allocator for that many waves per
 // SIMD (4: <= 128 VGPRs)
 #ifdef SK4P_WPE
@@ -710,25 +701,6 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
     const int kmax = m - d2;
     const int e2 = d2 - 1;
     const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
-#if SK4P_RANGE
-    // range-checked buffers: loads past kmax return 0, no per-slot guards
-    const int nk = kmax + 1;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      r.A[c] = s4c_ld64(A + Rd, nk, c, lane);
-      r.Bp[c] = s4c_ld64(B + cp + Rd, nk, c, lane);
-      r.bp[c] = 0.0f;
-      r.yl[c] = 0;
-    }
-    if (stack_c) {
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        r.bp[c] = s4c_ld32(bpy + ye, nk, c, lane);
-        r.yl[c] = s4c_ld8(ys + d2 - 1, nk, c, lane);
-      }
-    }
-    return;
-#endif
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + 64 * c;
@@ -768,52 +740,6 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
       A2[c] = wave_shl1(Am2[c], ha);
     }
     const int kmax = m - d2;
-#if SK4P_RANGE
-    {  // straight-line slots (as in sk_stem4d_col_kernel): stores past kmax are
-       // dropped by the buffer range, lanes past it feed no valid cell and add
-       // nothing to K
-      const bool stk_row = stack_c && d2 >= 2;
-      const double bpc = (double)bp_c;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const int k = k0 + 64 * c;
-        const double G1 = cr.Bp[c];
-        double G0 = cr.A[c] * g;
-        G0 += G1;
-        s4c_st64(cur + R, kmax + 1, c, lane, G0);
-        if (cons) {
-          double g3 = G3n[c] * g;
-          if (stk_row) {
-            const float bp_kl = cr.bp[c];
-            const bool src = bp_kl > bound && k <= kmax;
-            const bool match = xci == yk[c] && xcj == cr.yl[c];
-            const double g0 = A2[c];
-            const double t0 = g0 * stk;
-            const double tm = match ? t0 : t0 * sub;
-            const double term = tm * bpc * (double)bp_kl;
-            ksrc += src ? term : 0.0;
-            g3 += src && match ? g0 : 0.0;
-          }
-          double g2 = G2c[c] * g;
-          g2 += g3;
-          double Bn = G1 * g;
-          Bn += g2;
-          s4c_st64(cur + cp + R, kmax + 1, c, lane, Bn);
-          G2c[c] = g2;
-          G3c[c] = g3;
-        }
-      }
-    }
-    if (SK4P_RANGE) {
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        Am2[c] = Am1[c];
-        Am1[c] = cr.A[c];
-      }
-      R = Rn;
-      continue;
-    }
-#endif
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int k = k0 + 64 * c;
@@ -868,451 +794,333 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
   }
 }
 
-// full_dp, column-pipelined (r04): one WORKGROUP per pair walks the x
-// columns j = 1..n, and in column j the planes i = j-1, j-2, ..., 0, which
-// its W waves take in turn, each wave one row (y span d2) behind the previous.
-// Plane (i, j) needs G0(i, j-1) (the previous column's plane i, HBM) and its
-// pre-combined G1, B'(i, j) = G1(i+1, j) g + G2_(i,j), which the wave of plane
-// (i+1, j) forms from ITS A input -- G0(i+1, j-1), the stacking sources of
-// (i, j) -- one step earlier (the scheme of sk_stem4d_pre_kernel).  Here B'
-// goes from wave w to wave w+1 through an LDS double buffer instead of HBM,
-// so a cell costs the G0 read of (i, j-1) and the G0 write of (i, j) (in
-// place: plane slot i holds G0(i, j) of the latest column): 16 B, plus 16 B
-// for every W-th plane, whose B' crosses the round wrap (wave W-1 -> wave 0,
-// R - W + 1 steps later) through one plane-sized HBM buffer per pair.
-//
-// Schedule: positions p = 0, 1, ... run column by column; column j holds its
-// j planes (i = j-1 at offset 0) and then bubbles up to c_j = max(j, PF + 1)
-// positions, PF = 2 rows fetched ahead.  Position p is wave p % W's plane of
-// round p / W, and wave w processes row s of it at step T(p) + s, T(p) =
-// (p / W) R + p % W, R = m + 1 rows; one workgroup barrier per step.  Since
-// R >= W + PF + 1 (the host's choice of W), T is increasing with
-// T(p2) - T(p1) >= p2 - p1, so:
+// full_dp, column groups (r05): one WORKGROUP per pair walks the x columns in
+// groups of NB, j = gNB+1 .. j_hi = min(gNB+NB, n), and in group g the planes
+// i = j_hi-1, ..., 0 in turn ("positions"), which its W waves take in turn,
+// each wave one row (y span d2) behind the previous.  A position runs its
+// group's columns as NB CHAINS in the same step: chain c is the plane
+// (i, j_lo + c), and the G0 row it forms is the A row (G0(i, j-1)) of chain
+// c+1, so only chain 0 reads a G0 row from HBM (written in plane slot i by
+// the previous group's last chain) and only the last chain writes one: 16/NB
+// B per cell.  Each chain also forms its consumer's pre-combined G1,
+// B'(i-1, j) = G1(i, j) g + G2_(i-1,j), from its own A rows (the stacking
+// sources of (i-1, j), the scheme of sk_stem4d_pre_kernel) and hands it to
+// the next wave through an LDS double buffer (slot = step parity); the wave
+// of every W-th position hands it across the round wrap through one plane per
+// chain in HBM (16/W B per cell).  A consumer whose x pair is no stacking
+// pair (prob(i-1, j-1) <= bound) has G3 = G2 = 0 in every cell, so its chain
+// costs one FMA and one multiply per cell (stem_kernel.cpp:320-334).
+// Schedule (tests/test_stem4d_col_schedule.py emulates it step by step
+// against the oracle): group g holds c_g = max(j_hi, F + PF) positions (its
+// planes, then bubbles); position p is wave p % W's plane of round p / W,
+// row s at step T(p) + s, T(p) = (p / W) R + p % W, R = m + 1 rows, one
+// workgroup barrier per step.  With R >= W + F + PF (the host's W), T is
+// increasing with T(p2) - T(p1) >= p2 - p1, so:
 //  * B' of row s is written by wave w-1 at step t-1 and read by wave w at
-//    step t (LDS slot t & 1), or, at the wrap, at least PF + 1 steps later;
-//  * the A row s + PF that a plane prefetches at step T(p) + s was written
-//    (by the previous column's plane i, >= PF + 2 positions earlier) at a
-//    step before that;
-//  * row 0 is never stored: G0(i, j, l, l) = g^(j-i) (the repeated products
-//    of gap_powers, as the chain G0(i+1,j,l,l) g forms it, :313-317).
-// The K chain is summed (sk_stem4d_gsum_kernel): every lane keeps one running
-// sum of its consumers' stacking sources over all its planes; the pair's
-// K = 1 + the waves' lane-reduced sums in wave order.
+//    step t (LDS slot t & 1), or, at the wrap, >= F + PF steps later;
+//  * the A row that position (g, i) fetches PF rows ahead was written by
+//    position (g-1, i), >= c_{g-1} >= F + PF positions earlier;
+//  * row 0 is never stored: G0(i, j, l, l) = g^(j-i), the repeated products
+//    of gap_powers, as the chain G0(i+1, j, l, l) g forms it (:313-317).
+// Barriers: between steps only the LDS B' rows must be visible, so a step
+// starts with an LDS-only barrier (lgkmcnt); every F-th is a full one (a
+// workgroup release of global memory), so a global store of step u is seen
+// from the first multiple of F above u on -- hence the F + PF lags.
+// The K chain is summed (sk_stem4d_gsum_kernel): each lane sums its sources
+// over every chain of every position, the waves' sums are added in wave
+// order.  Lanes past a row's end compute values that are never stored (the
+// range-checked buffers end at the row) nor read by a valid cell of a later
+// row (a cell reads k and k+1 of earlier rows, both valid there), and add
+// nothing to K (their bp loads return 0, and bound >= 0).
 #ifndef SK4C_PF
-#define SK4C_PF 2  // rows fetched ahead
+#define SK4C_PF 2  // rows fetched ahead (the step loop is unrolled over the two row buffers)
+#endif
+static_assert(SK4C_PF == 2, "sk_stem4d_col_kernel keeps two row buffers");
+#ifndef SK4C_NB4  // column-group width of the CPL 4 class (|y| 128..255)
+#define SK4C_NB4 2
 #endif
 
-// Barriers: between steps only the LDS B' rows need to be visible, so most
-// barriers wait for LDS traffic alone (lgkmcnt) -- a workgroup release of
-// global memory would wait for every outstanding vector memory op (vmcnt:
-// the prefetched rows too), i.e. pay the HBM latency every step.  Every F-th
-// barrier (P.col_f; the one before step t, t % F == 0) is a full one, so a
-// global store of step u is visible from the first multiple of F above u
-// on: readers of global data need a lag of F + PF steps -- column j holds
-// c_j = max(j, F + 2) positions, and W <= m - F - 1 (the round wrap).
-//
-// Between the full barriers the waves need not run in lockstep (SK4C_P2P):
-// wave w publishes in LDS the number of steps it has completed, and waits
-// only for what it touches -- its producer's step t-1 before it reads link
-// slot (t-1) % D, its consumer's step t-D+1 before it overwrites slot t % D
-// -- so a wave held up by a late row delays its consumers alone and not the
-// whole workgroup.  Every wait is on a strictly earlier step, so there is no
-// cycle; a wait that runs past ~0.5 s gives up and the pair's K is NaN.
-#ifndef SK4C_RANGE  // 1: the row step as straight-line slots over range-checked buffers
-#define SK4C_RANGE 0   // (off: 260 against 306 pairs/s with the per-slot guards, r04k)
-#endif
-#ifndef SK4C_P2P  // off: 278 against 305 pairs/s lockstep on C3 (r04e)
-#define SK4C_P2P 0
-#endif
-#ifndef SK4C_D  // link slots per wave (a power of 2; 2 when lockstep)
-#define SK4C_D (SK4C_P2P ? 4 : 2)
-#endif
-static_assert(SK4C_D >= 2 && (SK4C_D & (SK4C_D - 1)) == 0, "SK4C_D: a power of 2");
-
-__device__ __forceinline__ void s4c_publish(int* done, int v) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __hip_atomic_store(done, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+template <int CPL>
+constexpr int s4c_nb() {
+  return CPL <= 2 ? 4 : CPL == 4 ? SK4C_NB4 : 1;
 }
-
-__device__ __forceinline__ void s4c_wait_ge(const int* done, int v, bool& bad) {
-  if (bad) return;
-  int it = 0;
-  while (__builtin_amdgcn_readfirstlane(
-             __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < v) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++it > (1 << 23)) {
-      bad = true;
-      break;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-
-__device__ __forceinline__ int s4c_cols(int j, int F) { return j > F + SK4C_PF ? j : F + SK4C_PF; }
-
-// position -> plane of the column schedule; advance() moves on by W positions
-struct S4cPos {
-  int j = 1, off = 0;  // column, offset in the column (i = j - 1 - off; off >= j: bubble)
-  __device__ void advance(int W, int n, int F) {
-    off += W;
-    while (j <= n && off >= s4c_cols(j, F)) {
-      off -= s4c_cols(j, F);
-      ++j;
-    }
-  }
-  __device__ bool valid(int n) const { return j <= n; }
-  __device__ bool plane(int n) const { return j <= n && off < j; }
-  __device__ int i() const { return j - 1 - off; }
-};
-
-// waves per workgroup at most: 4, 3 and 2 per SIMD (the register budget)
-#ifndef SK4C_W4  // waves per workgroup of the CPL 4 class (12: 3 per SIMD; 16 needs SK4C_PF 1)
-#define SK4C_W4 12
-#endif
+// waves per workgroup at most (registers: two waves per SIMD)
 template <int CPL>
 constexpr int s4c_max_waves() {
-  return CPL <= 2 ? 16 : CPL == 4 ? SK4C_W4 : 8;
+  return 8;
 }
+
+__device__ __forceinline__ int s4c_group_len(int g, int n, int nb, int fp) {
+  const int jh = min((g + 1) * nb, n);
+  return jh > fp ? jh : fp;
+}
+
+// position -> (column group, offset in the group); advance() moves on by W
+struct S4cPos {
+  int g = 0, off = 0;
+  __device__ void advance(int W, int n, int nb, int fp) {
+    off += W;
+    while (g * nb < n) {
+      const int c = s4c_group_len(g, n, nb, fp);
+      if (off < c) break;
+      off -= c;
+      ++g;
+    }
+  }
+  __device__ bool valid(int n, int nb) const { return g * nb < n; }
+};
 
 template <int CPL>
 __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kernel(Stem4dLaunch P) {
-  extern __shared__ __attribute__((aligned(16))) double s4c_lds[];
+  constexpr int NB = s4c_nb<CPL>();
   constexpr int TW = 64 * CPL;
+  extern __shared__ __attribute__((aligned(16))) double s4c_lds[];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = blockDim.x >> 6;
   const Stem4dPair pr = P.pairs[blockIdx.x];
   const int n = pr.n, m = pr.m, R = m + 1;
+  if (m <= 1) {  // no y pair (k, l-1) with k < l-1: no stacking source, K = 1 (the host's W ignores it)
+    if (threadIdx.x == 0) P.out[pr.out_index] = 1.0;
+    return;
+  }
   const int64_t cp = pr.plane_doubles;
-  double* __restrict__ planes = P.scratch + pr.scratch_off;  // slot i: G0(i, latest j)
-  double* __restrict__ wrapb = planes + (int64_t)n * cp;     // B' across the round wrap
+  double* __restrict__ planes = P.scratch + pr.scratch_off;  // slot i: G0(i, latest column)
+  double* __restrict__ wrapb = planes + (int64_t)n * cp;     // NB planes: B' across the round wrap
   const float* bpx = P.bpdiag + pr.x_bp;
   const float* bpy = P.bpdiag + pr.y_bp;
   const uint8_t* xs = P.chars + pr.x_chr;
-  const uint8_t* ys = P.chars + pr.y_chr;
   const double* gpow = P.gpow;
   const float bound = P.bp_bound;
   const double g = P.gap, stk = P.stack, sub = P.subst;
   const int F = max(P.col_f, 1);
-  // links: wave w writes link w (slot t % D), wave w+1 reads it a step later
-  constexpr int D = SK4C_D;
-  double* link_out = s4c_lds + (int64_t)w * D * TW;
-  const double* link_in = s4c_lds + (int64_t)(w - 1) * D * TW;
-  double* red = s4c_lds + (int64_t)W * D * TW;  // W per-wave sums
-  int* done = reinterpret_cast<int*>(red + W);  // W step counters (SK4C_P2P)
-  bool bad = false;
+  const int FP = F + SK4C_PF;
+  // LDS: links [W][2][NB][TW] (wave w writes link w, wave w+1 reads it a step
+  // later), W per-wave sums, y (zero padded: y[k + s - 1] for every slot)
+  double* link_out = s4c_lds + (int64_t)w * 2 * NB * TW;
+  const double* link_in = s4c_lds + (int64_t)(w - 1) * 2 * NB * TW;
+  double* red = s4c_lds + (int64_t)W * 2 * NB * TW;
+  uint8_t* ysl = reinterpret_cast<uint8_t*>(red + W);
+  for (int k = threadIdx.x; k < TW + R + 8; k += blockDim.x) ysl[k] = k < m ? P.chars[pr.y_chr + k] : 0;
+  __syncthreads();
 
   // steps: T(last position) + R
   int64_t np = 0;
-  for (int j = 1; j <= n; ++j) np += s4c_cols(j, F);
+  for (int gg = 0; gg * NB < n; ++gg) np += s4c_group_len(gg, n, NB, FP);
   const int64_t total = np > 0 ? ((np - 1) / W) * R + (np - 1) % W + R : 0;
 
-  // per-plane constants of the plane at a position
+  // the position's planes (wave-uniform: SGPRs)
   struct Plane {
-    int i, j;
-    bool on, first, cons, stack;
-    float bp_c;
-    uint8_t xci, xcj;
+    int i, c0, nbg, j_lo;
+    bool on, bnd, cons;
+    uint32_t stack;  // bit c: chain c's consumer (i-1, j_lo+c) is a stacking pair
+    uint32_t xci;
+    uint32_t xcj[NB];
+    double cm[NB], cs[NB];  // stack bp(i-1, j-1): match / mismatch factors (:320-331)
   };
   auto describe = [&](const S4cPos& q) __attribute__((always_inline)) -> Plane {
     Plane d;
-    d.on = q.plane(n);
-    d.i = d.on ? q.i() : 0;
-    d.j = d.on ? q.j : 1;
-    d.first = d.i == d.j - 1;
-    d.cons = d.on && d.i >= 1;
-    d.bp_c = 0.0f;
-    d.xci = d.xcj = 0;
-    if (d.cons) {  // the consumer (i-1, j): bp(i-1, j-1) (:320)
-      // (wave-uniform loads made uniform in SGPRs: the plane's branches on
-      // them are then scalar branches, not exec-mask juggling per slot)
-      const int e = d.j - d.i;
-      d.bp_c = __uint_as_float(__builtin_amdgcn_readfirstlane(
-          __float_as_uint(bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (d.i - 1)])));
-      d.xci = (uint8_t)__builtin_amdgcn_readfirstlane(xs[d.i - 1]);
-      d.xcj = (uint8_t)__builtin_amdgcn_readfirstlane(xs[d.j - 1]);
+    d.on = d.bnd = d.cons = false;
+    d.i = d.c0 = d.nbg = 0;
+    d.j_lo = 1;
+    d.stack = 0u;
+    d.xci = 0u;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+      d.xcj[c] = 0u;
+      d.cm[c] = d.cs[c] = 0.0;
     }
-    d.stack = d.cons && d.bp_c > bound;
-    return d;
-  };
-  // one row's HBM inputs, fetched PF rows ahead: G0(i, j-1) (A), the wrap
-  // B' (wave 0 of a non-first plane), prob_y(k, l-1), y[l-1]
-  struct Row {
-    double A[CPL], Bw[CPL];
-    float bp[CPL];
-    uint8_t yl[CPL];  // y[l-1], compared at the row's step: an operation on a
-                      // loaded value here would wait for the load (no prefetch)
-  };
-#if SK4C_RANGE
-  auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
-    // cells k <= m - s of the row; past them every load returns 0 (buffer
-    // range), the branches below are on wave-uniform values
-    const int nk = d.on && s >= 1 ? m - s + 1 : 0;
-    const int ro = row_off(m, s);
-    const int e2 = s - 1;
-    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+    if (!q.valid(n, NB)) return d;
+    d.j_lo = q.g * NB + 1;
+    const int j_hi = min(q.g * NB + NB, n);
+    d.nbg = j_hi - d.j_lo + 1;
+    if (q.off >= j_hi) return d;  // a bubble
+    d.on = true;
+    d.i = j_hi - 1 - q.off;
+    d.c0 = max(0, d.i + 1 - d.j_lo);
+    d.bnd = d.i + 1 >= d.j_lo;  // the first chain is the plane (i, i+1): A = g^(l-k), G1 = 0
+    d.cons = d.i >= 1;
+    if (d.cons) {
+      d.xci = __builtin_amdgcn_readfirstlane(xs[d.i - 1]);
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      r.A[c] = r.Bw[c] = 0.0;
-      r.bp[c] = 0.0f;
-      r.yl[c] = 0;
-    }
-    if (nk == 0) return;
-    if (d.first) {  // G0(j-1, j-1) = g^(l-k)
-      const double gs = gpow[s];
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) r.A[c] = lane + 64 * c < nk ? gs : 0.0;
-    } else {
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) r.A[c] = s4c_ld64(planes + (int64_t)d.i * cp + ro, nk, c, lane);
-      if (w == 0) {  // the round wrap's B'
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) r.Bw[c] = s4c_ld64(wrapb + ro, nk, c, lane);
-      }
-    }
-    if (d.stack) {
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        r.bp[c] = s4c_ld32(bpy + ye, nk, c, lane);
-        r.yl[c] = s4c_ld8(ys + s - 1, nk, c, lane);
-      }
-    }
-  };
-#else
-  auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
-    const int kmax = m - s;
-    const int ro = row_off(m, s);
-    const int e2 = s - 1;
-    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
-    const double* Ai = planes + (int64_t)d.i * cp + ro;
-    const bool wrap_in = w == 0 && !d.first;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const int k = lane + 64 * c;
-      r.A[c] = 0.0;
-      r.Bw[c] = 0.0;
-      r.bp[c] = 0.0f;
-      r.yl[c] = 0;
-
-      if (d.on && s >= 1 && k <= kmax) {
-        r.A[c] = d.first ? gpow[s] : Ai[k];  // G0(j-1, j-1) = g^(l-k)
-        if (wrap_in) r.Bw[c] = wrapb[ro + k];
-        if (d.stack) {
-          r.bp[c] = bpy[ye + k];
-          r.yl[c] = ys[k + s - 1];
+      for (int c = 0; c < NB; ++c) {
+        if (c < d.c0 || c >= d.nbg) continue;
+        const int jp = d.j_lo + c, e = jp - d.i;  // bp(i-1, jp-1): diagonal e
+        const float bc = __uint_as_float(__builtin_amdgcn_readfirstlane(
+            __float_as_uint(bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (d.i - 1)])));
+        d.xcj[c] = __builtin_amdgcn_readfirstlane(xs[jp - 1]);
+        if (bc > bound) {
+          d.stack |= 1u << c;
+          d.cm[c] = stk * (double)bc;
+          d.cs[c] = stk * sub * (double)bc;
         }
       }
     }
+    return d;
   };
-#endif
-
-  uint32_t yk = 0;  // y[k] of slot c in byte c (CPL <= 4), else reread per plane
+  // one row's HBM inputs, fetched PF rows ahead: G0(i, j_lo - 1) (chain 0's
+  // A row), prob_y(k, l-1), and on wave 0 the chains' round-wrap B' rows
+  struct Row {
+    double A[CPL];
+    double Bw[NB][CPL];
+    float bp[CPL];
+  };
+  auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
+    const int nk = d.on && s >= 1 ? m - s + 1 : 0;  // valid cells of the row
+    if (nk == 0) return;
+    const int ro = row_off(m, s);
+    const int e2 = s - 1;
+    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
 #pragma unroll
-  for (int c = 0; c < CPL && c < 4; ++c) {
-    const int k = lane + 64 * c;
-    yk |= (uint32_t)(k < m ? ys[k] : 0) << (8 * c);
-  }
-  uint32_t xkm = 0;  // bit c: y[k] == x[i-1] of the consumer (per plane)
+    for (int c = 0; c < CPL; ++c) {
+      if (64 * c >= nk) break;
+      if (!d.bnd) r.A[c] = s4c_ld64(planes + (int64_t)d.i * cp + ro, nk, c, lane);
+      r.bp[c] = s4c_ld32(bpy + ye, nk, c, lane);
+      if (w == 0) {
+#pragma unroll
+        for (int ch = 0; ch < NB; ++ch)
+          if (ch >= d.c0 && ch < d.nbg && !(ch == d.c0 && d.bnd))
+            r.Bw[ch][c] = s4c_ld64(wrapb + (int64_t)ch * cp + ro, nk, c, lane);
+      }
+    }
+  };
+
   double ksrc = 0.0;
-  double Am1[CPL], Am2[CPL], G2c[CPL], G3c[CPL];
+  double Am1[NB][CPL], Am2[NB][CPL], G2c[NB][CPL], G3c[NB][CPL];
+  bool xk[CPL];  // y[k] == x[i-1] (the consumer's left base), per position
 #pragma unroll
-  for (int c = 0; c < CPL; ++c) Am1[c] = Am2[c] = G2c[c] = G3c[c] = 0.0;
+  for (int c = 0; c < CPL; ++c) {
+    xk[c] = false;
+#pragma unroll
+    for (int ch = 0; ch < NB; ++ch) Am1[ch][c] = Am2[ch][c] = G2c[ch][c] = G3c[ch][c] = 0.0;
+  }
 
-  // this wave's position (p = w) and the fetch cursor PF rows ahead
   S4cPos cur;
-  cur.advance(w, n, F);  // from position 0
+  cur.advance(w, n, NB, FP);  // from position 0
   Plane dc = describe(cur);
   S4cPos fpos = cur;
   Plane df = dc;
   int fs = 0;  // fetch cursor: (fpos, fs)
-  Row rq[SK4C_PF];  // rows fetched ahead, oldest first
+  int s = 0, ro = 0;
+  // the row of step t is fetched at step t - PF into the buffer of t's parity
+  // (an even step consumes E, an odd one O; steps -2, -1 before the loop)
+  Row E, O;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    E.A[c] = O.A[c] = 0.0;
+    E.bp[c] = O.bp[c] = 0.0f;
+#pragma unroll
+    for (int ch = 0; ch < NB; ++ch) E.Bw[ch][c] = O.Bw[ch][c] = 0.0;
+  }
   auto fetch_next = [&](Row& r) __attribute__((always_inline)) {
     fetch(r, df, fs);
     if (++fs == R) {
       fs = 0;
-      fpos.advance(W, n, F);
+      fpos.advance(W, n, NB, FP);
       df = describe(fpos);
     }
   };
-  // a wave's first rows are fetched PF steps before its first step (t = w),
-  // not earlier: their A rows may be written in the steps before
-#pragma unroll
-  for (int q = 0; q < SK4C_PF; ++q)
-    if (w - SK4C_PF + q < 0) fetch_next(rq[q]);
-  int s = 0;
-#if SK4C_P2P
-  done[w] = cur.valid(n) ? 0 : INT_MAX;
-  __syncthreads();
-#endif
+  if (w <= 0) fetch_next(E);  // step -2's fetch: the row of step 0
+  if (w <= 1) fetch_next(O);  // step -1's: the row of step 1
 
-  for (int64_t t = 0; t < total; ++t) {
+  auto step = [&](int64_t t, Row& X) __attribute__((always_inline)) {
     if (t > 0) {  // (every wave takes every barrier)
       if (t % F == 0) {
         __syncthreads();
-      } else if (!SK4C_P2P) {
+      } else {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
       }
     }
-    if (!cur.valid(n)) continue;
+    if (!cur.valid(n, NB)) return;
     if (t < w) {
-#pragma unroll
-      for (int q = 0; q < SK4C_PF; ++q)
-        if (t == w - SK4C_PF + q) fetch_next(rq[q]);
-      if (SK4C_P2P) s4c_publish(done + w, (int)t + 1);
-      continue;
+      if (t >= w - SK4C_PF) fetch_next(X);
+      return;
     }
-    const Row cr = rq[0];
-#pragma unroll
-    for (int q = 0; q + 1 < SK4C_PF; ++q) rq[q] = rq[q + 1];
-    fetch_next(rq[SK4C_PF - 1]);
     if (dc.on) {
-      const int kmax = m - s;
-      if (s == 0) {  // cells (l, l): G0 = g^(j-i), never stored; chain registers reset
-        xkm = 0u;
+      if (s == 0) {  // cells (l, l): G0 = g^(j-i), never stored; the chains' registers reset
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          const int k = lane + 64 * c;
-          const uint32_t ykc = c < 4 ? (yk >> (8 * (c & 3))) & 0xffu : (k < m ? ys[k] : 0u);
-          xkm |= (dc.stack && ykc == dc.xci ? 1u : 0u) << c;
-        }
+        for (int c = 0; c < CPL; ++c) xk[c] = ysl[lane + 64 * c] == dc.xci;
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          const int k = lane + 64 * c;
-          Am1[c] = (dc.stack && k <= m) ? gpow[dc.j - 1 - dc.i] : 0.0;  // G0(i, j-1, l, l)
-          Am2[c] = G2c[c] = G3c[c] = 0.0;
+        for (int ch = 0; ch < NB; ++ch) {
+          if (!((dc.stack >> ch) & 1u)) continue;
+          const double a0 = gpow[dc.j_lo + ch - 1 - dc.i];  // G0(i, j-1, l, l)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            Am1[ch][c] = a0;
+            Am2[ch][c] = G2c[ch][c] = G3c[ch][c] = 0.0;
+          }
         }
-#if SK4C_RANGE
       } else {
-        // Straight-line slots: lanes past kmax compute values that are never
-        // stored (the output buffers' range ends at kmax) nor read by a valid
-        // cell of a later row (a cell reads k+1 of the row before, valid
-        // there), and add nothing to K (their bp loads are 0 and masked)
-        const int ro = row_off(m, s);
-        const int nk = kmax + 1;
+        const int kmax = m - s;
+        const double* lin = link_in + ((t - 1) & 1) * NB * TW;
+        double* lout = link_out + (t & 1) * NB * TW;
+        const bool to_link = w + 1 < W;
         double* const gout = planes + (int64_t)dc.i * cp + ro;
-        const bool wrap_in = w == 0;
-        const double* lin = link_in + ((t - 1) & (D - 1)) * TW;
-        double* lout = dc.cons && w + 1 < W ? link_out + (t & (D - 1)) * TW : nullptr;
-        const int nk_wrap = dc.cons && !lout ? nk : 0;
-        if (SK4C_P2P) {
-          if (!dc.first && !wrap_in) s4c_wait_ge(done + w - 1, (int)t, bad);
-          if (lout) s4c_wait_ge(done + w + 1, (int)t - D + 2, bad);
-        }
-        const bool stk_row = dc.stack && s >= 2;
-        const double bpc = (double)dc.bp_c;
+        const double gs = gpow[s];
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-          // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
-          // (k+1, l-1): the next lane's, or the next slot's lane 0 -- formed
-          // here, before slot c's update, while slot c+1's is still the old
-          // row's (short live ranges: the registers of 4 waves per SIMD)
-          const double hg = c + 1 < CPL ? bcast_lane0(G3c[c + 1 < CPL ? c + 1 : c]) : 0.0;
-          const double ha = c + 1 < CPL ? bcast_lane0(Am2[c + 1 < CPL ? c + 1 : c]) : 0.0;
-          const double G3n = wave_shl1(G3c[c], hg);
-          const double A2 = wave_shl1(Am2[c], ha);
+          if (64 * c > kmax) break;
           const int k = lane + 64 * c;
-          // this plane: G1 = B' (formed by the plane (i+1, j)), G0 (:85-111)
-          const double G1 = dc.first ? 0.0 : wrap_in ? cr.Bw[c] : lin[k];
-          double G0 = cr.A[c] * g;
-          G0 += G1;
-          s4c_st64(gout, nk, c, lane, G0);
-          if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
-            double g3 = G3n * g;
-            if (stk_row) {
-              const float bp_kl = cr.bp[c];
-              const bool src = bp_kl > bound && k <= kmax;
-              const bool match = ((xkm >> c) & 1u) && cr.yl[c] == dc.xcj;
-              const double g0 = A2;
-              // the reference's products in its order; +0 where no source
-              const double t0 = g0 * stk;
-              const double tm = match ? t0 : t0 * sub;
-              const double term = tm * bpc * (double)bp_kl;
-              ksrc += src ? term : 0.0;
-              g3 += src && match ? g0 : 0.0;
-            }
-            double g2 = G2c[c] * g;
-            g2 += g3;
-            double Bn = G1 * g;
-            Bn += g2;
-            if (lout) lout[k] = Bn;
-            else s4c_st64(wrapb + ro, nk_wrap, c, lane, Bn);
-            G2c[c] = g2;
-            G3c[c] = g3;
-          }
-        }
-#else
-      } else {
-        const int ro = row_off(m, s);
-        double* __restrict__ out = planes + (int64_t)dc.i * cp + ro;
-        const bool wrap_in = w == 0;
-        const double* lin = link_in + ((t - 1) & (D - 1)) * TW;
-        double* lout = dc.cons && w + 1 < W ? link_out + (t & (D - 1)) * TW : nullptr;
-        if (SK4C_P2P) {
-          if (!dc.first && !wrap_in) s4c_wait_ge(done + w - 1, (int)t, bad);
-          if (lout) s4c_wait_ge(done + w + 1, (int)t - D + 2, bad);
-        }
+          const float bpf = X.bp[c];
+          const bool sok = bpf > bound;
+          const double bpd = sok ? (double)bpf : 0.0;
+          const uint32_t yl = ysl[k + s - 1];
+          double A = dc.bnd ? gs : X.A[c];
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
-          // (k+1, l-1): the next lane's, or the next slot's lane 0 -- formed
-          // here, before slot c's update, while slot c+1's is still the old
-          // row's (short live ranges: the registers of 4 waves per SIMD)
-          const double hg = c + 1 < CPL ? bcast_lane0(G3c[c + 1 < CPL ? c + 1 : c]) : 0.0;
-          const double ha = c + 1 < CPL ? bcast_lane0(Am2[c + 1 < CPL ? c + 1 : c]) : 0.0;
-          const double G3n = wave_shl1(G3c[c], hg);
-          const double A2 = wave_shl1(Am2[c], ha);
-          const int k = lane + 64 * c;
-          if (k <= kmax) {
-            // this plane: G1 = B' (formed by the plane (i+1, j)), G0 (:85-111)
-            const double G1 = dc.first ? 0.0 : wrap_in ? cr.Bw[c] : lin[k];
-            double G0 = cr.A[c] * g;
+          for (int ch = 0; ch < NB; ++ch) {
+            if (ch < dc.c0 || ch >= dc.nbg) continue;
+            double G1 = 0.0;
+            if (!(ch == dc.c0 && dc.bnd)) G1 = w == 0 ? X.Bw[ch][c] : lin[ch * TW + k];
+            double G0 = A * g;
             G0 += G1;
-            out[k] = G0;
-            if (dc.cons) {  // the consumer (i-1, j): dp_init / stacking / dp_update of its G chain
-              double g3 = G3n * g;
-              if (dc.stack && s >= 2) {
-                const float bp_kl = cr.bp[c];
-                if (bp_kl > bound) {
-                  const double g0 = A2;
-                  if (((xkm >> c) & 1u) && cr.yl[c] == dc.xcj) {
-                    ksrc += g0 * stk * (double)dc.bp_c * (double)bp_kl;
-                    g3 += g0;
-                  } else {
-                    ksrc += g0 * stk * sub * (double)dc.bp_c * (double)bp_kl;
-                  }
-                }
-              }
-              double g2 = G2c[c] * g;
-              g2 += g3;
+            if (dc.cons) {
               double Bn = G1 * g;
-              Bn += g2;
-              if (lout) lout[k] = Bn;
-              else wrapb[ro + k] = Bn;
-              G2c[c] = g2;
-              G3c[c] = g3;
+              if ((dc.stack >> ch) & 1u) {
+                // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
+                // (k+1, l-1) (row s-2): the next lane's, or the next slot's
+                // lane 0 (slot c+1 not yet updated this row)
+                const double hg = c + 1 < CPL ? bcast_lane0(G3c[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
+                const double ha = c + 1 < CPL ? bcast_lane0(Am2[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
+                const double G3n = wave_shl1(G3c[ch][c], hg);
+                const double A2 = wave_shl1(Am2[ch][c], ha);
+                const bool mt = sok && xk[c] && yl == dc.xcj[ch];
+                ksrc += A2 * bpd * (mt ? dc.cm[ch] : dc.cs[ch]);
+                double g3 = G3n * g;
+                g3 += mt ? A2 : 0.0;
+                double g2 = G2c[ch][c] * g;
+                g2 += g3;
+                Bn += g2;
+                G2c[ch][c] = g2;
+                G3c[ch][c] = g3;
+                Am2[ch][c] = Am1[ch][c];
+                Am1[ch][c] = A;
+              }
+              if (to_link) lout[ch * TW + k] = Bn;
+              else s4c_st64(wrapb + (int64_t)ch * cp + ro, kmax + 1, c, lane, Bn);
             }
+            A = G0;
           }
-        }
-#endif
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          Am2[c] = Am1[c];
-          Am1[c] = cr.A[c];
+          s4c_st64(gout, kmax + 1, c, lane, A);  // the last chain's G0 (i, j_hi)
         }
       }
     }
+    fetch_next(X);  // the row of step t + PF
+    ro += pad4(m + 1 - s);
     if (++s == R) {
       s = 0;
-      cur.advance(W, n, F);
+      ro = 0;
+      cur.advance(W, n, NB, FP);
       dc = describe(cur);
     }
-    if (SK4C_P2P) s4c_publish(done + w, cur.valid(n) ? (int)t + 1 : INT_MAX);
+  };
+  for (int64_t t = 0; t < total; t += 2) {
+    step(t, E);
+    if (t + 1 < total) step(t + 1, O);
   }
   for (int off = 32; off > 0; off >>= 1) ksrc += __shfl_xor(ksrc, off, 64);
-  if (lane == 0) red[w] = bad ? __builtin_nan("") : ksrc;
+  if (lane == 0) red[w] = ksrc;
   __syncthreads();
   if (threadIdx.x == 0) {
     double K = 0.0;
@@ -1322,17 +1130,23 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
 }
 
 int stem4d_col_max_waves(int cpl) {
-  return cpl <= 2 ? s4c_max_waves<2>() : cpl == 4 ? s4c_max_waves<4>() : s4c_max_waves<8>();
+  return cpl <= 1 ? s4c_max_waves<1>() : cpl == 2 ? s4c_max_waves<2>() : cpl == 4 ? s4c_max_waves<4>()
+                                                                          : s4c_max_waves<8>();
 }
 
-size_t stem4d_col_lds_bytes(int cpl, int waves) {
-  return ((size_t)waves * SK4C_D * 64 * cpl + 2 * waves) * sizeof(double);
+int stem4d_col_nb(int cpl) {
+  return cpl <= 1 ? s4c_nb<1>() : cpl == 2 ? s4c_nb<2>() : cpl == 4 ? s4c_nb<4>() : s4c_nb<8>();
 }
 
-hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves,
+size_t stem4d_col_lds_bytes(int cpl, int waves, int m) {
+  const int nb = stem4d_col_nb(cpl);
+  return ((size_t)waves * 2 * nb * 64 * cpl + waves) * sizeof(double) + (size_t)(64 * cpl + m + 1 + 8 + 15) / 16 * 16;
+}
+
+hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves, int max_m,
                              hipStream_t st) {
   if (n_pairs == 0) return hipSuccess;
-  const size_t lds = stem4d_col_lds_bytes(cpl, waves);
+  const size_t lds = stem4d_col_lds_bytes(cpl, waves, max_m);
   const dim3 grid((unsigned)n_pairs), block(64 * waves);
 #define SK_L(C)                                                                                   \
   {                                                                                               \

@@ -712,10 +712,9 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
         std::vector<int32_t> cm;  // prefix maximum of the children's lengths
         int32_t run = -1, placed = 0;
         // done: parents completed by the chunk just formed; their edges are
-        // ready SK_SWEEP_GAP chunks on (pend holds the ones in between; a
-        // chunk with nothing ready is all dummies, so the gap holds)
-        std::vector<int> take, done, pend;
-        while (!ready.empty() || !pend.empty()) {
+        // ready from the next chunk on
+        std::vector<int> take, done;
+        while (!ready.empty()) {
           take.clear();
           done.clear();
           while (!ready.empty() && (int)take.size() < 64) {
@@ -739,12 +738,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
           }
           placed += (int)take.size();
           cm.push_back(run);
-          if (SK_SWEEP_GAP >= 2) {
-            for (int q : pend) push_edges_of(q);  // completed the chunk before: ready from the next on
-            pend.swap(done);
-          } else {
-            for (int q : done) push_edges_of(q);  // ready from the next chunk on
-          }
+          for (int q : done) push_edges_of(q);  // ready from the next chunk on
         }
         if (placed != ne_all) {
           Y.err = "IY sweep schedule: DAG has a cycle";
@@ -1417,9 +1411,8 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
     if (tstats) {
       long tch = 0;
       for (int32_t c : P.ex_nch) tch += c;
-      fprintf(stderr, "[sk pack] y-role %.1f ms (%d threads) + append %.1f ms; sweep chunks %ld (%.2f per y, gap %d)\n",
-              ty1 - tp2, nthr, tnow() - ty1, tch, P.ex_nch.empty() ? 0.0 : (double)tch / P.ex_nch.size(),
-              SK_SWEEP_GAP);
+      fprintf(stderr, "[sk pack] y-role %.1f ms (%d threads) + append %.1f ms; sweep chunks %ld (%.2f per y)\n",
+              ty1 - tp2, nthr, tnow() - ty1, tch, P.ex_nch.empty() ? 0.0 : (double)tch / P.ex_nch.size());
     }
   }
   return SK_OK;
@@ -1889,11 +1882,12 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   const bool banded = ali_phmm || (!ali && kp->len_band > 0);
   const bool gsum = !banded && !std::getenv("SK4_NO_GSUM");
   const size_t nst = gsum ? 2 : 4;
-  // full_dp with one k tile: the pre-combined span kernel; SK4_COL=1 runs the
-  // column-pipelined kernel instead (one workgroup per pair, B' handed on
-  // through LDS; stem4d.hip sk_stem4d_col_kernel): half the bytes, but slower
-  // on MI355X (r04) -- kept as an option and tested
-  const bool colk = gsum && !ktiles && std::getenv("SK4_COL") && !std::getenv("SK4_NO_PRE");
+  // full_dp with one k tile: the column-group kernel (one workgroup per pair,
+  // B' handed on through LDS, NB columns chained per position;
+  // stem4d.hip sk_stem4d_col_kernel); SK4_SPAN=1 (per call, A/B) runs the
+  // pre-combined span kernel instead, SK4_NO_PRE=1 the K-sum span kernel
+  const bool colk = gsum && !ktiles && !std::getenv("SK4_SPAN") && !std::getenv("SK4_NO_PRE");
+  const int col_nb = colk ? sk::stem4d_col_nb(cpl) : 0;
   double total_ms = 0.0;
   int launches = 0;
   Stem4dBatch& Bt = ctx->s4d;
@@ -1910,9 +1904,9 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       p.n = xs_->ex[x[q]].len;
       p.m = ys_->ex[y[q]].len;
       p.plane_doubles = stem4d_plane_doubles(p.m);
-      // column kernel: n G0 planes (slot i) + the round wrap's B' plane;
+      // column kernel: n G0 planes (slot i) + the round wrap's NB B' planes;
       // span kernels: a ring of three spans of n + 1 planes (+ acc)
-      const size_t rb = colk ? ((size_t)(p.n + 1) * (size_t)p.plane_doubles * 8 + 255) & ~(size_t)255
+      const size_t rb = colk ? ((size_t)(p.n + col_nb) * (size_t)p.plane_doubles * 8 + 255) & ~(size_t)255
                              : ((size_t)3 * (p.n + 1) * nst * (size_t)p.plane_doubles * 8 +
                                 (gsum ? (size_t)(p.n + 1) * 8 : 0) + 255) & ~(size_t)255;
       const double pb = (double)rb + (double)(p.n + 1) * (double)kb_stride * 8.0;
@@ -1930,16 +1924,20 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       ++b1;
     }
     if (colk) {
-      // one launch for the batch: W waves per pair, W <= m - 2 for every pair
-      // (the schedule's R >= W + PF + 1) and the class's register budget
+      // one launch for the batch: W waves per pair, W <= m - F - 1 for every
+      // pair (the round wrap's lag, stem4d.hip), the class's register budget
+      // and 160 KB of LDS; full barriers every F = 8 steps where the y's are
+      // long enough, else every step (SK4C_F / SK4C_W: other values, A/B)
+      // (|y| <= 1: no stacking source, K = 1 without a step)
       int min_m = INT32_MAX;
-      for (const auto& p : prs) min_m = std::min(min_m, p.m);
-      // W <= m - F - 1 (the round wrap's lag, stem4d.hip); full barriers every
-      // F = 8 steps where the y's are long enough, else every step
-      // (SK4C_F: another interval, A/B)
+      for (const auto& p : prs)
+        if (p.m >= 2) min_m = std::min(min_m, p.m);
       static const int f_env = std::getenv("SK4C_F") ? std::max(1, std::atoi(std::getenv("SK4C_F"))) : 8;
+      static const int w_env = std::getenv("SK4C_W") ? std::max(1, std::atoi(std::getenv("SK4C_W"))) : 0;
       const int F = min_m - f_env - 1 >= 4 ? f_env : 1;
-      const int W = std::max(1, std::min(sk::stem4d_col_max_waves(cpl), min_m - F - 1));
+      int W = std::max(1, std::min(w_env ? w_env : sk::stem4d_col_max_waves(cpl), min_m - F - 1));
+      W = std::min(W, sk::stem4d_col_max_waves(cpl));
+      while (W > 1 && sk::stem4d_col_lds_bytes(cpl, W, max_m) > 160 * 1024) --W;
       rc = ensure_scratch(ctx, ring_bytes + 64);
       if (rc) return rc;
       if (Bt.cap_pairs < prs.size()) {
@@ -1967,7 +1965,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       L.col_f = F;
       SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
       SK_HIP(ctx, sk::lev_mark(ctx, S));
-      SK_HIP(ctx, sk::launch_stem4d_col(L, (int64_t)prs.size(), cpl, W, S));
+      SK_HIP(ctx, sk::launch_stem4d_col(L, (int64_t)prs.size(), cpl, W, max_m, S));
       SK_HIP(ctx, sk::lev_mark(ctx, S));
       ctx->last_s4d_classes |= 1u << ((cpl == 1 ? 0 : cpl == 2 ? 1 : cpl == 4 ? 2 : 3) + 8);
       ++launches;
@@ -2667,10 +2665,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
 #endif
     ctx->last_launches = (int32_t)classes.size() + (big_x.empty() ? 0 : 1);
   }
-  // SK_STR_SKIP=1: cost experiment only (wrong values): the string kernel of
-  // a stem + string kind is not launched
-  static const bool str_skip = std::getenv("SK_STR_SKIP") != nullptr;
-  if (str && !str_skip) {
+  if (str) {
     const hipStream_t SS = side ? ctx->side : S;
     sk::StrLaunch T;
     T.xset = xs_->dev;
@@ -2750,7 +2745,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   if (mode != sk::kCombineStem && mode != sk::kCombineStr)
     SK_HIP(ctx, sk::launch_combine(d_stem, d_str, out_dev, n, mode, kp->alpha, kp->beta, S));
   // timings: now (synchronous calls), or when sk_sync_timing asks (async)
-  SK_HIP(ctx, sk::call_finish(ctx, S, stem, str && !str_skip));
+  SK_HIP(ctx, sk::call_finish(ctx, S, stem, str));
   return SK_OK;
 }
 

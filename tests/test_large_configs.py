@@ -28,9 +28,12 @@ DAG = np.load(os.path.join(GOLDEN, "large_dag.npz"))
 S4D = np.load(os.path.join(GOLDEN, "large_4d.npz"))
 BPLA = np.load(os.path.join(GOLDEN, "large_bpla.npz"))
 SETS = ["c2_L150", "ns_L200", "c5_L300", "wide_L380_420"]
+# 6, 7: the log compositions, 7 the north star's LSuStemStrKernel (the CLI's
+# --log mode): components as the fixtures' K0 (SuStemKernel()) and K2
+# (StringKernel(gap=0.8, alpha=0.2)), which are LSuStemStrKernel()'s
 STR_KINDS = {0: ska.SuStemKernel(), 1: ska.SiStemKernel(), 2: ska.StringKernel(gap=0.8, alpha=0.2),
              3: ska.StringKernel(gap=0.8, match=1.0, mismatch=0.8), 4: ska.SuStemStrKernel(),
-             5: ska.SiStemStrKernel()}
+             5: ska.SiStemStrKernel(), 6: ska.LSuStemKernel(), 7: ska.LSuStemStrKernel()}
 
 
 def _digest(rows_list):
@@ -42,6 +45,13 @@ def _digest(rows_list):
 
 
 def _expected(name, kind):
+    """the fixtures' components, composed in oracle/pyoracle.py kernel_value's
+    operation order (def_kernel.h:113-138, :165-190)"""
+    p = STR_KINDS[kind].params
+    if kind == 6:
+        return p.beta * np.log(DAG[f"{name}_K0"]) + 0.0
+    if kind == 7:
+        return (p.beta * np.log(DAG[f"{name}_K0"]) + 0.0) + (p.alpha * np.log(DAG[f"{name}_K2"]) + 0.0)
     if kind == 4:
         return DAG[f"{name}_K0"] + DAG[f"{name}_K2"]
     if kind == 5:
@@ -126,7 +136,7 @@ def test_dag_pairs_at_config_size(gpu_ctx, dag_sets, name, kind):
     x, y = (a.ravel() for a in np.meshgrid(np.arange(n), np.arange(n), indexing="ij"))
     got = gpu_ctx.pairs(ds, STR_KINDS[kind], x, y).reshape(n, n)
     assert rel_err(got, _expected(name, kind)) < TOL
-    if kind in (0, 1, 4, 5):
+    if kind in (0, 1, 4, 5, 6, 7):
         nl = [int(np.sum(ds.dag(i)["n_edges"] > 0)) for i in range(n)]
         assert gpu_ctx.last_classes()["stem_maxk"] == sorted({_maxk(v) for v in nl})
 

@@ -89,17 +89,17 @@ def test_stem4d_ksum_equals_four_state(gpu_ctx, monkeypatch, mode):
     stacking source) against the four-state planes
     (SK4_NO_GSUM=1): equal up to the association of non-negative sums, CPL
     1-4, empty and one-residue sequences included, both against the oracle.
-    "pre" runs the pre-combined kernel (sk_stem4d_pre_kernel, the default for
-    |y| < 512), "col" the column-pipelined kernel (SK4_COL=1), "ksum" the
-    K-sum kernel (sk_stem4d_gsum_kernel) on the same short sequences
-    (SK4_NO_PRE=1)."""
+    "col" runs the column-group kernel (sk_stem4d_col_kernel, the default for
+    |y| < 512), "pre" the pre-combined span kernel (sk_stem4d_pre_kernel,
+    SK4_SPAN=1), "ksum" the K-sum span kernel (sk_stem4d_gsum_kernel) on the
+    same short sequences (SK4_NO_PRE=1)."""
     seqs = _seqs() + ["", "G"] + ska.random_sequences(2, 130, 0x5EED0043)
     ds, _ = make_examples(seqs)
     kern = ska.StemKernel4D()
     if mode == "ksum":
         monkeypatch.setenv("SK4_NO_PRE", "1")
-    if mode == "col":
-        monkeypatch.setenv("SK4_COL", "1")
+    if mode == "pre":
+        monkeypatch.setenv("SK4_SPAN", "1")
     a = gpu_ctx.gram(ds, kern)
     assert bool(gpu_ctx.last_classes()["stem4d_col"]) == (mode == "col")
     monkeypatch.setenv("SK4_NO_GSUM", "1")

@@ -1,13 +1,15 @@
-"""CPU check of the column-pipelined 4-D schedule (stem4d.hip
+"""CPU check of the column-group 4-D schedule (stem4d.hip
 sk_stem4d_col_kernel): a step-by-step numpy emulation of the kernel's waves --
-positions, rows, the LDS B' double buffer by step parity, the round-wrap B'
-plane, the in-place G0 planes, the PF-rows-ahead fetch cursor -- in which
-every read of a step sees memory as it was when the step began and every
-write lands when it ends.  A schedule that read anything before it was
-written (a race between waves on the GPU) gives a different K; the emulated
-K must equal the C oracle's full_dp (stem_kernel/stem_kernel.cpp:282-351)
-for several (n, m, W), including W at the host's limit m - 2 and ragged
-lengths."""
+column groups of NB columns, positions, rows, the chains of one position (one
+per column of the group, each chain's G0 row the next chain's A row), the LDS
+B' double buffer by step parity, the round-wrap B' planes (one per chain), the
+in-place G0 planes, the PF-rows-ahead fetch cursor -- in which every read of a
+step sees memory as it was when the step began, an LDS write lands when the
+step ends and a global write at the next full barrier.  A schedule that read
+anything before it was written (a race between waves on the GPU) gives a
+different K (unwritten memory is NaN); the emulated K must equal the C
+oracle's full_dp (stem_kernel/stem_kernel.cpp:282-351) for several (n, m, W,
+F, NB), including W at the host's limit m - F - 1 and groups cut short by n."""
 import numpy as np
 import pytest
 
@@ -17,23 +19,30 @@ from oracle import pyoracle as po
 PF = 2
 
 
-def cols(j, F, pf=PF):
-    return max(j, F + pf)
+def group_positions(g, n, nb, F, pf=PF):
+    """positions of column group g: its planes (i = j_hi - 1 down to 0),
+    then bubbles up to F + PF"""
+    j_hi = min((g + 1) * nb, n)
+    return max(j_hi, F + pf)
 
 
 class Pos:
+    """stem4d.hip S4cPos: (group, offset in the group)"""
     def __init__(self):
-        self.j, self.off = 1, 0
+        self.g, self.off = 0, 0
 
-    def advance(self, W, n, F, pf=PF):
+    def advance(self, W, n, nb, F, pf=PF):
         self.off += W
-        while self.j <= n and self.off >= cols(self.j, F, pf):
-            self.off -= cols(self.j, F, pf)
-            self.j += 1
+        while self.g * nb < n and self.off >= group_positions(self.g, n, nb, F, pf):
+            self.off -= group_positions(self.g, n, nb, F, pf)
+            self.g += 1
+
+    def valid(self, n, nb):
+        return self.g * nb < n
 
     def copy(self):
         q = Pos()
-        q.j, q.off = self.j, self.off
+        q.g, q.off = self.g, self.off
         return q
 
 
@@ -57,7 +66,7 @@ def bpdiag(seq, bpp):
     return np.array(out, np.float32)
 
 
-def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None, pf=PF):
+def emulate(x, bx, y, by, W, F=1, nb=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None, pf=PF):
     """F: steps between full barriers -- a global store of step u is seen
     from the first multiple of F above u on; LDS stores from the next step."""
     n, m = len(x), len(y)
@@ -71,24 +80,38 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
         gpow.append(gpow[-1] * g)
     bpx, bpy = bpdiag(x, bx), bpdiag(y, by)
     cp = row_off(m, m + 1)
-    mem = {"planes": np.full(max(n, 1) * cp + cp, np.nan), "lds": np.full((W, 2, TW), np.nan)}
-    np_ = sum(cols(j, F, pf) for j in range(1, n + 1))
+    G = -(-n // nb)
+    mem = {"planes": np.full(max(n, 1) * cp + nb * cp, np.nan),
+           "lds": np.full((W, 2, nb, TW), np.nan)}
+    wrap0 = max(n, 1) * cp
+    np_ = sum(group_positions(gg, n, nb, F, pf) for gg in range(G))
     total = ((np_ - 1) // W) * R + (np_ - 1) % W + R if np_ else 0
     k = np.arange(TW)
     yk = np.array([y[kk] if kk < m else "\0" for kk in k])
 
+    def bp_x(a, b):  # prob(a, b), a <= b
+        e = b - a
+        return bpx[e * n - e * (e - 1) // 2 + a]
+
     def describe(q):
-        on = q.j <= n and q.off < q.j
-        d = dict(on=on, i=q.j - 1 - q.off if on else 0, j=q.j if on else 1)
-        d["first"] = d["i"] == d["j"] - 1
-        d["cons"] = on and d["i"] >= 1
-        d["bp_c"] = np.float32(0)
-        d["xci"] = d["xcj"] = "\0"
+        d = dict(on=False, i=0, c0=0, nbg=0, bnd=False, cons=False, stack=[False] * nb,
+                 bp_c=[np.float32(0)] * nb, xcj=["\0"] * nb, xci="\0", j_lo=1)
+        if not q.valid(n, nb):
+            return d
+        j_lo, j_hi = q.g * nb + 1, min((q.g + 1) * nb, n)
+        d["j_lo"] = j_lo
+        d["nbg"] = j_hi - j_lo + 1
+        if q.off >= j_hi:
+            return d
+        i = j_hi - 1 - q.off
+        d.update(on=True, i=i, c0=max(0, i + 1 - j_lo), bnd=i + 1 >= j_lo, cons=i >= 1)
         if d["cons"]:
-            e = d["j"] - d["i"]
-            d["bp_c"] = bpx[e * n - e * (e - 1) // 2 + d["i"] - 1]
-            d["xci"], d["xcj"] = x[d["i"] - 1], x[d["j"] - 1]
-        d["stack"] = d["cons"] and d["bp_c"] > bound
+            d["xci"] = x[i - 1]
+            for c in range(d["c0"], d["nbg"]):
+                jp = j_lo + c
+                d["bp_c"][c] = bp_x(i - 1, jp - 1)
+                d["xcj"][c] = x[jp - 1]
+                d["stack"][c] = d["bp_c"][c] > bound
         return d
 
     class Wave:
@@ -97,13 +120,13 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
     for w in range(W):
         v = Wave()
         v.cur = Pos()
-        v.cur.advance(w, n, F, pf)
+        v.cur.advance(w, n, nb, F, pf)
         v.dc = describe(v.cur)
         v.fpos, v.df, v.fs = v.cur.copy(), dict(v.dc), 0
         v.rows = []
         v.s = 0
         v.ksrc = np.zeros(TW)
-        v.Am1, v.Am2, v.G2c, v.G3c = (np.zeros(TW) for _ in range(4))
+        v.Am1, v.Am2, v.G2c, v.G3c = ([np.zeros(TW) for _ in range(nb)] for _ in range(4))
         waves.append(v)
 
     def fetch(v, snap, w):
@@ -112,24 +135,24 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
         ro = row_off(m, s)
         ok = d["on"] and s >= 1
         msk = ok & (k <= kmax)
-        r = dict(A=np.zeros(TW), Bw=np.zeros(TW), bp=np.zeros(TW, np.float32), yl=np.array(["\0"] * TW))
+        r = dict(A=np.zeros(TW), Bw=[np.zeros(TW) for _ in range(nb)], bp=np.zeros(TW, np.float32),
+                 yl=np.array(["\0"] * TW))
         if ok:
             kk = k[msk]
-            if d["first"]:
-                r["A"][msk] = gpow[s]
-            else:
+            if not d["bnd"]:
                 r["A"][msk] = snap["planes"][d["i"] * cp + ro + kk]
-            if w == 0 and not d["first"]:
-                r["Bw"][msk] = snap["planes"][n * cp + ro + kk]
-            if d["stack"]:
-                e2 = s - 1
-                ye = e2 * m - e2 * (e2 - 1) // 2
-                r["bp"][msk] = bpy[ye + kk]
-                r["yl"][msk] = np.array(list(y))[kk + s - 1]
+            if w == 0:
+                for c in range(d["c0"], d["nbg"]):
+                    if c > d["c0"] or not d["bnd"]:
+                        r["Bw"][c][msk] = snap["planes"][wrap0 + c * cp + ro + kk]
+            e2 = s - 1
+            ye = e2 * m - e2 * (e2 - 1) // 2
+            r["bp"][msk] = bpy[ye + kk]
+            r["yl"][msk] = np.array(list(y))[kk + s - 1]
         v.fs += 1
         if v.fs == R:
             v.fs = 0
-            v.fpos.advance(W, n, F, pf)
+            v.fpos.advance(W, n, nb, F, pf)
             v.df = describe(v.fpos)
         return r
 
@@ -154,7 +177,7 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
         snap = {kk: vv.copy() for kk, vv in mem.items()}
         writes = []
         for w, v in enumerate(waves):
-            if not v.cur.j <= n:
+            if not v.cur.valid(n, nb):
                 continue
             if t < w:
                 if t >= w - pf:
@@ -167,44 +190,54 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
             if dc["on"]:
                 kmax = m - s
                 msk = k <= kmax
+                kk = k[msk]
+                i = dc["i"]
                 if s == 0:
-                    v.Am1 = np.where(dc["stack"] & (k <= m), gpow[dc["j"] - 1 - dc["i"]], 0.0)
-                    v.Am2, v.G2c, v.G3c = np.zeros(TW), np.zeros(TW), np.zeros(TW)
+                    for c in range(dc["c0"], dc["nbg"]):
+                        jp = dc["j_lo"] + c
+                        v.Am1[c] = np.where(dc["stack"][c] & (k <= m), gpow[jp - 1 - i], 0.0)
+                        v.Am2[c], v.G2c[c], v.G3c[c] = np.zeros(TW), np.zeros(TW), np.zeros(TW)
                 else:
                     ro = row_off(m, s)
-                    G3n, A2 = shl1(v.G3c), shl1(v.Am2)
-                    if dc["first"]:
-                        G1 = np.zeros(TW)
-                    elif w == 0:
-                        G1 = cr["Bw"]
-                    else:
-                        G1 = snap["lds"][w - 1, (t - 1) & 1].copy()
-                    G0 = cr["A"] * g + G1
-                    kk = k[msk]
-                    writes.append(("planes", dc["i"] * cp + ro + kk, G0[msk]))
-                    if dc["cons"]:
-                        g3 = G3n * g
-                        if dc["stack"] and s >= 2:
-                            src = msk & (cr["bp"] > bound)
-                            match = (yk == dc["xci"]) & (cr["yl"] == dc["xcj"])
-                            a = src & match
-                            b = src & ~match
-                            v.ksrc[a] += A2[a] * stk * float(dc["bp_c"]) * cr["bp"][a].astype(np.float64)
-                            g3[a] += A2[a]
-                            v.ksrc[b] += A2[b] * stk * sub * float(dc["bp_c"]) * cr["bp"][b].astype(np.float64)
-                        g2 = v.G2c * g + g3
-                        Bn = G1 * g + g2
-                        if w + 1 < W:
-                            writes.append(("lds", (w, t & 1, kk), Bn[msk]))
+                    A = np.where(msk, gpow[s], 0.0) if dc["bnd"] else cr["A"]
+                    for c in range(dc["c0"], dc["nbg"]):
+                        if c == dc["c0"] and dc["bnd"]:
+                            G1 = np.zeros(TW)
+                        elif w == 0:
+                            G1 = cr["Bw"][c]
                         else:
-                            writes.append(("planes", n * cp + ro + kk, Bn[msk]))
-                        v.G2c = np.where(msk, g2, v.G2c)
-                        v.G3c = np.where(msk, g3, v.G3c)
-                    v.Am2, v.Am1 = v.Am1, cr["A"]
+                            G1 = snap["lds"][w - 1, (t - 1) & 1, c].copy()
+                        G0 = A * g + G1
+                        if dc["cons"]:
+                            if dc["stack"][c]:
+                                G3n, A2 = shl1(v.G3c[c]), shl1(v.Am2[c])
+                                g3 = G3n * g
+                                src = msk & (cr["bp"] > bound)
+                                match = (yk == dc["xci"]) & (cr["yl"] == dc["xcj"][c])
+                                a = src & match
+                                b = src & ~match
+                                bpc = float(dc["bp_c"][c])
+                                v.ksrc[a] += A2[a] * stk * bpc * cr["bp"][a].astype(np.float64)
+                                g3[a] += A2[a]
+                                v.ksrc[b] += A2[b] * stk * sub * bpc * cr["bp"][b].astype(np.float64)
+                                g2 = v.G2c[c] * g + g3
+                                v.G2c[c] = np.where(msk, g2, v.G2c[c])
+                                v.G3c[c] = np.where(msk, g3, v.G3c[c])
+                            else:
+                                g2 = 0.0
+                            Bn = G1 * g + g2
+                            if w + 1 < W:
+                                writes.append(("lds", (w, t & 1, c, kk), Bn[msk]))
+                            else:
+                                writes.append(("planes", wrap0 + c * cp + ro + kk, Bn[msk]))
+                        if dc["stack"][c]:
+                            v.Am2[c], v.Am1[c] = v.Am1[c], A
+                        A = G0
+                    writes.append(("planes", i * cp + ro + kk, A[msk]))
             v.s += 1
             if v.s == R:
                 v.s = 0
-                v.cur.advance(W, n, F, pf)
+                v.cur.advance(W, n, nb, F, pf)
                 v.dc = describe(v.cur)
         for name, idx, val in writes:
             if name == "lds":
@@ -214,12 +247,7 @@ def emulate(x, bx, y, by, W, F=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=
     return 1.0 + sum(float(v.ksrc.sum()) for v in waves)
 
 
-@pytest.mark.parametrize("n,m,W,F", [(9, 11, 3, 1), (12, 7, 5, 1), (6, 14, 12, 1), (1, 5, 3, 1),
-                                     (0, 6, 2, 1), (10, 4, 2, 1), (7, 9, 1, 1), (13, 13, 11, 1),
-                                     (12, 17, 4, 8), (10, 21, 12, 8), (16, 13, 4, 8), (5, 30, 12, 8),
-                                     (8, 30, 4, 16), (6, 40, 12, 24)])
-@pytest.mark.parametrize("pf", [2, 1])
-def test_column_schedule_equals_oracle(n, m, W, F, pf):
+def _case(n, m):
     seqs = ska.random_sequences(2, max(n, m, 1), 0x5EED0C01 + n * 31 + m)
     x, y = seqs[0][:n].lower(), seqs[1][:m].lower()
     # dense base-pair probabilities (every cell a stacking source), so that any
@@ -227,10 +255,40 @@ def test_column_schedule_equals_oracle(n, m, W, F, pf):
     rng = np.random.default_rng(n * 1000 + m)
     bx = rng.uniform(0.05, 0.6, n * (n - 1) // 2)
     by = rng.uniform(0.05, 0.6, m * (m - 1) // 2)
+    return x, bx, y, by
+
+
+def _ref(x, bx, y, by):
+    f = lambda v: float(np.float32(v))  # the CLI's float options, as StemKernel4D rounds them
+    return po.stem4d(x, bx, y, by, f(0.8), f(1.0), f(0.5), 0.0)
+
+
+@pytest.mark.parametrize("n,m,W,F", [(9, 11, 3, 1), (12, 7, 5, 1), (6, 14, 12, 1), (1, 5, 3, 1),
+                                     (0, 6, 2, 1), (10, 4, 2, 1), (7, 9, 1, 1), (13, 13, 11, 1),
+                                     (12, 17, 4, 8), (10, 21, 12, 8), (16, 13, 4, 8), (5, 30, 12, 8),
+                                     (8, 30, 4, 16), (6, 40, 12, 24)])
+@pytest.mark.parametrize("pf", [2, 1])
+def test_column_schedule_equals_oracle(n, m, W, F, pf):
+    x, bx, y, by = _case(n, m)
     assert W <= max(1, m - F - 1)  # the host's limit (the round wrap's lag)
     got = emulate(x, bx, y, by, W, F, pf=pf)
-    f = lambda v: float(np.float32(v))  # the CLI's float options, as StemKernel4D rounds them
-    ref = po.stem4d(x, bx, y, by, f(0.8), f(1.0), f(0.5), 0.0)
+    ref = _ref(x, bx, y, by)
+    assert abs(got - ref) <= 1e-12 * abs(ref), (got, ref)
+
+
+@pytest.mark.parametrize("n,m,W,F", [(9, 11, 3, 1), (12, 7, 5, 1), (13, 13, 11, 1), (1, 5, 3, 1),
+                                     (0, 6, 2, 1), (10, 4, 2, 1), (7, 9, 1, 1), (11, 17, 4, 8),
+                                     (14, 21, 12, 8), (16, 13, 4, 8), (5, 30, 12, 8), (17, 30, 8, 8)])
+@pytest.mark.parametrize("nb", [2, 3, 4])
+def test_column_group_schedule_equals_oracle(n, m, W, F, nb):
+    """NB columns per group (one chain each per position): groups cut short
+    by n (n % NB != 0), the top triangle of a group (positions with fewer
+    chains, the first of them a boundary plane), the round wrap of every
+    chain."""
+    x, bx, y, by = _case(n, m)
+    assert W <= max(1, m - F - 1)
+    got = emulate(x, bx, y, by, W, F, nb=nb)
+    ref = _ref(x, bx, y, by)
     assert abs(got - ref) <= 1e-12 * abs(ref), (got, ref)
 
 
@@ -240,10 +298,10 @@ def test_emulation_sees_a_broken_schedule():
     rng = np.random.default_rng(5)
     x, y = "acguacgua", "ggcaugcaucc"
     bx, by = rng.uniform(0.05, 0.6, 36), rng.uniform(0.05, 0.6, 55)
-    f = lambda v: float(np.float32(v))
-    ref = po.stem4d(x, bx, y, by, f(0.8), f(1.0), f(0.5), 0.0)
-    assert abs(emulate(x, bx, y, by, 9) - ref) <= 1e-12 * ref
-    bad = emulate(x, bx, y, by, 11)
-    assert not abs(bad - ref) <= 1e-12 * ref
-    # with full barriers every F = 8 steps, W = m - 2 is past the limit m - F - 1
-    assert not abs(emulate(x, bx, y, by, 9, F=8) - ref) <= 1e-12 * ref
+    ref = _ref(x, bx, y, by)
+    for nb in (1, 3):
+        assert abs(emulate(x, bx, y, by, 9, nb=nb) - ref) <= 1e-12 * ref
+        bad = emulate(x, bx, y, by, 11, nb=nb)
+        assert not abs(bad - ref) <= 1e-12 * ref
+        # with full barriers every F = 8 steps, W = m - 2 is past the limit m - F - 1
+        assert not abs(emulate(x, bx, y, by, 9, F=8, nb=nb) - ref) <= 1e-12 * ref
