@@ -47,6 +47,8 @@ $(BUILD)/%.o: $(ROOT)stem_kernel_amd/csrc/%.hip $(HDRS)
 # the PairHMM's log-space sums must round like the host restatement
 $(BUILD)/kernels/phmm.o: HIPFLAGS += -ffp-contract=off
 $(BUILD)/kernels/bpla_grad.o: HIPFLAGS += -ffp-contract=off
+# the synthetic fold's AVX2 clone and baseline must round alike (no FMA)
+$(BUILD)/host/synth.o: CXXFLAGS += -ffp-contract=off
 
 $(LIB): $(HOST_OBJ) $(HIP_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

@@ -709,8 +709,9 @@ def main():
     S = a.slices
     if a.full:
         a.steps, a.warmup = 1, 0
-    if not cfg.get("whole"):
-        S = max(S, (a.warmup + a.steps) * world)
+    # the configured step size whatever --steps is: past S / N steps the slices
+    # repeat (each step recomputed in full, as C2's whole-Gram steps repeat),
+    # rather than shrinking the step to (warmup + steps) * N slices
     S = -(-S // world) * world  # a multiple of N: rank r's slices are cells k % N == r
     slice_of, per, step_kind, n_cells = make_plan(kind, a.n, world, rank, S)
     eng.alloc(per)

@@ -249,6 +249,39 @@ struct sk_context {
   void* comm = nullptr;
 };
 
+// Host thread pools: f(t) for t = 1..n-1 on new threads, f(0) on the calling
+// thread; a slice whose thread cannot be created (std::system_error) runs on
+// the calling thread too, so a pool never escapes through the C ABI.  The
+// no-index form is for workers that share an atomic cursor.
+template <class F>
+void run_slices(int n, F&& f) {
+  std::vector<std::thread> th;
+  std::vector<int> here;
+  for (int t = 1; t < n; ++t) {
+    try {
+      th.emplace_back(f, t);
+    } catch (const std::system_error&) {
+      here.push_back(t);
+    }
+  }
+  f(0);
+  for (int t : here) f(t);
+  for (auto& x : th) x.join();
+}
+template <class F>
+void run_pool(int n, F&& work) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < n; ++t) {
+    try {
+      th.emplace_back(work);
+    } catch (const std::system_error&) {
+      break;  // the calling thread's share drains the cursor
+    }
+  }
+  work();
+  for (auto& x : th) x.join();
+}
+
 namespace sk {
 hipStream_t ctx_stream(sk_context* ctx) { return ctx->stream; }
 
@@ -316,7 +349,14 @@ hipError_t call_begin(sk_context* ctx) {
     if ((r = tset_resolve(ctx, k)) != hipSuccess) return r;  // the ring came round
     ctx->tk = k;
     sk_context::Stage& G = ctx->stage[ctx->ncalls++ & 1];
-    if (G.recorded && (r = hipEventSynchronize(G.ev)) != hipSuccess) return r;
+    if (G.recorded) {
+      if ((r = hipEventSynchronize(G.ev)) != hipSuccess) return r;
+    } else if (G.blk || G.off) {
+      // the slot's call staged copies but failed before call_finish recorded
+      // its event: the copy engine may still read the pinned bytes
+      if ((r = hipStreamSynchronize(ctx->stream)) != hipSuccess) return r;
+      if (ctx->cps && (r = hipStreamSynchronize(ctx->cps)) != hipSuccess) return r;
+    }
     G.recorded = false;
     G.blk = G.off = 0;
   } else {
@@ -597,10 +637,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
         }
       }
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nthr; ++t) th.emplace_back(keys, t);
-    keys(0);
-    for (auto& t : th) t.join();
+    run_slices(nthr, keys);
     for (int t = 0; t < nthr; ++t) {
       P.gam_key.insert(P.gam_key.end(), tk[t].begin(), tk[t].end());
       phi_raw.insert(phi_raw.end(), tp[t].begin(), tp[t].end());
@@ -1241,10 +1278,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
     auto work = [&]() {
       for (int e = next.fetch_add(1); e < n; e = next.fetch_add(1)) pack_x(e, xo[e]);
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nthr; ++t) th.emplace_back(work);
-    work();
-    for (auto& t : th) t.join();
+    run_pool(nthr, work);
     tpx = tnow();
     P.ex_node_base.push_back(0);
     P.ex_edge_base.push_back(0);
@@ -1313,10 +1347,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
           O = XOut();  // free as we go
         }
       };
-      std::vector<std::thread> tc;
-      for (int t = 1; t < nthr; ++t) tc.emplace_back(copy);
-      copy();
-      for (auto& t : tc) t.join();
+      run_pool(nthr, copy);
     }
     if (tstats) fprintf(stderr, "[sk pack] offsets %.1f ms, resize %.1f ms, copy %.1f ms\n", tq1 - tpx, tq2 - tq1, tnow() - tq2);
 #undef SK_BIG
@@ -1365,10 +1396,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
     auto work = [&]() {
       for (size_t e = next.fetch_add(1); e < yjobs.size(); e = next.fetch_add(1)) pack_y(yjobs[e], yo[e]);
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nthr; ++t) th.emplace_back(work);
-    work();
-    for (auto& t : th) t.join();
+    run_pool(nthr, work);
     const double ty1 = tnow();
     // appended at prefix-sum offsets, copied on the threads (as the x role)
     const size_t ny = yo.size();
@@ -1403,10 +1431,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
         Y = YOut();  // free as we go
       }
     };
-    th.clear();
-    for (int t = 1; t < nthr; ++t) th.emplace_back(copy);
-    copy();
-    for (auto& t : th) t.join();
+    run_pool(nthr, copy);
 #undef SK_YBIG
     if (tstats) {
       long tch = 0;
@@ -3205,10 +3230,7 @@ int sk_dataset_add_synthetic_rows(sk_dataset* ds, int32_t n, int32_t n_rows,
       }
     }
   };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
-  work();
-  for (auto& t : pool) t.join();
+  run_pool(nt, work);
   if (stats)
     std::fprintf(stderr, "[sk] synthetic examples: %d on %d threads, fold %.3f s, build %.3f s (thread-seconds)\n", n,
                  nt, ns_fold.load() * 1e-9, ns_build.load() * 1e-9);
@@ -3780,10 +3802,7 @@ int add_examples_threaded(sk_dataset* ds, int32_t n, int32_t n_rows, const char*
       }
     }
   };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
-  work();
-  for (auto& t : pool) t.join();
+  run_pool(nt, work);
   if (status.load() != SK_OK) {
     ds->ex.resize(base);
     ds->labels.resize(base);
