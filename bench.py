@@ -216,17 +216,39 @@ def stem4d_cells(lens, x, y):
     return float(np.sum((n + 1) * (n + 2) / 2 * (m + 1) * (m + 2) / 2))
 
 
-def algorithmic(kind, shapes, x, y):
-    """(bound, unit, peak, model description, algorithmic work of the pairs)."""
+def dag_row_bytes(rt, x, y):
+    """Row transfers of the DAG stem kernel's gamma schedule,
+    from sk_dataset_row_traffic: per pair (x, y) every transfer of one of x's
+    rows moves 8 * y_slots(y) bytes.  (lower, schedule): the compulsory bytes
+    -- each stored row written once and read back once (a second parent's
+    read could be an L2 hit) -- and every transfer the schedule issues
+    (stored rows, slab / Gamma / Phi child-row reads; register-held rows
+    move nothing)."""
+    slot_b = 8.0 * rt[y, 6]
+    lower = float(np.sum(slot_b * 2.0 * rt[x, 1]))
+    sched = float(np.sum(slot_b * (rt[x, 1] + rt[x, 2] + rt[x, 3] + rt[x, 4])))
+    return lower, sched
+
+
+def algorithmic(kind, shapes, x, y, rt=None):
+    """(bound, unit, peak, model description, algorithmic work of the pairs,
+    extra model figures)."""
     lens = shapes[:, 4]
     if kind in ("ss", "stem"):
+        survey = dag_bytes(shapes, x, y)
+        if rt is None:
+            return "hbm", "GB/s", PEAK_HBM_GBS, \
+                "SURVEY §8d: 32*|Vx|*|Vy| + S(x) + S(y) + 8 bytes per pair", survey, {}
+        lower, sched = dag_row_bytes(rt, x, y)
         return "hbm", "GB/s", PEAK_HBM_GBS, \
-            "SURVEY §8d: 32*|Vx|*|Vy| + S(x) + S(y) + 8 bytes per pair", dag_bytes(shapes, x, y)
+            "compulsory row traffic of the gamma schedule: 2 x 8 B x y_slots(y) per row of x stored " \
+            "in the HBM slab (written once, read back once; sk_dataset_row_traffic, DESIGN.md §6)", lower, \
+            {"schedule_bytes": sched, "survey_model_bytes": survey}
     if kind == "stem4d":
         if os.environ.get("SK4_NO_GSUM"):  # the four-state planes (A/B switch)
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 "SURVEY §8d: 72 B per (i,j,k,l) cell, [n(n+1)/2][m(m+1)/2] cells", \
-                72.0 * stem4d_cells(lens, x, y)
+                72.0 * stem4d_cells(lens, x, y), {}
         col = not (os.environ.get("SK4_SPAN") or os.environ.get("SK4_NO_PRE"))
         if col and int(lens[y].max()) + 1 <= 512:
             # column groups (stem4d.hip sk_stem4d_col_kernel): G0 of (i, j_lo-1)
@@ -237,7 +259,7 @@ def algorithmic(kind, shapes, x, y):
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 f"16/NB B per (i,j,k,l) cell (G0 read by a group's first column, written by its last; " \
                 f"NB = {NB}) + 16/W B (W = {W}: every W-th position's pre-combined G1 across the round " \
-                "wrap), [n(n+1)/2][m(m+1)/2] cells", (16.0 / NB + 16.0 / W) * stem4d_cells(lens, x, y)
+                "wrap), [n(n+1)/2][m(m+1)/2] cells", (16.0 / NB + 16.0 / W) * stem4d_cells(lens, x, y), {}
         if os.environ.get("SK4_NO_PRE") or int(lens[y].max()) + 1 > 512:
             # full_dp with the K chain summed (stem4d.hip): G0, G1 written once
             # (16 B), G0 of (i,j-1), G1 of (i+1,j) and the stacking G0 of
@@ -246,15 +268,15 @@ def algorithmic(kind, shapes, x, y):
             return "hbm", "GB/s", PEAK_HBM_GBS, \
                 "40 B per (i,j,k,l) cell (G0, G1 written; G0, G1, stacking G0 read; SURVEY §8d's 72 B " \
                 "less the K states, which are summed), [n(n+1)/2][m(m+1)/2] cells", \
-                40.0 * stem4d_cells(lens, x, y)
+                40.0 * stem4d_cells(lens, x, y), {}
         # + each plane's stacking chain produced one span early (pre-combined G1)
         return "hbm", "GB/s", PEAK_HBM_GBS, \
             "32 B per (i,j,k,l) cell (G0 and the consumer's pre-combined G1 written, G0 and the own " \
             "pre-combined G1 read; SURVEY §8d's 72 B less the summed K states and the stacking read), " \
-            "[n(n+1)/2][m(m+1)/2] cells", 32.0 * stem4d_cells(lens, x, y)
+            "[n(n+1)/2][m(m+1)/2] cells", 32.0 * stem4d_cells(lens, x, y), {}
     return "valu", "TFLOP/s", PEAK_FP64_TFS, \
         "SURVEY §8d: 24 flop per cell (exp counted as 1), Lx*Ly cells", \
-        24.0 * float(np.sum(lens[x].astype(np.float64) * lens[y]))
+        24.0 * float(np.sum(lens[x].astype(np.float64) * lens[y])), {}
 
 
 def load_profile(config, kind, length, path=None):
@@ -272,20 +294,26 @@ def load_profile(config, kind, length, path=None):
     return pm, pm.get("source_hash") == provenance.source_hash(), path
 
 
-def roofline(config, kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, cells, pmc_json=None):
+def roofline(config, kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, cells, pmc_json=None, rt=None):
     """The dominant kernel's roofline.
 
     HBM-bound kernels (DAG stem, 4-D stem): the headline `achieved` is the
     MEASURED HBM bytes per launch (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, per
     cell, scaled to this run's cells) over the launches' span per launch (the
     launches run on several streams and overlap: span / launches), so `frac`
-    cannot pass 1.  The survey's algorithmic bytes give `model_frac` (same
-    time base) and `model_frac_per_launch` (over the average launch duration,
-    no overlap credit).  A profile measured on other kernel sources is
-    `stale`: then `traffic` is null and `frac` falls back to the model per
-    launch (`basis` says which).  FP64 kernels (BPLA): algorithmic flops per
-    launch over the average launch duration."""
-    bound, unit, peak, model, alg = algorithmic(kind, shapes, xs, ys)
+    cannot pass 1.  `algorithmic_per_launch` is the implemented algorithm's
+    compulsory bytes (DAG: the gamma schedule's stored rows written and read
+    back once, `dag_row_bytes`; 4-D: 16/NB + 16/W B per cell), a lower bound
+    of the measured bytes; `algorithmic_frac` puts it over the same span.  The
+    DAG kernel also reports every row transfer its schedule issues
+    (`schedule_bytes_per_launch`) and SURVEY §8d's model bytes
+    (`survey_model_bytes_per_launch`, no fraction: the path-sum, gamma and phi
+    reformulation never moves them).  A profile measured on other kernel
+    sources is `stale`: then `traffic` is null and `frac` falls back to the
+    algorithmic bytes over the average launch duration (`basis` says which).
+    FP64 kernels (BPLA): algorithmic flops per launch over the average launch
+    duration."""
+    bound, unit, peak, model, alg, extra = algorithmic(kind, shapes, xs, ys, rt)
     n_launch = max(1, n_launch)
     avg_s = sum_ms / n_launch * 1e-3
     eff_s = span_ms / n_launch * 1e-3
@@ -305,9 +333,10 @@ def roofline(config, kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, ce
          "profile_source_hash": pm.get("source_hash") if pm else None,
          "profile_git_head": pm.get("git_head") if pm else None,
          "stale": (not fresh) if pm is not None else None}
+    for k, v in extra.items():
+        r[k + "_per_launch"] = v / n_launch
     if bound == "hbm":
-        r["model_frac"] = alg_pl / eff_s / scale / peak if eff_s > 0 else None
-        r["model_frac_per_launch"] = alg_pl / avg_s / scale / peak if avg_s > 0 else None
+        r["algorithmic_frac"] = alg_pl / eff_s / scale / peak if eff_s > 0 else None
         if traffic is not None and fresh and eff_s > 0:
             r["achieved"] = traffic / eff_s / scale
             r["basis"] = ("measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, " + rel +
@@ -315,7 +344,7 @@ def roofline(config, kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, ce
             r["traffic"] = traffic
         else:
             r["achieved"] = alg_pl / avg_s / scale if avg_s > 0 else 0.0
-            r["basis"] = ("survey model bytes per launch / average launch duration (no fresh "
+            r["basis"] = ("algorithmic bytes per launch / average launch duration (no fresh "
                           "measured traffic: " + ("stale profile" if pm is not None else "no profile") + ")")
             r["traffic"] = None
             if traffic is not None:
@@ -778,8 +807,11 @@ def main():
         # by sk_last_timing
         rf = None
         if not a.cpu_stub:
+            rt = None
+            if kind in ("ss", "stem"):  # the DAG schedule's row transfers per example (packed set)
+                rt = np.array([list(eng.ds.row_traffic(i).values()) for i in range(a.n)], dtype=np.float64)
             rf = roofline(a.config, kind, a.length, shapes, xs, ys, float(np.sum(k_ms)), float(np.sum(l_ms)),
-                          int(np.sum(launches)), cells, a.pmc_json)
+                          int(np.sum(launches)), cells, a.pmc_json, rt)
             rf["kernel"] = {"ss": "sk_dag_stem_kernel", "stem": "sk_dag_stem_kernel",
                             "stem4d": "sk_stem4d_kernel" if os.environ.get("SK4_NO_GSUM") else
                             "sk_stem4d_gsum_kernel" if os.environ.get("SK4_NO_PRE") else

@@ -155,6 +155,19 @@ const char *sk_dataset_label(const sk_dataset *ds, int i);
 int sk_dataset_shape(const sk_dataset *ds, int i, int32_t *n_nodes,
                      int32_t *n_edges, int32_t *n_bpfreq, int32_t *n_roots,
                      int32_t *seq_len);
+/* Row traffic of example i in the x role of the DAG stem kernel's gamma
+ * schedule (dag_stem.hip): its rows (the x nodes the schedule
+ * computes per pair), the rows it stores in the HBM slab, and the child-row
+ * reads of its rows from the slab, the y's Gamma and Phi tables and
+ * registers; y_slots = its non-leaf node count, the length of every row a
+ * pair (x', example i as y) moves.  Per pair (x, y) the engine moves each of
+ * x's row transfers as 8 * y_slots(y) bytes.  Replaces nothing in the
+ * reference (its DP keeps K0/G0 tables per pair in host memory,
+ * stem_kernel_lite/stem_kernel.cpp:14-95): a roofline input of bench.py.
+ * The dataset must be uploaded (packed). */
+int sk_dataset_row_traffic(const sk_dataset *ds, int i, int32_t *rows, int32_t *stored,
+                           int32_t *slab_reads, int32_t *gamma_reads, int32_t *phi_reads,
+                           int32_t *reg_reads, int32_t *y_slots);
 /* DAG arrays of example i (packer-parity introspection; any pointer may be
  * NULL).  Node arrays have n_nodes entries, edge arrays n_edges (node-major,
  * reference list order), bp arrays n_bpfreq. */

@@ -64,6 +64,7 @@ SIGNATURES = {
     "sk_dataset_add_copy": (C.c_int, [_P, _P, C.c_int32]),
     "sk_dataset_label": (C.c_char_p, [_P, C.c_int]),
     "sk_dataset_shape": (C.c_int, [_P, C.c_int, _I32P, _I32P, _I32P, _I32P, _I32P]),
+    "sk_dataset_row_traffic": (C.c_int, [_P, C.c_int, _I32P, _I32P, _I32P, _I32P, _I32P, _I32P, _I32P]),
     "sk_dataset_dag": (C.c_int, [_P, C.c_int, _U32P, _U32P, _U32P, _U32P, _F32P, _U32P,
                                  _U32P, _U32P, _U32P, _F32P, _U32P, _F32P]),
     "sk_dataset_profile": (C.c_int, [_P, C.c_int, _F32P, _F32P]),

@@ -3266,6 +3266,40 @@ int sk_dataset_shape(const sk_dataset* ds, int i, int32_t* n_nodes, int32_t* n_e
   return SK_OK;
 }
 
+int sk_dataset_row_traffic(const sk_dataset* ds, int i, int32_t* rows, int32_t* stored,
+                           int32_t* slab_reads, int32_t* gamma_reads, int32_t* phi_reads,
+                           int32_t* reg_reads, int32_t* y_slots) {
+  if (!ds) return SK_ERR_INVALID;
+  if (i < 0 || i >= (int)ds->ex.size()) return SK_ERR_RANGE;
+  const HostPack& P = ds->pack;
+  if ((int)P.ex_nlxg.size() != (int)ds->ex.size()) return SK_ERR_INVALID;  // not packed yet
+  // the kernel's row reads: slab / Gamma / Phi child records, minus the
+  // previous row's (taken from registers); stored rows (slot < 0x4000)
+  int32_t st = 0, sl = 0, ga = 0, ph = 0, rg = 0;
+  uint32_t prev = 0xffffu;
+  size_t k = (size_t)P.ex_xgch_base[i];
+  for (size_t r = (size_t)P.ex_xg_base[i]; r < (size_t)P.ex_xg_base[i] + P.ex_nlxg[i]; ++r) {
+    const int ne = P.xgrow[r].a & 0xff;
+    for (int t = 0; t < ne; ++t, ++k) {
+      const uint32_t c = P.xg_ch[k] & 0xffffu;
+      if (c == prev) ++rg;
+      else if (c & 0x8000u) ++ga;
+      else if (c & 0x4000u) ++ph;
+      else ++sl;
+    }
+    prev = P.xgrow[r].b >> 16;
+    st += prev < 0x4000u;
+  }
+  if (rows) *rows = P.ex_nlxg[i];
+  if (stored) *stored = st;
+  if (slab_reads) *slab_reads = sl;
+  if (gamma_reads) *gamma_reads = ga;
+  if (phi_reads) *phi_reads = ph;
+  if (reg_reads) *reg_reads = rg;
+  if (y_slots) *y_slots = P.ex_nl[i];
+  return SK_OK;
+}
+
 int sk_dataset_dag(const sk_dataset* ds, int i, uint32_t* first, uint32_t* last,
                    uint32_t* n_edges, uint32_t* n_bpfreq, float* weight, uint32_t* max_pa,
                    uint32_t* edge_to, uint32_t* edge_gaps, uint32_t* bp_code, float* bp_p,

@@ -395,6 +395,14 @@ class Dataset:
         check(lib().sk_dataset_shape(self._h, i, *[C.byref(a) for a in v]))
         return tuple(a.value for a in v)  # nodes, edges, bpfreq, roots, len
 
+    def row_traffic(self, i: int) -> dict:
+        """Row transfers of example i in the DAG stem kernel's gamma schedule
+        (sk_dataset_row_traffic; the dataset must be uploaded)."""
+        v = [C.c_int32() for _ in range(7)]
+        check(lib().sk_dataset_row_traffic(self._h, i, *[C.byref(a) for a in v]))
+        return dict(zip(("rows", "stored", "slab_reads", "gamma_reads", "phi_reads", "reg_reads",
+                         "y_slots"), (a.value for a in v)))
+
     def dag(self, i: int) -> dict:
         """The DAG of example i (reference numbering), for packer parity."""
         nn, ne, nb, nr, L = self.shape(i)

@@ -159,3 +159,18 @@ def test_libsvm_output(gpu_ctx, small_set):
     assert first[0] == "+1" and first[1] == "1" or first[1] == "0:1"
     assert first[1] == "0:1"
     assert float(first[2].split(":")[1]) == pytest.approx(km.matrix[0, 0], rel=1e-5)
+
+
+@pytest.mark.gpu
+def test_row_traffic_counts(gpu_ctx):
+    """sk_dataset_row_traffic (the DAG roofline's compulsory bytes, bench.py
+    dag_row_bytes): per example, stored rows <= rows, counts >= 0,
+    y_slots = the non-leaf node count."""
+    seqs = ska.random_sequences(6, 120, 0x5EED0707)
+    ds = ska.Dataset.synthetic(seqs)
+    gpu_ctx.upload(ds)
+    for i in range(len(seqs)):
+        t = ds.row_traffic(i)
+        assert 0 <= t["stored"] <= t["rows"]
+        assert min(t.values()) >= 0
+        assert t["y_slots"] == int(np.sum(ds.dag(i)["n_edges"] > 0))

@@ -30,6 +30,17 @@ __global__ void write8(double* __restrict__ a, size_t n) {
     a[i] = (double)i;
 }
 
+// scattered 8-B reads (the DAG kernel's node / edge record accesses): one
+// double per `stride`-element line of the buffer, the lines visited in a
+// permuted order (odd multiplier mod a power of two: every line once), so
+// each load is a separate request to a line no other load touches
+__global__ void read8_scatter(const double* __restrict__ a, size_t lines, size_t stride, double* out) {
+  double s = 0.0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x)
+    s += a[((i * 0x9E3779B1ull) & (lines - 1)) * stride];
+  if (s == 12345.678) out[0] = s;
+}
+
 int main() {
   const size_t bytes = (size_t)1 << 30;
   double* a = nullptr;
@@ -39,8 +50,13 @@ int main() {
   hipLaunchKernelGGL(write8, dim3(4096), dim3(256), 0, 0, a, n8);
   hipLaunchKernelGGL(read8, dim3(4096), dim3(256), 0, 0, a, n8, out);
   hipLaunchKernelGGL(read16, dim3(4096), dim3(256), 0, 0, reinterpret_cast<const double2*>(a), n8 / 2, out);
+  // one 8-B load per 128-B line and per 64-B line: 8 MiB / 16 MiB of loaded
+  // bytes touching every line of the 1 GiB once
+  hipLaunchKernelGGL(read8_scatter, dim3(4096), dim3(256), 0, 0, a, n8 / 16, (size_t)16, out);
+  hipLaunchKernelGGL(read8_scatter, dim3(4096), dim3(256), 0, 0, a, n8 / 8, (size_t)8, out);
   if (hipDeviceSynchronize() != hipSuccess) return 2;
-  std::printf("moved %zu bytes per launch (write8, read8, read16)\n", bytes);
+  std::printf("moved %zu bytes per launch (write8, read8, read16); read8_scatter: one 8-B load per 128-B "
+              "line (%zu loads), then per 64-B line (%zu loads)\n", bytes, n8 / 16, n8 / 8);
   (void)hipFree(a);
   (void)hipFree(out);
   return 0;
