@@ -201,14 +201,12 @@ COL_NB = {1: 4, 2: 4, 4: 2, 8: 1}
 def col_shape(lens, y):
     """(NB, W) of the 4-D column kernel, as run_stem4d picks them for a batch:
     NB columns per group by class, W = 8 waves at most (two per SIMD), at most
-    m - F - 1 (the smallest y of the batch; F = 8 steps between full
-    barriers, 1 for short y; one batch per bench step)."""
+    m - 2 PF - 2 = m - 10 (the smallest y of the batch: the round wrap's lag,
+    stem4d.hip kS4cV; one batch per bench step)."""
     m = lens[y]
     cpl = 1 if m.max() + 1 <= 64 else 2 if m.max() + 1 <= 128 else 4 if m.max() + 1 <= 256 else 8
-    f_env = max(1, int(os.environ.get("SK4C_F", "8")))
-    F = f_env if int(m.min()) - f_env - 1 >= 4 else 1
     w_env = int(os.environ.get("SK4C_W", "0"))
-    return COL_NB[cpl], int(max(1, min(w_env or 8, 8, int(m.min()) - F - 1)))
+    return COL_NB[cpl], int(max(1, min(w_env or 8, 8, int(m.min()) - 10)))
 
 
 def stem4d_cells(lens, x, y):

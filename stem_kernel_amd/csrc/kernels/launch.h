@@ -242,7 +242,9 @@ hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st);
 // full_dp, column groups (stem4d.hip sk_stem4d_col_kernel): one workgroup of
 // `waves` waves per pair (pairs[0..n_pairs)); per pair n planes of
 // plane_doubles (G0) and stem4d_col_nb(cpl) B' planes (the round wrap) at
-// scratch_off; |y| < 512, and m + 1 >= waves + col_f + 2
+// scratch_off; |y| < 512, and waves <= stem4d_col_w_max(m) for every pair
+// with m >= 2 (pairs with m <= 1 have K = 1 and take any waves)
+int stem4d_col_w_max(int m);
 int stem4d_col_nb(int cpl);
 size_t stem4d_col_lds_bytes(int cpl, int waves, int max_m);
 int stem4d_col_max_waves(int cpl);

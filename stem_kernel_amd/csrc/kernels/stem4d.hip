@@ -23,6 +23,8 @@
 // Per pair, a ring of three span buffers of n+1 planes each.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "device_set.h"
 #include "launch.h"
 
@@ -37,6 +39,11 @@ __device__ __forceinline__ double wave_shl1(double v, double high) {
 }
 
 __device__ __forceinline__ int pad4(int v) { return (v + 3) & ~3; }
+
+// read-only, wave-uniform global data through the constant address space
+// (scalar loads: no vector-memory wait behind the prefetched rows)
+template <typename T>
+using s4_cst = const __attribute__((address_space(4))) T*;
 
 __device__ __forceinline__ double bcast_lane0(double v) {
   const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
@@ -832,10 +839,19 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 // range-checked buffers end at the row) nor read by a valid cell of a later
 // row (a cell reads k and k+1 of earlier rows, both valid there), and add
 // nothing to K (their bp loads return 0, and bound >= 0).
+// Rows fetched ahead (PF, in registers) and the visibility lag of a global
+// store (V steps).  There are no full barriers: every step issues at least
+// one vector load after its stores and waits, PF steps later, for the load
+// issued PF steps before (vmcnt counts loads and stores together, in issue
+// order), so a store of step u is complete when its wave starts step u + PF
+// and seen by the other waves after the next barrier; V = PF + 2 keeps one
+// step of margin.  Hence groups of at least PF + V positions and
+// W <= m - 2 PF - 2 (run_stem4d), which tests/test_stem4d_col_schedule.py
+// emulates step by step (m - 2 PF - 1 is exact there).
 #ifndef SK4C_PF
-#define SK4C_PF 2  // rows fetched ahead (the step loop is unrolled over the two row buffers)
+#define SK4C_PF 4
 #endif
-static_assert(SK4C_PF == 2, "sk_stem4d_col_kernel keeps two row buffers");
+constexpr int kS4cV = SK4C_PF + 2;
 #ifndef SK4C_NB4  // column-group width of the CPL 4 class (|y| 128..255)
 #define SK4C_NB4 2
 #endif
@@ -858,7 +874,7 @@ __device__ __forceinline__ int s4c_group_len(int g, int n, int nb, int fp) {
 // position -> (column group, offset in the group); advance() moves on by W
 struct S4cPos {
   int g = 0, off = 0;
-  __device__ void advance(int W, int n, int nb, int fp) {
+  __device__ __forceinline__ void advance(int W, int n, int nb, int fp) {
     off += W;
     while (g * nb < n) {
       const int c = s4c_group_len(g, n, nb, fp);
@@ -866,14 +882,38 @@ struct S4cPos {
       off -= c;
       ++g;
     }
+    g = __builtin_amdgcn_readfirstlane(g);  // (uniform: keeps the cursors in SGPRs)
+    off = __builtin_amdgcn_readfirstlane(off);
   }
-  __device__ bool valid(int n, int nb) const { return g * nb < n; }
+  __device__ __forceinline__ bool valid(int n, int nb) const { return g * nb < n; }
 };
+
+// a range-checked buffer over one row of nk elements (loads past them return
+// 0, stores are dropped); slot c of the row at voffset (lane + 64 c) * size
+template <class T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s4c_rowbuf(const T* base, int nk) {
+  // (wave-uniform by construction; readfirstlane tells the compiler, which
+  // otherwise may build the descriptor in VGPRs and waterfall every access)
+  return s4c_rsrc(base, __builtin_amdgcn_readfirstlane(nk * (int)sizeof(T)));
+}
+__device__ __forceinline__ double s4c_rld64(__amdgpu_buffer_rsrc_t r, int c, int lane) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (lane + 64 * c) * 8, 0, 0));
+}
+__device__ __forceinline__ float s4c_rld32(__amdgpu_buffer_rsrc_t r, int c, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (lane + 64 * c) * 4, 0, 0));
+}
+__device__ __forceinline__ void s4c_rst64(__amdgpu_buffer_rsrc_t r, int c, int lane, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, v), r, (lane + 64 * c) * 8, 0, 0);
+}
 
 template <int CPL>
 __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kernel(Stem4dLaunch P) {
   constexpr int NB = s4c_nb<CPL>();
   constexpr int TW = 64 * CPL;
+  constexpr int NSEG = NB * CPL;         // a step's round-wrap rows: segments (chain, slot) of 64 doubles
+  constexpr int SEGR = (NSEG + 7) / 8;   // segments a wave stages through registers (W >= NSEG / SEGR)
+  constexpr int PF = SK4C_PF;
+  constexpr int FP = PF + kS4cV;  // positions per group at least
   extern __shared__ __attribute__((aligned(16))) double s4c_lds[];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -884,240 +924,415 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     if (threadIdx.x == 0) P.out[pr.out_index] = 1.0;
     return;
   }
-  const int64_t cp = pr.plane_doubles;
+  const int cp = (int)pr.plane_doubles;  // (< 2^17 doubles: |y| < 512)
   double* __restrict__ planes = P.scratch + pr.scratch_off;  // slot i: G0(i, latest column)
   double* __restrict__ wrapb = planes + (int64_t)n * cp;     // NB planes: B' across the round wrap
-  const float* bpx = P.bpdiag + pr.x_bp;
+  const s4_cst<float> bpx = (s4_cst<float>)(P.bpdiag + pr.x_bp);
   const float* bpy = P.bpdiag + pr.y_bp;
-  const uint8_t* xs = P.chars + pr.x_chr;
-  const double* gpow = P.gpow;
+  const s4_cst<double> gpow = (s4_cst<double>)P.gpow;
   const float bound = P.bp_bound;
-  const double g = P.gap, stk = P.stack, sub = P.subst;
-  const int F = max(P.col_f, 1);
-  const int FP = F + SK4C_PF;
   // LDS: links [W][2][NB][TW] (wave w writes link w, wave w+1 reads it a step
-  // later), W per-wave sums, y (zero padded: y[k + s - 1] for every slot)
+  // later), the round-wrap staging [2][NB][TW] (wave 0's link in), W per-wave
+  // sums, y (zero padded: y[k + s - 1] for every slot) and x.  The links and
+  // the staging start at 0, so every value any lane computes is finite.
   double* link_out = s4c_lds + (int64_t)w * 2 * NB * TW;
-  const double* link_in = s4c_lds + (int64_t)(w - 1) * 2 * NB * TW;
-  double* red = s4c_lds + (int64_t)W * 2 * NB * TW;
+  double* wst = s4c_lds + (int64_t)W * 2 * NB * TW;
+  const double* link_in = w == 0 ? wst : link_out - 2 * NB * TW;
+  double* red = wst + 2 * NB * TW;
   uint8_t* ysl = reinterpret_cast<uint8_t*>(red + W);
+  uint8_t* xsl = ysl + TW + R + 8;
+  for (int k = threadIdx.x; k < (W + 1) * 2 * NB * TW; k += blockDim.x) s4c_lds[k] = 0.0;
   for (int k = threadIdx.x; k < TW + R + 8; k += blockDim.x) ysl[k] = k < m ? P.chars[pr.y_chr + k] : 0;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) xsl[k] = P.chars[pr.x_chr + k];
   __syncthreads();
 
   // steps: T(last position) + R
-  int64_t np = 0;
+  int np = 0;
   for (int gg = 0; gg * NB < n; ++gg) np += s4c_group_len(gg, n, NB, FP);
-  const int64_t total = np > 0 ? ((np - 1) / W) * R + (np - 1) % W + R : 0;
+  const int total = np > 0 ? ((np - 1) / W) * R + (np - 1) % W + R : 0;  // (< 2^31 for |x|, |y| < 512)
 
-  // the position's planes (wave-uniform: SGPRs)
+  // Every position runs all NB chains: a group cut short by n runs virtual
+  // columns past n (no stacking sources; the last group's G0 store is never
+  // read), and in a group's top triangle (i >= j_lo - 1) the chains before
+  // the plane (i, i+1) -- the boundary chain c0 = i + 1 - j_lo, whose A row is
+  // G0(i, i) = g^(l-k) and G1 0 -- compute values that are discarded (their
+  // A is replaced at c0, their consumers have no sources, their B' rows reach
+  // no real chain: the next position reads them only at its boundary chain,
+  // which reads none).
   struct Plane {
-    int i, c0, nbg, j_lo;
-    bool on, bnd, cons;
-    uint32_t stack;  // bit c: chain c's consumer (i-1, j_lo+c) is a stacking pair
-    uint32_t xci;
-    uint32_t xcj[NB];
-    double cm[NB], cs[NB];  // stack bp(i-1, j-1): match / mismatch factors (:320-331)
+    int i, c0;          // plane row, the boundary chain (c0 < 0: none)
+    bool on;            // a plane (not a bubble)
+    uint32_t stack;     // bit c: chain c's consumer (i-1, j_lo+c) is a stacking pair
+    uint32_t xci, xcj;  // x[i-1], x[j_lo+c-1] in byte c
+    float bpc[NB];      // bp(i-1, j_lo+c-1) of the stacking consumers
   };
   auto describe = [&](const S4cPos& q) __attribute__((always_inline)) -> Plane {
     Plane d;
-    d.on = d.bnd = d.cons = false;
-    d.i = d.c0 = d.nbg = 0;
-    d.j_lo = 1;
-    d.stack = 0u;
-    d.xci = 0u;
+    d.on = false;
+    d.i = 0;
+    d.c0 = -1;
+    d.stack = d.xci = d.xcj = 0u;
 #pragma unroll
-    for (int c = 0; c < NB; ++c) {
-      d.xcj[c] = 0u;
-      d.cm[c] = d.cs[c] = 0.0;
-    }
+    for (int c = 0; c < NB; ++c) d.bpc[c] = 0.0f;
     if (!q.valid(n, NB)) return d;
-    d.j_lo = q.g * NB + 1;
-    const int j_hi = min(q.g * NB + NB, n);
-    d.nbg = j_hi - d.j_lo + 1;
+    const int j_lo = q.g * NB + 1, j_hi = min(q.g * NB + NB, n);
     if (q.off >= j_hi) return d;  // a bubble
     d.on = true;
-    d.i = j_hi - 1 - q.off;
-    d.c0 = max(0, d.i + 1 - d.j_lo);
-    d.bnd = d.i + 1 >= d.j_lo;  // the first chain is the plane (i, i+1): A = g^(l-k), G1 = 0
-    d.cons = d.i >= 1;
-    if (d.cons) {
-      d.xci = __builtin_amdgcn_readfirstlane(xs[d.i - 1]);
+    const int i = j_hi - 1 - q.off;
+    d.i = i;
+    d.c0 = i + 1 >= j_lo ? i + 1 - j_lo : -1;
+    if (i >= 1) {
+      d.xci = __builtin_amdgcn_readfirstlane(xsl[i - 1]);
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
-        if (c < d.c0 || c >= d.nbg) continue;
-        const int jp = d.j_lo + c, e = jp - d.i;  // bp(i-1, jp-1): diagonal e
-        const float bc = __uint_as_float(__builtin_amdgcn_readfirstlane(
-            __float_as_uint(bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (d.i - 1)])));
-        d.xcj[c] = __builtin_amdgcn_readfirstlane(xs[jp - 1]);
+        const int jp = j_lo + c, e = jp - i;  // bp(i-1, jp-1): diagonal e
+        if (c < (d.c0 < 0 ? 0 : d.c0) || jp > n) continue;
+        const float bc = bpx[(int64_t)e * n - (int64_t)e * (e - 1) / 2 + (i - 1)];
+        d.xcj |= (uint32_t)__builtin_amdgcn_readfirstlane(xsl[jp - 1]) << (8 * c);
         if (bc > bound) {
           d.stack |= 1u << c;
-          d.cm[c] = stk * (double)bc;
-          d.cs[c] = stk * sub * (double)bc;
+          d.bpc[c] = bc;
         }
       }
     }
+    // (the compiler's divergence analysis loses these through the LDS / the
+    // loops: without readfirstlane the per-chain branches become exec-mask
+    // branches with both sides executed)
+    d.i = __builtin_amdgcn_readfirstlane(d.i);
+    d.c0 = __builtin_amdgcn_readfirstlane(d.c0);
+    d.stack = __builtin_amdgcn_readfirstlane(d.stack);
+    d.xci = __builtin_amdgcn_readfirstlane(d.xci);
+    d.xcj = __builtin_amdgcn_readfirstlane(d.xcj);
     return d;
   };
+  auto pos_of = [&](const S4cPos& q, bool& on) __attribute__((always_inline)) -> int {
+    on = false;
+    if (!q.valid(n, NB)) return 0;
+    const int j_hi = min(q.g * NB + NB, n);
+    on = q.off < j_hi;
+    return j_hi - 1 - q.off;
+  };
+  // a cursor over this wave's (or wave 0's) rows: position, row, the row's
+  // offset in a plane and in prob_y
+  struct Cur {
+    S4cPos q;
+    bool on;
+    int i, s, ro, ye;
+  };
+  auto cur_init = [&](Cur& c, int p) __attribute__((always_inline)) {
+    c.q = S4cPos();
+    c.q.advance(p, n, NB, FP);
+    c.i = pos_of(c.q, c.on);
+    c.s = c.ro = c.ye = 0;
+  };
+  auto cur_next = [&](Cur& c) __attribute__((always_inline)) {
+    c.ro = __builtin_amdgcn_readfirstlane(c.ro + pad4(m + 1 - c.s));
+    c.ye = __builtin_amdgcn_readfirstlane(c.ye + (c.s >= 1 ? m + 1 - c.s : 0));  // prob_y row s at ((s-1) m - (s-1)(s-2)/2)
+    c.s = __builtin_amdgcn_readfirstlane(c.s + 1);
+    if (c.s == R) {
+      c.s = c.ro = c.ye = 0;
+      c.q.advance(W, n, NB, FP);
+      c.i = __builtin_amdgcn_readfirstlane(pos_of(c.q, c.on));
+    }
+  };
+
   // one row's HBM inputs, fetched PF rows ahead: G0(i, j_lo - 1) (chain 0's
-  // A row), prob_y(k, l-1), and on wave 0 the chains' round-wrap B' rows
+  // A row) and prob_y(k, l-1)
   struct Row {
     double A[CPL];
-    double Bw[NB][CPL];
     float bp[CPL];
   };
-  auto fetch = [&](Row& r, const Plane& d, int s) __attribute__((always_inline)) {
-    const int nk = d.on && s >= 1 ? m - s + 1 : 0;  // valid cells of the row
-    if (nk == 0) return;
-    const int ro = row_off(m, s);
-    const int e2 = s - 1;
-    const int64_t ye = (int64_t)e2 * m - (int64_t)e2 * (e2 - 1) / 2;
+  Row rq[PF];  // oldest first: the row of step t is fetched at step t - PF
+#pragma unroll
+  for (int q = 0; q < PF; ++q)
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      if (64 * c >= nk) break;
-      if (!d.bnd) r.A[c] = s4c_ld64(planes + (int64_t)d.i * cp + ro, nk, c, lane);
-      r.bp[c] = s4c_ld32(bpy + ye, nk, c, lane);
-      if (w == 0) {
-#pragma unroll
-        for (int ch = 0; ch < NB; ++ch)
-          if (ch >= d.c0 && ch < d.nbg && !(ch == d.c0 && d.bnd))
-            r.Bw[ch][c] = s4c_ld64(wrapb + (int64_t)ch * cp + ro, nk, c, lane);
-      }
+      rq[q].A[c] = 0.0;
+      rq[q].bp[c] = 0.0f;
     }
-  };
-
-  double ksrc = 0.0;
-  double Am1[NB][CPL], Am2[NB][CPL], G2c[NB][CPL], G3c[NB][CPL];
-  bool xk[CPL];  // y[k] == x[i-1] (the consumer's left base), per position
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    xk[c] = false;
-#pragma unroll
-    for (int ch = 0; ch < NB; ++ch) Am1[ch][c] = Am2[ch][c] = G2c[ch][c] = G3c[ch][c] = 0.0;
-  }
-
-  S4cPos cur;
-  cur.advance(w, n, NB, FP);  // from position 0
-  Plane dc = describe(cur);
-  S4cPos fpos = cur;
-  Plane df = dc;
-  int fs = 0;  // fetch cursor: (fpos, fs)
-  int s = 0, ro = 0;
-  // the row of step t is fetched at step t - PF into the buffer of t's parity
-  // (an even step consumes E, an odd one O; steps -2, -1 before the loop)
-  Row E, O;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    E.A[c] = O.A[c] = 0.0;
-    E.bp[c] = O.bp[c] = 0.0f;
-#pragma unroll
-    for (int ch = 0; ch < NB; ++ch) E.Bw[ch][c] = O.Bw[ch][c] = 0.0;
-  }
+  Cur fc;  // fetch cursor, from the wave's first step on (fdelay: the steps before)
+  cur_init(fc, w);
+  int fdelay = w;
   auto fetch_next = [&](Row& r) __attribute__((always_inline)) {
-    fetch(r, df, fs);
-    if (++fs == R) {
-      fs = 0;
-      fpos.advance(W, n, NB, FP);
-      df = describe(fpos);
-    }
-  };
-  if (w <= 0) fetch_next(E);  // step -2's fetch: the row of step 0
-  if (w <= 1) fetch_next(O);  // step -1's: the row of step 1
-
-  auto step = [&](int64_t t, Row& X) __attribute__((always_inline)) {
-    if (t > 0) {  // (every wave takes every barrier)
-      if (t % F == 0) {
-        __syncthreads();
-      } else {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      }
-    }
-    if (!cur.valid(n, NB)) return;
-    if (t < w) {
-      if (t >= w - SK4C_PF) fetch_next(X);
+    if (fdelay > 0) {
+      --fdelay;
       return;
     }
-    if (dc.on) {
-      if (s == 0) {  // cells (l, l): G0 = g^(j-i), never stored; the chains' registers reset
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) xk[c] = ysl[lane + 64 * c] == dc.xci;
-#pragma unroll
-        for (int ch = 0; ch < NB; ++ch) {
-          if (!((dc.stack >> ch) & 1u)) continue;
-          const double a0 = gpow[dc.j_lo + ch - 1 - dc.i];  // G0(i, j-1, l, l)
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            Am1[ch][c] = a0;
-            Am2[ch][c] = G2c[ch][c] = G3c[ch][c] = 0.0;
-          }
-        }
-      } else {
-        const int kmax = m - s;
-        const double* lin = link_in + ((t - 1) & 1) * NB * TW;
-        double* lout = link_out + (t & 1) * NB * TW;
-        const bool to_link = w + 1 < W;
-        double* const gout = planes + (int64_t)dc.i * cp + ro;
-        const double gs = gpow[s];
+    if (fc.q.valid(n, NB)) {
+      if (fc.on && fc.s >= 1) {
+        const int nk = m - fc.s + 1;  // valid cells of the row
+        const auto ra = s4c_rowbuf(planes + (int64_t)fc.i * cp + fc.ro, nk);
+        const auto rb = s4c_rowbuf(bpy + fc.ye, nk);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-          if (64 * c > kmax) break;
-          const int k = lane + 64 * c;
-          const float bpf = X.bp[c];
-          const bool sok = bpf > bound;
-          const double bpd = sok ? (double)bpf : 0.0;
-          const uint32_t yl = ysl[k + s - 1];
-          double A = dc.bnd ? gs : X.A[c];
+          r.A[c] = s4c_rld64(ra, c, lane);
+          r.bp[c] = s4c_rld32(rb, c, lane);
+        }
+      }
+      cur_next(fc);
+    }
+  };
+
+  // The round wrap: wave 0's positions are 0, W, 2W, ..., so at step u it
+  // runs row u mod R of position (u div R) W, whose chains read their B'
+  // rows from the wrap planes.  Every wave stages a share of them: the
+  // segments (chain, slot) w, w + W, ... of wave 0's rows of step u are
+  // loaded at step u - PF - 1, written to wst[(u - 1) & 1] at step u-1 (the
+  // slot a link of step u-1 takes) and read by wave 0 at step u after the
+  // barrier.  zc: the rows of the last staging load, yc: of the next store.
+  Cur zc, yc;
+  cur_init(zc, 0);
+  cur_init(yc, 0);
+  cur_next(yc);  // wave 0's rows of step 1 are the first the stores write
+  double wrq[PF][SEGR];  // staged segments in flight, oldest first
 #pragma unroll
-          for (int ch = 0; ch < NB; ++ch) {
-            if (ch < dc.c0 || ch >= dc.nbg) continue;
-            double G1 = 0.0;
-            if (!(ch == dc.c0 && dc.bnd)) G1 = w == 0 ? X.Bw[ch][c] : lin[ch * TW + k];
-            double G0 = A * g;
-            G0 += G1;
-            if (dc.cons) {
-              double Bn = G1 * g;
-              if ((dc.stack >> ch) & 1u) {
-                // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
-                // (k+1, l-1) (row s-2): the next lane's, or the next slot's
-                // lane 0 (slot c+1 not yet updated this row)
-                const double hg = c + 1 < CPL ? bcast_lane0(G3c[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
-                const double ha = c + 1 < CPL ? bcast_lane0(Am2[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
-                const double G3n = wave_shl1(G3c[ch][c], hg);
-                const double A2 = wave_shl1(Am2[ch][c], ha);
-                const bool mt = sok && xk[c] && yl == dc.xcj[ch];
-                ksrc += A2 * bpd * (mt ? dc.cm[ch] : dc.cs[ch]);
-                double g3 = G3n * g;
-                g3 += mt ? A2 : 0.0;
-                double g2 = G2c[ch][c] * g;
-                g2 += g3;
-                Bn += g2;
-                G2c[ch][c] = g2;
-                G3c[ch][c] = g3;
-                Am2[ch][c] = Am1[ch][c];
-                Am1[ch][c] = A;
-              }
-              if (to_link) lout[ch * TW + k] = Bn;
-              else s4c_st64(wrapb + (int64_t)ch * cp + ro, kmax + 1, c, lane, Bn);
-            }
-            A = G0;
-          }
-          s4c_st64(gout, kmax + 1, c, lane, A);  // the last chain's G0 (i, j_hi)
+  for (int q = 0; q < PF; ++q)
+#pragma unroll
+    for (int e = 0; e < SEGR; ++e) wrq[q][e] = 0.0;
+  auto zload = [&](double (&wr)[SEGR]) __attribute__((always_inline)) {
+    if (!zc.on || zc.s == 0) return;
+    const int nk = m - zc.s + 1;
+#pragma unroll
+    for (int q = 0; q < SEGR; ++q) {
+      const int sg = w + q * W, ch = sg / CPL, c = sg % CPL;
+      if (sg < NSEG) wr[q] = s4c_rld64(s4c_rowbuf(wrapb + (int64_t)ch * cp + zc.ro, nk), c, lane);
+    }
+  };
+  auto zstore = [&](double* dst, const double (&wr)[SEGR]) __attribute__((always_inline)) {
+    if (!yc.on || yc.s == 0) return;
+#pragma unroll
+    for (int q = 0; q < SEGR; ++q) {
+      const int sg = w + q * W, ch = sg / CPL, c = sg % CPL;
+      if (sg < NSEG) dst[ch * TW + 64 * c + lane] = wr[q];
+    }
+    if (SEGR * W < NSEG) {  // few waves (short y): the rest loaded here
+      const int nk = m - yc.s + 1;
+      for (int sg = w + SEGR * W; sg < NSEG; sg += W) {
+        const int ch = sg / CPL, c = sg % CPL;
+        dst[ch * TW + 64 * c + lane] = s4c_rld64(s4c_rowbuf(wrapb + (int64_t)ch * cp + yc.ro, nk), c, lane);
+      }
+    }
+  };
+  // the fence loads: one 4-byte load per step into fq, consumed PF steps
+  // later, so every step's stores complete by then (see kS4cV)
+  float fq[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) fq[q] = 0.0f;
+  const auto fence_buf = s4c_rowbuf(bpy, 1);
+
+  // steps -PF .. -1: this wave's first rows (of steps 0 .. PF-1; before its
+  // first step, t = w, nothing) and the staging loads of wave 0's rows of
+  // steps 1 .. PF
+#pragma unroll
+  for (int q = 0; q < PF; ++q) fetch_next(rq[q]);
+#pragma unroll
+  for (int q = 0; q < PF; ++q) {
+    cur_next(zc);
+    zload(wrq[q]);
+  }
+
+  // every step: the barrier, this wave's row of the step (rq[0]) ...
+  auto head = [&](int t, Row& X) __attribute__((always_inline)) {
+    if (t > 0) {  // (every wave takes every barrier) LDS-only: the global stores by vmcnt (kS4cV)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      asm volatile("" ::: "memory");
+    }
+    {  // the fence load of step t - PF: this wave's stores up to then are complete
+      const float f0 = fq[0];
+#pragma unroll
+      for (int q = 0; q + 1 < PF; ++q) fq[q] = fq[q + 1];
+      asm volatile("" ::"v"(f0));
+    }
+    X = rq[0];
+#pragma unroll
+    for (int q = 0; q + 1 < PF; ++q) rq[q] = rq[q + 1];
+  };
+  // ... and after the step's compute: the row of step t + PF, wave 0's wrap
+  // rows (step t+1's into LDS, step t+PF+1's loaded), the fence load
+  auto tail = [&](int t) __attribute__((always_inline)) {
+    fetch_next(rq[PF - 1]);
+    if (yc.q.valid(n, NB)) {
+      zstore(wst + (t & 1) * NB * TW, wrq[0]);
+      cur_next(yc);
+#pragma unroll
+      for (int q = 0; q + 1 < PF; ++q)
+#pragma unroll
+        for (int e = 0; e < SEGR; ++e) wrq[q][e] = wrq[q + 1][e];
+      cur_next(zc);
+      zload(wrq[PF - 1]);
+    }
+    fq[PF - 1] = s4c_rld32(fence_buf, 0, lane);  // (lane 0 reads bpy[0], the rest nothing)
+  };
+
+  double ksrc = 0.0, kacc[NB];
+  double Am1[NB][CPL], Am2[NB][CPL], G2c[NB][CPL], G3c[NB][CPL];
+#pragma unroll
+  for (int ch = 0; ch < NB; ++ch) {
+    kacc[ch] = 0.0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) Am1[ch][c] = Am2[ch][c] = G2c[ch][c] = G3c[ch][c] = 0.0;
+  }
+  // loop-invariant kernel constants in VGPRs (SGPRs are the scarce ones here)
+  double gv = P.gap, subv = P.subst;
+  asm volatile("" : "+v"(gv), "+v"(subv));
+  uint32_t xk = 0u;  // bit c: y[k] == x[i-1] (the consumer's left base), per position
+  Plane dc;
+  Row X;
+
+  // row s >= 1 of the position: NS slots hold its cells (64 (NS-1) <= m - s
+  // < 64 NS), chain by chain (one uniform branch per chain on its consumer's
+  // stacking); BND: a boundary chain c0 (a top-triangle position)
+  auto row = [&](int t, int s, int ro, auto bnd_tag, auto ns_tag) __attribute__((always_inline)) {
+    constexpr bool BND = decltype(bnd_tag)::value;
+    constexpr int NS = decltype(ns_tag)::value;
+    const int nk = m - s + 1;
+    const double* lin = link_in + ((t - 1) & 1) * NB * TW;
+    double* lout = link_out + (t & 1) * NB * TW;
+    const bool to_link = w + 1 < W;
+    const double gs = gpow[s];
+    double A[NS], bpd[NS];
+    uint32_t yl[NS];
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+      A[c] = X.A[c];
+      bpd[c] = X.bp[c] > bound ? (double)X.bp[c] : 0.0;
+      yl[c] = ysl[lane + 64 * c + s - 1];
+    }
+    const uint32_t stk_mask = __builtin_amdgcn_readfirstlane(dc.stack);
+    const int bch = BND ? __builtin_amdgcn_readfirstlane(dc.c0) : -1;
+#pragma unroll
+    for (int ch = 0; ch < NB; ++ch) {
+      const bool bz = BND && ch == bch;  // G0(i, i) row and no G1
+      const auto rw = s4c_rowbuf(wrapb + (int64_t)ch * cp + ro, nk);
+      if ((stk_mask >> ch) & 1u) {
+        const uint32_t xcj = (dc.xcj >> (8 * ch)) & 0xffu;
+#pragma unroll
+        for (int c = 0; c < NS; ++c) {
+          const int k = lane + 64 * c;
+          double G1 = 0.0;
+          if (bz) A[c] = gs;
+          else G1 = lin[ch * TW + k];
+          double G0 = A[c] * gv;
+          G0 += G1;
+          // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
+          // (k+1, l-1) (row s-2): the next lane's, or the next slot's lane 0
+          // (slot c+1 not yet updated this row; past the row's slots, lanes
+          // of no valid cell)
+          const double hg = c + 1 < CPL ? bcast_lane0(G3c[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
+          const double ha = c + 1 < CPL ? bcast_lane0(Am2[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
+          const double G3n = wave_shl1(G3c[ch][c], hg);
+          const double A2 = wave_shl1(Am2[ch][c], ha);
+          const bool mt = ((xk >> c) & 1u) && yl[c] == xcj && bpd[c] != 0.0;
+          // the source (:320-331) without its stack * bp(i-1, j-1) factor,
+          // which the position's sum takes at its end
+          kacc[ch] += A2 * bpd[c] * (mt ? 1.0 : subv);
+          double g3 = G3n * gv;
+          g3 += mt ? A2 : 0.0;
+          double g2 = G2c[ch][c] * gv;
+          g2 += g3;
+          double Bn = G1 * gv;
+          Bn += g2;
+          G2c[ch][c] = g2;
+          G3c[ch][c] = g3;
+          Am2[ch][c] = Am1[ch][c];
+          Am1[ch][c] = A[c];
+          if (to_link) lout[ch * TW + k] = Bn;
+          else s4c_rst64(rw, c, lane, Bn);
+          A[c] = G0;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < NS; ++c) {
+          const int k = lane + 64 * c;
+          double G1 = 0.0;
+          if (bz) A[c] = gs;
+          else G1 = lin[ch * TW + k];
+          double G0 = A[c] * gv;
+          G0 += G1;
+          const double Bn = G1 * gv;
+          if (to_link) lout[ch * TW + k] = Bn;
+          else s4c_rst64(rw, c, lane, Bn);
+          A[c] = G0;
         }
       }
     }
-    fetch_next(X);  // the row of step t + PF
-    ro += pad4(m + 1 - s);
-    if (++s == R) {
-      s = 0;
-      ro = 0;
-      cur.advance(W, n, NB, FP);
-      dc = describe(cur);
-    }
+    const auto rg = s4c_rowbuf(planes + (int64_t)dc.i * cp + ro, nk);
+#pragma unroll
+    for (int c = 0; c < NS; ++c) s4c_rst64(rg, c, lane, A[c]);  // the last chain's G0 (i, j_hi)
   };
-  for (int64_t t = 0; t < total; t += 2) {
-    step(t, E);
-    if (t + 1 < total) step(t + 1, O);
+
+  int t = 0;
+  for (; t < w && t < total; ++t) {  // before the wave's first position
+    head(t, X);
+    tail(t);
+  }
+  // a position's rows 1 .. m in phases of NS active slots, CPL down to 1
+  auto rows = [&](auto bnd_tag) __attribute__((always_inline)) {
+    int s = 1, ro = pad4(m + 1);
+    auto phase = [&](auto ns_tag) __attribute__((always_inline)) {
+      constexpr int NS = decltype(ns_tag)::value;
+      const int s_end = NS > 1 ? m - 64 * (NS - 1) : m;
+      for (; s <= s_end; ++s, ++t) {
+        head(t, X);
+        row(t, s, ro, bnd_tag, ns_tag);
+        tail(t);
+        ro += pad4(m + 1 - s);
+      }
+    };
+    if constexpr (CPL >= 8) {
+      phase(std::integral_constant<int, 8>());
+      phase(std::integral_constant<int, 7>());
+      phase(std::integral_constant<int, 6>());
+      phase(std::integral_constant<int, 5>());
+    }
+    if constexpr (CPL >= 4) {
+      phase(std::integral_constant<int, 4>());
+      phase(std::integral_constant<int, 3>());
+    }
+    if constexpr (CPL >= 2) phase(std::integral_constant<int, 2>());
+    phase(std::integral_constant<int, 1>());
+  };
+  S4cPos cur;
+  cur.advance(w, n, NB, FP);  // from position 0
+  while (cur.valid(n, NB)) {
+    dc = describe(cur);
+    if (!dc.on) {  // a bubble
+      for (int s = 0; s < R; ++s, ++t) {
+        head(t, X);
+        tail(t);
+      }
+    } else {
+      head(t, X);  // row 0, cells (l, l): G0 = g^(j-i), never stored; the chains' registers reset
+      xk = 0u;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) xk |= (ysl[lane + 64 * c] == dc.xci ? 1u : 0u) << c;
+#pragma unroll
+      for (int ch = 0; ch < NB; ++ch) {
+        const double a0 = (dc.stack >> ch) & 1u ? gpow[cur.g * NB + ch - dc.i] : 0.0;  // G0(i, j-1, l, l)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          Am1[ch][c] = a0;
+          Am2[ch][c] = G2c[ch][c] = G3c[ch][c] = 0.0;
+        }
+      }
+      tail(t);
+      ++t;
+      if (dc.c0 >= 0) rows(std::true_type());
+      else rows(std::false_type());
+#pragma unroll
+      for (int ch = 0; ch < NB; ++ch) {  // the position's sources: times stack * bp(i-1, j-1)
+        ksrc += kacc[ch] * (P.stack * (double)dc.bpc[ch]);
+        kacc[ch] = 0.0;
+      }
+    }
+    cur.advance(W, n, NB, FP);
+  }
+  for (; t < total; ++t) {  // after the wave's last position
+    head(t, X);
+    tail(t);
   }
   for (int off = 32; off > 0; off >>= 1) ksrc += __shfl_xor(ksrc, off, 64);
   if (lane == 0) red[w] = ksrc;
@@ -1128,6 +1343,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     P.out[pr.out_index] = 1.0 + K;
   }
 }
+
+int stem4d_col_w_max(int m) { return m - 2 * SK4C_PF - 2; }
 
 int stem4d_col_max_waves(int cpl) {
   return cpl <= 1 ? s4c_max_waves<1>() : cpl == 2 ? s4c_max_waves<2>() : cpl == 4 ? s4c_max_waves<4>()
@@ -1140,7 +1357,8 @@ int stem4d_col_nb(int cpl) {
 
 size_t stem4d_col_lds_bytes(int cpl, int waves, int m) {
   const int nb = stem4d_col_nb(cpl);
-  return ((size_t)waves * 2 * nb * 64 * cpl + waves) * sizeof(double) + (size_t)(64 * cpl + m + 1 + 8 + 15) / 16 * 16;
+  return ((size_t)(waves + 1) * 2 * nb * 64 * cpl + waves) * sizeof(double) +
+         (size_t)(64 * cpl + m + 1 + 8 + 512 + 15) / 16 * 16;  // y, x (|x| < 512)
 }
 
 hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves, int max_m,

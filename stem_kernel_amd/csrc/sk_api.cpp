@@ -1877,9 +1877,6 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   const double budget = std::min(128e9, 0.5 * (double)free_b);
   std::vector<int64_t> order(n);
   std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-    return xs_->ex[x[a]].len > xs_->ex[x[b]].len;
-  });
   // g^k for y spans (d1 = 0 planes) and, in the column kernel, x spans (the
   // diagonal cells G0(i, j, l, l) = g^(j-i))
   const std::vector<double> gp = gap_powers(kp->gap, std::max(max_m, max_n) + 2);
@@ -1911,8 +1908,20 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // B' handed on through LDS, NB columns chained per position;
   // stem4d.hip sk_stem4d_col_kernel); SK4_SPAN=1 (per call, A/B) runs the
   // pre-combined span kernel instead, SK4_NO_PRE=1 the K-sum span kernel
-  const bool colk = gsum && !ktiles && !std::getenv("SK4_SPAN") && !std::getenv("SK4_NO_PRE");
-  const int col_nb = colk ? sk::stem4d_col_nb(cpl) : 0;
+  // (pairs whose y is too short for the column schedule, 2 <= m < 2 PF + 3,
+  // go to the span kernel in batches of their own)
+  const bool colk_call = gsum && !ktiles && !std::getenv("SK4_SPAN") && !std::getenv("SK4_NO_PRE");
+  const int col_nb = colk_call ? sk::stem4d_col_nb(cpl) : 0;
+  auto col_ok = [&](int64_t q) {
+    const int m = ys_->ex[y[q]].len;
+    return colk_call && (m <= 1 || sk::stem4d_col_w_max(m) >= 1);
+  };
+  // batches of one kernel: the column kernel's pairs first, then longest x first
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+    const bool ca = col_ok(a), cb = col_ok(b);
+    if (ca != cb) return ca;
+    return xs_->ex[x[a]].len > xs_->ex[x[b]].len;
+  });
   double total_ms = 0.0;
   int launches = 0;
   Stem4dBatch& Bt = ctx->s4d;
@@ -1923,7 +1932,8 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     size_t ring_bytes = 0;  // rings only: pair p's at scratch_off, boundary columns after all
     int64_t b1 = b0;
     int maxn = 0;
-    while (b1 < n && prs.size() < 4096) {
+    const bool colk = col_ok(order[b0]);
+    while (b1 < n && prs.size() < 4096 && col_ok(order[b1]) == colk) {
       const int64_t q = order[b1];
       sk::Stem4dPair p;
       p.n = xs_->ex[x[q]].len;
@@ -1949,19 +1959,17 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       ++b1;
     }
     if (colk) {
-      // one launch for the batch: W waves per pair, W <= m - F - 1 for every
-      // pair (the round wrap's lag, stem4d.hip), the class's register budget
-      // and 160 KB of LDS; full barriers every F = 8 steps where the y's are
-      // long enough, else every step (SK4C_F / SK4C_W: other values, A/B)
-      // (|y| <= 1: no stacking source, K = 1 without a step)
+      // one launch for the batch: W waves per pair, W <= m - 2 PF - 2 for
+      // every pair (the round wrap's lag, stem4d.hip kS4cV; |y| <= 1: no
+      // stacking source, K = 1 without a step), the class's register budget
+      // and 160 KB of LDS (SK4C_W: fewer, A/B)
       int min_m = INT32_MAX;
       for (const auto& p : prs)
         if (p.m >= 2) min_m = std::min(min_m, p.m);
-      static const int f_env = std::getenv("SK4C_F") ? std::max(1, std::atoi(std::getenv("SK4C_F"))) : 8;
       static const int w_env = std::getenv("SK4C_W") ? std::max(1, std::atoi(std::getenv("SK4C_W"))) : 0;
-      const int F = min_m - f_env - 1 >= 4 ? f_env : 1;
-      int W = std::max(1, std::min(w_env ? w_env : sk::stem4d_col_max_waves(cpl), min_m - F - 1));
-      W = std::min(W, sk::stem4d_col_max_waves(cpl));
+      int W = std::min(w_env ? w_env : sk::stem4d_col_max_waves(cpl), sk::stem4d_col_max_waves(cpl));
+      if (min_m != INT32_MAX) W = std::min(W, sk::stem4d_col_w_max(min_m));
+      W = std::max(W, 1);
       while (W > 1 && sk::stem4d_col_lds_bytes(cpl, W, max_m) > 160 * 1024) --W;
       rc = ensure_scratch(ctx, ring_bytes + 64);
       if (rc) return rc;
@@ -1987,7 +1995,6 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       L.bp_bound = (float)kp->bp_bound;
       L.out = out_dev;
       L.gsum = 3;
-      L.col_f = F;
       SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
       SK_HIP(ctx, sk::lev_mark(ctx, S));
       SK_HIP(ctx, sk::launch_stem4d_col(L, (int64_t)prs.size(), cpl, W, max_m, S));

@@ -66,9 +66,15 @@ def bpdiag(seq, bpp):
     return np.array(out, np.float32)
 
 
-def emulate(x, bx, y, by, W, F=1, nb=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None, pf=PF):
+def emulate(x, bx, y, by, W, F=1, nb=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0, CPL=None, pf=PF,
+            vis=None, zlead=None):
     """F: steps between full barriers -- a global store of step u is seen
-    from the first multiple of F above u on; LDS stores from the next step."""
+    from the first multiple of F above u on; or, with vis, from step u + vis
+    on (no full barriers: a wave's store is complete once it has waited for a
+    load issued after it, PF steps later, and seen after the next barrier);
+    LDS stores from the next step.  zlead: wave 0's round-wrap rows are
+    loaded zlead steps before the step that uses them (by the staging waves),
+    else with its own rows, PF steps ahead."""
     n, m = len(x), len(y)
     R = m + 1
     TW = 64 * (CPL or max(1, -(-(m + 1) // 64)))
@@ -129,7 +135,7 @@ def emulate(x, bx, y, by, W, F=1, nb=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0
         v.Am1, v.Am2, v.G2c, v.G3c = ([np.zeros(TW) for _ in range(nb)] for _ in range(4))
         waves.append(v)
 
-    def fetch(v, snap, w):
+    def fetch(v, snap, w, zsnap=None):
         d, s = v.df, v.fs
         kmax = m - s
         ro = row_off(m, s)
@@ -142,9 +148,10 @@ def emulate(x, bx, y, by, W, F=1, nb=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0
             if not d["bnd"]:
                 r["A"][msk] = snap["planes"][d["i"] * cp + ro + kk]
             if w == 0:
+                src = zsnap if zsnap is not None else snap
                 for c in range(d["c0"], d["nbg"]):
                     if c > d["c0"] or not d["bnd"]:
-                        r["Bw"][c][msk] = snap["planes"][wrap0 + c * cp + ro + kk]
+                        r["Bw"][c][msk] = src["planes"][wrap0 + c * cp + ro + kk]
             e2 = s - 1
             ye = e2 * m - e2 * (e2 - 1) // 2
             r["bp"][msk] = bpy[ye + kk]
@@ -162,29 +169,33 @@ def emulate(x, bx, y, by, W, F=1, nb=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0
         return out
 
     snap = {kk: vv.copy() for kk, vv in mem.items()}
+    hist = {}  # step -> global snapshot (the staging loads of wave 0's wrap rows)
     for v_i, v in enumerate(waves):  # first rows: PF steps before the wave's first step
-        v.rows = [fetch(v, snap, v_i) for _ in range(max(0, pf - v_i))]
+        v.rows = [fetch(v, snap, v_i, snap) for _ in range(max(0, pf - v_i))]
     pending = []  # global stores not yet visible: (first visible step, index, values)
     for t in range(total):
         # global stores become visible at the full barriers (before steps t % F == 0)
         keep = []
-        for vis, idx, val in pending:
-            if vis <= t:
+        for when, idx, val in pending:
+            if when <= t:
                 mem["planes"][idx] = val
             else:
-                keep.append((vis, idx, val))
+                keep.append((when, idx, val))
         pending = keep
         snap = {kk: vv.copy() for kk, vv in mem.items()}
+        hist[t] = snap
         writes = []
         for w, v in enumerate(waves):
             if not v.cur.valid(n, nb):
                 continue
+            # wave 0's wrap rows for step t + pf: loaded at step t + pf - zlead
+            zs = hist.get(t + pf - zlead, hist[0]) if zlead is not None else snap
             if t < w:
                 if t >= w - pf:
-                    v.rows.append(fetch(v, snap, w))
+                    v.rows.append(fetch(v, snap, w, zs))
                 continue
             cr = v.rows.pop(0)
-            v.rows.append(fetch(v, snap, w))
+            v.rows.append(fetch(v, snap, w, zs))
             dc = v.dc
             s = v.s
             if dc["on"]:
@@ -243,7 +254,7 @@ def emulate(x, bx, y, by, W, F=1, nb=1, gap=0.8, stack=1.0, subst=0.5, bound=0.0
             if name == "lds":
                 mem[name][idx] = val
             else:
-                pending.append(((t // F + 1) * F, idx, val))
+                pending.append(((t // F + 1) * F if vis is None else t + vis, idx, val))
     return 1.0 + sum(float(v.ksrc.sum()) for v in waves)
 
 
@@ -305,3 +316,40 @@ def test_emulation_sees_a_broken_schedule():
         assert not abs(bad - ref) <= 1e-12 * ref
         # with full barriers every F = 8 steps, W = m - 2 is past the limit m - F - 1
         assert not abs(emulate(x, bx, y, by, 9, F=8, nb=nb) - ref) <= 1e-12 * ref
+
+
+# the kernel's schedule (stem4d.hip sk_stem4d_col_kernel): rows PF = 4 ahead in
+# registers, no full barriers -- a global store is visible V = PF + 2 steps
+# later (the writer's in-order vmcnt wait for a load issued after it, PF
+# steps on, then a barrier; one step of margin) -- groups of at least
+# PF + V positions, wave 0's wrap rows staged PF + 1 steps ahead, and
+# W <= m - 2 PF - 2 (host: run_stem4d)
+KPF, KV = 4, 6
+
+
+def kernel_w_max(m):
+    return max(1, m - 2 * KPF - 2)
+
+
+@pytest.mark.parametrize("n,m,W", [(9, 14, 4), (12, 17, 7), (13, 20, 10), (5, 30, 12), (17, 30, 8),
+                                   (10, 11, 1), (7, 12, 2), (20, 25, 8)])
+@pytest.mark.parametrize("nb", [1, 2, 3])
+def test_kernel_schedule_equals_oracle(n, m, W, nb):
+    x, bx, y, by = _case(n, m)
+    assert W <= kernel_w_max(m)
+    got = emulate(x, bx, y, by, W, F=KV, nb=nb, pf=KPF, vis=KV, zlead=KPF + 1)
+    ref = _ref(x, bx, y, by)
+    assert abs(got - ref) <= 1e-12 * abs(ref), (got, ref)
+
+
+def test_kernel_schedule_limits_have_teeth():
+    """Two waves past the host's W limit (which keeps one wave of margin:
+    m - 2 PF - 1 is exact here), or a visibility lag longer than the schedule
+    allows for, gives a wrong K."""
+    x, bx, y, by = _case(17, 20)
+    ref = _ref(x, bx, y, by)
+    W = kernel_w_max(20)
+    assert abs(emulate(x, bx, y, by, W, F=KV, nb=2, pf=KPF, vis=KV, zlead=KPF + 1) - ref) <= 1e-12 * ref
+    bad = [emulate(x, bx, y, by, W + 2, F=KV, nb=2, pf=KPF, vis=KV, zlead=KPF + 1),
+           emulate(x, bx, y, by, W, F=KV + 2, nb=2, pf=KPF, vis=KV + 2, zlead=KPF + 1)]
+    assert all(not abs(b - ref) <= 1e-12 * ref for b in bad), bad
