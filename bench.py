@@ -72,11 +72,11 @@ CONFIGS = {
     # unit the reference computes per call (kernel_matrix.cpp:485-575), not a
     # slice whose launch fill and tail would dominate ("whole": steps repeat it)
     "c2": dict(kernel="ss", n=256, L=150, slices=1, whole=True, cid=1, cpu_pairs=12288),
-    # C3: 384 pairs per step (the batch's span launches longer: 349.7 against
-    # 303.5 pairs/s for 512 against 256 pairs on one box, r04t; 367.4 for 384
-    # against 360.4 for 512 and 345.2 for 640 on another, r04t2; 768 pairs
-    # exceed the 128 GB batch cap and split)
-    "c3": dict(kernel="stem4d", n=1024, L=200, slices=1367, cid=2, cpu_pairs=32),
+    # C3: 1,023 pairs per step, one workgroup per pair (LDS: one per CU), so
+    # four rounds of 256 CUs: 591.8 / 755.2 / 759.5 pairs/s for 384 / 768 /
+    # 1,023 pairs on one box (r05j; 384 leaves half the CUs idle in its
+    # second round)
+    "c3": dict(kernel="stem4d", n=1024, L=200, slices=513, cid=2, cpu_pairs=32),
     # async: step t+1 planned while step t runs (sk_set_async): C4 +3.6 % (its
     # 7 ms steps had 0.6-0.9 ms host gaps); the DAG configs gain <1 % and
     # their two concurrent class launches would then overlap fully, which
@@ -194,19 +194,16 @@ def dag_bytes(shapes, x, y):
     return float(np.sum(32.0 * V[x] * V[y] + S[x] + S[y] + 8.0))
 
 
-# columns per group of the 4-D column kernel by class (stem4d.hip s4c_nb)
-COL_NB = {1: 4, 2: 4, 4: 2, 8: 1}
-
-
 def col_shape(lens, y):
-    """(NB, W) of the 4-D column kernel, as run_stem4d picks them for a batch:
-    NB columns per group by class, W = 8 waves at most (two per SIMD), at most
-    m - 2 PF - 2 = m - 10 (the smallest y of the batch: the round wrap's lag,
-    stem4d.hip kS4cV; one batch per bench step)."""
+    """(NB, W) of the 4-D column kernel as run_stem4d picks them for a batch
+    (sk_stem4d_col_shape: NB chained columns per group by class, W waves per
+    pair bounded by m - 2 PF - 2 of the smallest y, registers and LDS; one
+    batch per bench step)."""
+    from stem_kernel_amd.kernel_matrix import stem4d_col_shape
     m = lens[y]
-    cpl = 1 if m.max() + 1 <= 64 else 2 if m.max() + 1 <= 128 else 4 if m.max() + 1 <= 256 else 8
-    w_env = int(os.environ.get("SK4C_W", "0"))
-    return COL_NB[cpl], int(max(1, min(w_env or 8, 8, int(m.min()) - 10)))
+    big = m[m >= 2]
+    sh = stem4d_col_shape(int(big.min()) if big.size else 0, int(m.max()))
+    return sh["nb"], sh["waves"]
 
 
 def stem4d_cells(lens, x, y):

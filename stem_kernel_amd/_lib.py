@@ -101,6 +101,7 @@ SIGNATURES = {
     "sk_comm_allgather": (C.c_int, [_P, C.c_void_p, C.c_int64, C.c_void_p]),
     "sk_gram_sharded": (C.c_int, [_P, _P, C.POINTER(KernelParams), C.c_int, _F64P]),
     "sk_last_classes": (C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "sk_stem4d_col_shape": (C.c_int, [C.c_int32, C.c_int32, _I32P, _I32P, _I32P]),
     "sk_ribosum_tables": (None, [_F32P, _F32P]),
     "sk_char2rna": (C.c_int, [C.c_int]),
     "sk_bpla_gradients": (C.c_int, [_P, _P, _P, C.POINTER(KernelParams), _I32P, _I32P, C.c_int64,

@@ -216,8 +216,10 @@ struct Stem4dLaunch {
   int64_t n_items = 0;
   int32_t d1 = 0;
   double* scratch = nullptr;
-  const float* bpdiag = nullptr;  // per example: prob(a, a+e) by diagonal e
-  const uint8_t* chars = nullptr;  // lowercased sequences
+  const float* bpdiag = nullptr;  // per x example: prob(a, a+e) by diagonal e
+  const uint8_t* chars = nullptr;  // lowercased x sequences
+  const float* bpdiag_y = nullptr;  // the same of the y examples (their
+  const uint8_t* chars_y = nullptr;  // dataset's resident tables)
   const double* gpow = nullptr;   // gap^k
   double gap = 0.0, stack = 0.0, subst = 0.0;
   float bp_bound = 0.0f;
@@ -245,6 +247,7 @@ hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st);
 // scratch_off; |y| < 512, and waves <= stem4d_col_w_max(m) for every pair
 // with m >= 2 (pairs with m <= 1 have K = 1 and take any waves)
 int stem4d_col_w_max(int m);
+int stem4d_col_pf();  // rows fetched ahead per wave (SK4C_PF)
 int stem4d_col_nb(int cpl);
 size_t stem4d_col_lds_bytes(int cpl, int waves, int max_m);
 int stem4d_col_max_waves(int cpl);
@@ -256,7 +259,8 @@ hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, in
 struct PhmmLaunch {
   const Stem4dPair* pairs = nullptr;
   int64_t n_pairs = 0;
-  const uint8_t* chars = nullptr;  // ACGU only (checked on the host)
+  const uint8_t* chars = nullptr;  // x sequences, ACGU only (checked on the host)
+  const uint8_t* chars_y = nullptr;  // y sequences
   char* scratch = nullptr;         // n_pairs * pair_bytes
   size_t pair_bytes = 0;           // phmm_pair_bytes(n1, m1)
   int32_t n1 = 1, m1 = 1;          // max |x|+1, max |y|+1 of the launch

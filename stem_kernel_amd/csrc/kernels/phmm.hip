@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(64) sk_phmm_kernel(PhmmLaunch P) {
   int32_t* yc = reinterpret_cast<int32_t*>(row0 + 3 * M1);
   int32_t* path = yc + M1;
   const uint8_t* xs = P.chars + pr.x_chr;
-  const uint8_t* ys = P.chars + pr.y_chr;
+  const uint8_t* ys = P.chars_y + pr.y_chr;
   const bool fx = P.zerop_fixed != 0;
   const double NEG = -__builtin_inf();
 #define SKW(s_, t_, st_) (((size_t)(s_) * T + (t_)) * 3 + (st_)) * 64 + l

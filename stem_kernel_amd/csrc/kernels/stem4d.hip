@@ -149,9 +149,9 @@ __global__ void __launch_bounds__(256, SK4_MINB) sk_stem4d_kernel(Stem4dLaunch P
     Cg = P.scratch + pr.scratch_off + (int64_t)((d1 - 2) % 3) * (n + 1) * 4 * cp +
          (int64_t)(i + 1) * 4 * cp + cp;
   const float* bpx = P.bpdiag + pr.x_bp;  // prob(a, a+e) at e*n - e*(e-1)/2 + a
-  const float* bpy = P.bpdiag + pr.y_bp;
+  const float* bpy = P.bpdiag_y + pr.y_bp;
   const uint8_t* xs = P.chars + pr.x_chr;
-  const uint8_t* ys = P.chars + pr.y_chr;
+  const uint8_t* ys = P.chars_y + pr.y_chr;
   const float bound = P.bp_bound;
   // bp_ij = prob(i, j-1): diagonal e = j-1-i = d1-1 of x  (:320)
   const int e1 = d1 - 1;
@@ -445,9 +445,9 @@ __global__ void __launch_bounds__(256) sk_stem4d_gsum_kernel(Stem4dLaunch P) {
   const double* Cg = d1 >= 2 ? ring + (int64_t)((d1 - 2) % 3) * (n + 1) * ps + (int64_t)(i + 1) * ps
                              : nullptr;  // plane (i+1, j-1), G0
   const float* bpx = P.bpdiag + pr.x_bp;  // prob(a, a+e) at e*n - e*(e-1)/2 + a
-  const float* bpy = P.bpdiag + pr.y_bp;
+  const float* bpy = P.bpdiag_y + pr.y_bp;
   const uint8_t* xs = P.chars + pr.x_chr;
-  const uint8_t* ys = P.chars + pr.y_chr;
+  const uint8_t* ys = P.chars_y + pr.y_chr;
   const float bound = P.bp_bound;
   const int e1 = d1 - 1;  // bp_ij = prob(i, j-1) (:320)
   const float bp_ij = bpx[(int64_t)e1 * n - (int64_t)e1 * (e1 - 1) / 2 + i];
@@ -658,9 +658,9 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
   const double* __restrict__ A = span_p1 + (int64_t)i * ps;        // plane (i, j-1): G0
   const double* __restrict__ B = span_p1 + (int64_t)(i + 1) * ps;  // plane (i+1, j): G0, this plane's B'
   const float* bpx = P.bpdiag + pr.x_bp;
-  const float* bpy = P.bpdiag + pr.y_bp;
+  const float* bpy = P.bpdiag_y + pr.y_bp;
   const uint8_t* xs = P.chars + pr.x_chr;
-  const uint8_t* ys = P.chars + pr.y_chr;
+  const uint8_t* ys = P.chars_y + pr.y_chr;
   const float bound = P.bp_bound;
   // the consumer: plane (i-1, j) of span d1+1, bp_c = prob(i-1, j-1) (:320)
   const bool cons = i >= 1;
@@ -847,13 +847,16 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 // and seen by the other waves after the next barrier; V = PF + 2 keeps one
 // step of margin.  Hence groups of at least PF + V positions and
 // W <= m - 2 PF - 2 (run_stem4d), which tests/test_stem4d_col_schedule.py
-// emulates step by step (m - 2 PF - 1 is exact there).
+// emulates step by step (m - 2 PF - 1 is exact there).  PF = 1 with NB = 4
+// at CPL 4: C3 (1,024 x L200) A/B, pairs/s: PF 1 NB 4 698, PF 2 NB 3 677,
+// PF 1 NB 3 612, PF 4 NB 2 519 (wider groups halve the row traffic per
+// cell; the registers they take come out of the prefetch depth).
 #ifndef SK4C_PF
-#define SK4C_PF 4
+#define SK4C_PF 1
 #endif
 constexpr int kS4cV = SK4C_PF + 2;
 #ifndef SK4C_NB4  // column-group width of the CPL 4 class (|y| 128..255)
-#define SK4C_NB4 2
+#define SK4C_NB4 4
 #endif
 
 template <int CPL>
@@ -928,7 +931,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   double* __restrict__ planes = P.scratch + pr.scratch_off;  // slot i: G0(i, latest column)
   double* __restrict__ wrapb = planes + (int64_t)n * cp;     // NB planes: B' across the round wrap
   const s4_cst<float> bpx = (s4_cst<float>)(P.bpdiag + pr.x_bp);
-  const float* bpy = P.bpdiag + pr.y_bp;
+  const float* bpy = P.bpdiag_y + pr.y_bp;
   const s4_cst<double> gpow = (s4_cst<double>)P.gpow;
   const float bound = P.bp_bound;
   // LDS: links [W][2][NB][TW] (wave w writes link w, wave w+1 reads it a step
@@ -942,7 +945,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   uint8_t* ysl = reinterpret_cast<uint8_t*>(red + W);
   uint8_t* xsl = ysl + TW + R + 8;
   for (int k = threadIdx.x; k < (W + 1) * 2 * NB * TW; k += blockDim.x) s4c_lds[k] = 0.0;
-  for (int k = threadIdx.x; k < TW + R + 8; k += blockDim.x) ysl[k] = k < m ? P.chars[pr.y_chr + k] : 0;
+  for (int k = threadIdx.x; k < TW + R + 8; k += blockDim.x) ysl[k] = k < m ? P.chars_y[pr.y_chr + k] : 0;
   for (int k = threadIdx.x; k < n; k += blockDim.x) xsl[k] = P.chars[pr.x_chr + k];
   __syncthreads();
 
@@ -1131,8 +1134,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     zload(wrq[q]);
   }
 
-  // every step: the barrier, this wave's row of the step (rq[0]) ...
-  auto head = [&](int t, Row& X) __attribute__((always_inline)) {
+  // every step: the barrier (this wave's row of the step is rq[0]) ...
+  auto head = [&](int t) __attribute__((always_inline)) {
     if (t > 0) {  // (every wave takes every barrier) LDS-only: the global stores by vmcnt (kS4cV)
       asm volatile("" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1146,13 +1149,12 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       for (int q = 0; q + 1 < PF; ++q) fq[q] = fq[q + 1];
       asm volatile("" ::"v"(f0));
     }
-    X = rq[0];
-#pragma unroll
-    for (int q = 0; q + 1 < PF; ++q) rq[q] = rq[q + 1];
   };
-  // ... and after the step's compute: the row of step t + PF, wave 0's wrap
+  // ... and after the step's compute: the queue moved on, the row of step t + PF, wave 0's wrap
   // rows (step t+1's into LDS, step t+PF+1's loaded), the fence load
   auto tail = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q + 1 < PF; ++q) rq[q] = rq[q + 1];
     fetch_next(rq[PF - 1]);
     if (yc.q.valid(n, NB)) {
       zstore(wst + (t & 1) * NB * TW, wrq[0]);
@@ -1180,7 +1182,6 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   asm volatile("" : "+v"(gv), "+v"(subv));
   uint32_t xk = 0u;  // bit c: y[k] == x[i-1] (the consumer's left base), per position
   Plane dc;
-  Row X;
 
   // row s >= 1 of the position: NS slots hold its cells (64 (NS-1) <= m - s
   // < 64 NS), chain by chain (one uniform branch per chain on its consumer's
@@ -1191,22 +1192,34 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     const int nk = m - s + 1;
     const double* lin = link_in + ((t - 1) & 1) * NB * TW;
     double* lout = link_out + (t & 1) * NB * TW;
-    const bool to_link = w + 1 < W;
+    // every wave writes its links to LDS; the last wave's (no reader) also
+    // go to the wrap planes: a buffer of 0 bytes on the other waves drops
+    // their stores (no branch per store)
+    const int nkw = w + 1 < W ? 0 : nk;
     const double gs = gpow[s];
+    // per slot, shared by the chains: prob_y(k, l-1) where a source, y[l-1]
+    // (recomputed per stacking chain in the widest groups: registers)
+    constexpr bool SHARE = NB <= 3;
     double A[NS], bpd[NS];
     uint32_t yl[NS];
+    const Row& X = rq[0];
 #pragma unroll
     for (int c = 0; c < NS; ++c) {
       A[c] = X.A[c];
-      bpd[c] = X.bp[c] > bound ? (double)X.bp[c] : 0.0;
-      yl[c] = ysl[lane + 64 * c + s - 1];
+      if (SHARE) {
+        bpd[c] = X.bp[c] > bound ? (double)X.bp[c] : 0.0;
+        yl[c] = ysl[lane + 64 * c + s - 1];
+      }
     }
     const uint32_t stk_mask = __builtin_amdgcn_readfirstlane(dc.stack);
     const int bch = BND ? __builtin_amdgcn_readfirstlane(dc.c0) : -1;
 #pragma unroll
     for (int ch = 0; ch < NB; ++ch) {
+      // (one chain at a time: the scheduler would otherwise hoist every
+      // chain's LDS reads to the top, past the register budget)
+      if (NB >= 4) __builtin_amdgcn_sched_barrier(0);
       const bool bz = BND && ch == bch;  // G0(i, i) row and no G1
-      const auto rw = s4c_rowbuf(wrapb + (int64_t)ch * cp + ro, nk);
+      const auto rw = s4c_rowbuf(wrapb + (int64_t)ch * cp + ro, nkw);
       if ((stk_mask >> ch) & 1u) {
         const uint32_t xcj = (dc.xcj >> (8 * ch)) & 0xffu;
 #pragma unroll
@@ -1225,10 +1238,12 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           const double ha = c + 1 < CPL ? bcast_lane0(Am2[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
           const double G3n = wave_shl1(G3c[ch][c], hg);
           const double A2 = wave_shl1(Am2[ch][c], ha);
-          const bool mt = ((xk >> c) & 1u) && yl[c] == xcj && bpd[c] != 0.0;
+          const double bp_kl = SHARE ? bpd[c] : X.bp[c] > bound ? (double)X.bp[c] : 0.0;
+          const uint32_t y_l = SHARE ? yl[c] : ysl[lane + 64 * c + s - 1];
+          const bool mt = ((xk >> c) & 1u) && y_l == xcj && bp_kl != 0.0;
           // the source (:320-331) without its stack * bp(i-1, j-1) factor,
           // which the position's sum takes at its end
-          kacc[ch] += A2 * bpd[c] * (mt ? 1.0 : subv);
+          kacc[ch] += A2 * bp_kl * (mt ? 1.0 : subv);
           double g3 = G3n * gv;
           g3 += mt ? A2 : 0.0;
           double g2 = G2c[ch][c] * gv;
@@ -1239,8 +1254,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           G3c[ch][c] = g3;
           Am2[ch][c] = Am1[ch][c];
           Am1[ch][c] = A[c];
-          if (to_link) lout[ch * TW + k] = Bn;
-          else s4c_rst64(rw, c, lane, Bn);
+          lout[ch * TW + k] = Bn;
+          s4c_rst64(rw, c, lane, Bn);
           A[c] = G0;
         }
       } else {
@@ -1253,8 +1268,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           double G0 = A[c] * gv;
           G0 += G1;
           const double Bn = G1 * gv;
-          if (to_link) lout[ch * TW + k] = Bn;
-          else s4c_rst64(rw, c, lane, Bn);
+          lout[ch * TW + k] = Bn;
+          s4c_rst64(rw, c, lane, Bn);
           A[c] = G0;
         }
       }
@@ -1266,7 +1281,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
 
   int t = 0;
   for (; t < w && t < total; ++t) {  // before the wave's first position
-    head(t, X);
+    head(t);
     tail(t);
   }
   // a position's rows 1 .. m in phases of NS active slots, CPL down to 1
@@ -1276,7 +1291,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       constexpr int NS = decltype(ns_tag)::value;
       const int s_end = NS > 1 ? m - 64 * (NS - 1) : m;
       for (; s <= s_end; ++s, ++t) {
-        head(t, X);
+        head(t);
         row(t, s, ro, bnd_tag, ns_tag);
         tail(t);
         ro += pad4(m + 1 - s);
@@ -1301,11 +1316,11 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     dc = describe(cur);
     if (!dc.on) {  // a bubble
       for (int s = 0; s < R; ++s, ++t) {
-        head(t, X);
+        head(t);
         tail(t);
       }
     } else {
-      head(t, X);  // row 0, cells (l, l): G0 = g^(j-i), never stored; the chains' registers reset
+      head(t);  // row 0, cells (l, l): G0 = g^(j-i), never stored; the chains' registers reset
       xk = 0u;
 #pragma unroll
       for (int c = 0; c < CPL; ++c) xk |= (ysl[lane + 64 * c] == dc.xci ? 1u : 0u) << c;
@@ -1331,7 +1346,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     cur.advance(W, n, NB, FP);
   }
   for (; t < total; ++t) {  // after the wave's last position
-    head(t, X);
+    head(t);
     tail(t);
   }
   for (int off = 32; off > 0; off >>= 1) ksrc += __shfl_xor(ksrc, off, 64);
@@ -1345,6 +1360,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
 }
 
 int stem4d_col_w_max(int m) { return m - 2 * SK4C_PF - 2; }
+int stem4d_col_pf() { return SK4C_PF; }
 
 int stem4d_col_max_waves(int cpl) {
   return cpl <= 1 ? s4c_max_waves<1>() : cpl == 2 ? s4c_max_waves<2>() : cpl == 4 ? s4c_max_waves<4>()

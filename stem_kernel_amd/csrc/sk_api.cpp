@@ -151,6 +151,22 @@ struct HostPack {
 
 }  // namespace
 
+// 4-D stem kernel tables of every example of a dataset, resident on the
+// device: built on the first 4-D call for a bp model and loop, rebuilt when
+// examples were added since (examples are append-only); stem4d_tables
+struct Stem4dTables {
+  DeviceBuffers buf;
+  int device = -1, model = -1;
+  unsigned loop = 0;
+  size_t n_ex = 0;
+  const float* bp = nullptr;
+  const uint8_t* ch = nullptr;
+  std::vector<int64_t> bp_off, ch_off;
+  // per example: 0 usable, 1 several rows, 2 no base pairs (bp_model 0);
+  // acgu: only A/C/G/U residues (the PairHMM constraints need them)
+  std::vector<uint8_t> why, acgu;
+};
+
 struct sk_dataset {
   std::vector<Example> ex;
   std::vector<std::string> labels;
@@ -165,6 +181,7 @@ struct sk_dataset {
   // depend only on the dataset (immutable once uploaded) and loop_gap
   double* prep = nullptr;
   double prep_loop_gap = -1.0;
+  Stem4dTables s4;
 };
 
 struct Stem4dBatch {
@@ -1813,10 +1830,64 @@ void stem4d_tables(const Example& X, const sk_kernel_params* kp, std::vector<flo
     }
 }
 
+static int stem4d_dataset_tables(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp) {
+  Stem4dTables& T = ds->s4;
+  if (T.bp && T.device == ctx->device && T.model == kp->bp_model && T.loop == kp->loop &&
+      T.n_ex == ds->ex.size())
+    return SK_OK;
+  const size_t n = ds->ex.size();
+  std::vector<float> bpall, bp;
+  std::vector<uint8_t> chall, chr;
+  T.bp_off.assign(n, -1);
+  T.ch_off.assign(n, -1);
+  T.why.assign(n, 0);
+  T.acgu.assign(n, 0);
+  for (size_t e = 0; e < n; ++e) {
+    const Example& X = ds->ex[e];
+    if (X.n_rows != 1) {
+      T.why[e] = 1;
+      continue;
+    }
+    if (kp->bp_model == 0 && !X.has_bp) {
+      T.why[e] = 2;
+      continue;
+    }
+    stem4d_tables(X, kp, bp, chr);
+    T.acgu[e] = 1;
+    for (int a = 0; a < X.len; ++a)
+      if (!std::strchr("acgu", (char)chr[a]) || !chr[a]) T.acgu[e] = 0;
+    T.bp_off[e] = (int64_t)bpall.size();
+    T.ch_off[e] = (int64_t)chall.size();
+    bpall.insert(bpall.end(), bp.begin(), bp.end());
+    chall.insert(chall.end(), chr.begin(), chr.end());
+  }
+  T.bp = nullptr;
+  T.ch = nullptr;
+  T.buf.release();  // (hipFree waits for the launches that read the old tables)
+  SK_HIP(ctx, upload(T.buf, bpall, &T.bp));
+  SK_HIP(ctx, upload(T.buf, chall, &T.ch));
+  T.device = ctx->device;
+  T.model = kp->bp_model;
+  T.loop = kp->loop;
+  T.n_ex = n;
+  return SK_OK;
+}
+
 int64_t stem4d_plane_doubles(int m) {
   int64_t r = 0;
   for (int d2 = 0; d2 <= m; ++d2) r += ((m + 1 - d2) + 3) & ~3;
   return r;
+}
+
+// waves per pair of the column kernel for a batch whose y lengths lie in
+// [min_m, max_m] (min_m counts |y| >= 2 only; INT32_MAX for none)
+static int col_waves(int cpl, int min_m, int max_m) {
+  static const int w_env = std::getenv("SK4C_W") ? std::max(1, std::atoi(std::getenv("SK4C_W"))) : 0;
+  int W = std::min(w_env ? w_env : sk::stem4d_col_max_waves(cpl), sk::stem4d_col_max_waves(cpl));
+  if (min_m != INT32_MAX) W = std::min(W, sk::stem4d_col_w_max(min_m));
+  W = std::max(W, 1);
+  while (W > 1 && sk::stem4d_col_lds_bytes(cpl, W, max_m) > 160 * 1024) --W;
+  return W;
 }
 
 int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_params* kp,
@@ -1834,37 +1905,23 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // full NaN-propagating restatement), and partial_dp over the full range is
   // full_dp operation for operation.
   const bool ali_phmm = ali && kp->ali_zerop_fixed;
-  // per-example tables of the examples this call touches
-  struct Tab { int64_t bp = -1, chr = -1; };
-  std::vector<Tab> tx(xs_->ex.size()), ty(ys_->ex.size());
-  std::vector<float> bpall;
-  std::vector<uint8_t> chall;
-  std::vector<float> bp;
-  std::vector<uint8_t> chr;
-  auto touch = [&](const Example& X, Tab& t) -> int {
-    if (t.bp >= 0) return SK_OK;
-    if (X.n_rows != 1) return fail(ctx, SK_ERR_INVALID, "4-D stem kernel takes single sequences");
-    if (kp->bp_model == 0 && !X.has_bp)
-      return fail(ctx, SK_ERR_INVALID, "4-D stem kernel with bp_model 0 needs base pairs");
-    stem4d_tables(X, kp, bp, chr);
-    if (ali)  // PairHMM's char2rna asserts on anything else (phmm.cpp:247-258)
-      for (int a = 0; a < X.len; ++a)
-        if (!std::strchr("acguACGU", (char)chr[a]))
-          return fail(ctx, SK_ERR_INVALID,
-                      "4-D stem kernel: alignment constraints need A/C/G/U sequences");
-    t.bp = (int64_t)bpall.size();
-    t.chr = (int64_t)chall.size();
-    bpall.insert(bpall.end(), bp.begin(), bp.end());
-    chall.insert(chall.end(), chr.begin(), chr.end());
+  // per-example tables, resident per dataset (built on first use)
+  int rc = stem4d_dataset_tables(ctx, xs_, kp);
+  if (rc) return rc;
+  if (ys_ != xs_ && (rc = stem4d_dataset_tables(ctx, ys_, kp))) return rc;
+  const Stem4dTables& TX = xs_->s4;
+  const Stem4dTables& TY = ys_->s4;
+  auto usable = [&](const Stem4dTables& T, int e) -> int {
+    if (T.why[e] == 1) return fail(ctx, SK_ERR_INVALID, "4-D stem kernel takes single sequences");
+    if (T.why[e] == 2) return fail(ctx, SK_ERR_INVALID, "4-D stem kernel with bp_model 0 needs base pairs");
+    if (ali && !T.acgu[e])  // PairHMM's char2rna asserts on anything else (phmm.cpp:247-258)
+      return fail(ctx, SK_ERR_INVALID, "4-D stem kernel: alignment constraints need A/C/G/U sequences");
     return SK_OK;
   };
   int max_m = 0, max_n = 0;
   double cells = 0.0;
   for (int64_t k = 0; k < n; ++k) {
-    int rc = touch(xs_->ex[x[k]], tx[x[k]]);
-    if (rc) return rc;
-    rc = touch(ys_->ex[y[k]], ty[y[k]]);
-    if (rc) return rc;
+    if ((rc = usable(TX, x[k])) || (rc = usable(TY, y[k]))) return rc;
     const double a = xs_->ex[x[k]].len, b = ys_->ex[y[k]].len;
     max_m = std::max(max_m, (int)b);
     max_n = std::max(max_n, (int)a);
@@ -1880,18 +1937,11 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // g^k for y spans (d1 = 0 planes) and, in the column kernel, x spans (the
   // diagonal cells G0(i, j, l, l) = g^(j-i))
   const std::vector<double> gp = gap_powers(kp->gap, std::max(max_m, max_n) + 2);
-  // device-side tables for the whole call
-  const size_t nb_bp = std::max<size_t>(bpall.size(), 1), nb_ch = std::max<size_t>(chall.size(), 1);
-  size_t need = nb_bp * 4 + nb_ch + gp.size() * 8 + 4096;
-  int rc = ensure_work(ctx, need);
+  rc = ensure_work(ctx, gp.size() * 8 + 4096);
   if (rc) return rc;
   Arena A{static_cast<char*>(ctx->work), 0, ctx->work_bytes};
-  float* d_bp = A.take<float>(nb_bp);
-  uint8_t* d_ch = A.take<uint8_t>(nb_ch);
   double* d_gp = A.take<double>(gp.size());
   hipStream_t S = ctx->stream;
-  SK_HIP(ctx, hipMemcpyAsync(d_bp, bpall.data(), bpall.size() * 4, hipMemcpyHostToDevice, S));
-  SK_HIP(ctx, hipMemcpyAsync(d_ch, chall.data(), chall.size(), hipMemcpyHostToDevice, S));
   SK_HIP(ctx, hipMemcpyAsync(d_gp, gp.data(), gp.size() * 8, hipMemcpyHostToDevice, S));
   const int cpl = sk::stem4d_cpl(max_m);
   // |y| >= 512: the kernel sweeps k tiles of 512 and hands each tile's first
@@ -1949,10 +1999,10 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       p.scratch_off = (int64_t)(ring_bytes / 8);
       bytes += pb;
       ring_bytes += rb;
-      p.x_bp = tx[x[q]].bp;
-      p.x_chr = tx[x[q]].chr;
-      p.y_bp = ty[y[q]].bp;
-      p.y_chr = ty[y[q]].chr;
+      p.x_bp = TX.bp_off[x[q]];
+      p.x_chr = TX.ch_off[x[q]];
+      p.y_bp = TY.bp_off[y[q]];
+      p.y_chr = TY.ch_off[y[q]];
       p.out_index = q;
       maxn = std::max(maxn, p.n);
       prs.push_back(p);
@@ -1966,11 +2016,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       int min_m = INT32_MAX;
       for (const auto& p : prs)
         if (p.m >= 2) min_m = std::min(min_m, p.m);
-      static const int w_env = std::getenv("SK4C_W") ? std::max(1, std::atoi(std::getenv("SK4C_W"))) : 0;
-      int W = std::min(w_env ? w_env : sk::stem4d_col_max_waves(cpl), sk::stem4d_col_max_waves(cpl));
-      if (min_m != INT32_MAX) W = std::min(W, sk::stem4d_col_w_max(min_m));
-      W = std::max(W, 1);
-      while (W > 1 && sk::stem4d_col_lds_bytes(cpl, W, max_m) > 160 * 1024) --W;
+      const int W = col_waves(cpl, min_m, max_m);
       rc = ensure_scratch(ctx, ring_bytes + 64);
       if (rc) return rc;
       if (Bt.cap_pairs < prs.size()) {
@@ -1986,8 +2032,10 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       sk::Stem4dLaunch L;
       L.pairs = Bt.pairs;
       L.scratch = ctx->scratch;
-      L.bpdiag = d_bp;
-      L.chars = d_ch;
+      L.bpdiag = TX.bp;
+      L.chars = TX.ch;
+      L.bpdiag_y = TY.bp;
+      L.chars_y = TY.ch;
       L.gpow = d_gp;
       L.gap = kp->gap;
       L.stack = kp->stack;
@@ -2088,8 +2136,10 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     sk::Stem4dLaunch L;
     L.pairs = Bt.pairs;
     L.scratch = ctx->scratch;
-    L.bpdiag = d_bp;
-    L.chars = d_ch;
+    L.bpdiag = TX.bp;
+    L.chars = TX.ch;
+    L.bpdiag_y = TY.bp;
+    L.chars_y = TY.ch;
     L.gpow = d_gp;
     L.gap = kp->gap;
     L.stack = kp->stack;
@@ -2109,7 +2159,8 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       sk::PhmmLaunch H;
       H.pairs = Bt.pairs;
       H.n_pairs = (int64_t)prs.size();
-      H.chars = d_ch;
+      H.chars = TX.ch;
+      H.chars_y = TY.ch;
       H.scratch = reinterpret_cast<char*>(ctx->scratch);
       H.n1 = max_n1;
       H.m1 = max_m1;
@@ -3933,6 +3984,15 @@ int sk_last_launch_ms(const sk_context* ctx, double* ms_sum, int32_t* n_launches
   if (!ctx) return SK_ERR_INVALID;
   if (ms_sum) *ms_sum = ctx->last_launch_ms_sum;
   if (n_launches) *n_launches = ctx->last_launch_n;
+  return SK_OK;
+}
+
+int sk_stem4d_col_shape(int32_t min_len, int32_t max_len, int32_t* nb, int32_t* waves, int32_t* pf) {
+  if (max_len < 0 || min_len > max_len) return SK_ERR_INVALID;
+  const int cpl = sk::stem4d_cpl(max_len);
+  if (nb) *nb = sk::stem4d_col_nb(cpl);
+  if (waves) *waves = col_waves(cpl, min_len >= 2 ? min_len : INT32_MAX, max_len);
+  if (pf) *pf = sk::stem4d_col_pf();
   return SK_OK;
 }
 

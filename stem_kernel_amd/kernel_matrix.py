@@ -622,6 +622,15 @@ class Context:
         return dict(stem_maxk=maxk, stem4d=s4d, stem4d_col=col)
 
 
+def stem4d_col_shape(min_len: int, max_len: int) -> dict:
+    """Shape of the column-pipelined 4-D kernel for a batch of y examples of
+    lengths [min_len, max_len] (sk_stem4d_col_shape): chained columns per
+    group, waves per pair and rows fetched ahead per wave."""
+    v = [C.c_int32() for _ in range(3)]
+    check(lib().sk_stem4d_col_shape(int(min_len), int(max_len), *[C.byref(a) for a in v]))
+    return dict(nb=v[0].value, waves=v[1].value, pf=v[2].value)
+
+
 def format_libsvm(matrix: np.ndarray, labels: Sequence[str]) -> str:
     m = np.ascontiguousarray(matrix, dtype=np.float64)
     rows, cols = m.shape

@@ -127,6 +127,27 @@ def test_stem4d_params_and_predict(gpu_ctx):
     assert rel_err(row, ref) < TOL
 
 
+@pytest.mark.gpu
+def test_stem4d_resident_tables_two_datasets(gpu_ctx):
+    """The per-example tables stay resident per dataset (sk_api.cpp
+    stem4d_dataset_tables): test x train across two datasets reads each side
+    from its own dataset's tables, and a new bp model or loop rebuilds them
+    (the same datasets first under NormalBasePair loop 3, then -p, then
+    WobbleBasePair loop 5)."""
+    tr = ska.random_sequences(4, 45, 0x5EED0051) + ["GGGGAAAACCCC"]
+    te = ska.random_sequences(3, 70, 0x5EED0052)
+    dtr, _ = make_examples(tr)
+    dte, _ = make_examples(te)
+    for kern in [ska.StemKernel4D(bp_model=1, bp_bound=0.5), ska.StemKernel4D(),
+                 ska.StemKernel4D(bp_model=2, bp_bound=0.5, loop=5)]:
+        got, _ = gpu_ctx.test_matrix(dte, dtr, kern)
+        p = kern.params
+        ref = np.array([[po.stem4d(a.lower(), ska.fold(a), b.lower(), ska.fold(b), p.gap, p.stack,
+                                   p.subst, p.bp_bound, p.bp_model, p.loop, p.len_band,
+                                   p.ali_bound, p.ali_zerop_fixed) for b in tr] for a in te])
+        assert rel_err(got, ref) < TOL
+
+
 def test_oracle_band_wide_equals_full_dp():
     """partial_dp with a band wider than both sequences computes every cell."""
     s = ska.random_sequences(3, 24, 21) + ska.random_sequences(1, 17, 22)
