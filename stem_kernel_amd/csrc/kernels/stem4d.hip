@@ -840,21 +840,23 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 // row (a cell reads k and k+1 of earlier rows, both valid there), and add
 // nothing to K (their bp loads return 0, and bound >= 0).
 // Rows fetched ahead (PF, in registers) and the visibility lag of a global
-// store (V steps).  There are no full barriers: every step issues at least
-// one vector load after its stores and waits, PF steps later, for the load
-// issued PF steps before (vmcnt counts loads and stores together, in issue
-// order), so a store of step u is complete when its wave starts step u + PF
-// and seen by the other waves after the next barrier; V = PF + 2 keeps one
-// step of margin.  Hence groups of at least PF + V positions and
-// W <= m - 2 PF - 2 (run_stem4d), which tests/test_stem4d_col_schedule.py
-// emulates step by step (m - 2 PF - 1 is exact there).  PF = 1 with NB = 4
+// store (V steps).  There are no full barriers: every step ends with a
+// vector load issued after its stores (the fence load), and the next step's
+// tail waits for it (vmcnt counts loads and stores together, in issue order),
+// so a store of step u is complete when its wave ends step u + 1 and seen by
+// the other waves after the barrier of step u + 2: V = 2.  Hence groups of at
+// least PF + V positions and W <= m - PF - V (run_stem4d), which
+// tests/test_stem4d_col_schedule.py emulates step by step (m - PF - V + 1 is
+// exact there).  Every load of a step is issued whether its row exists or
+// not (a range-checked buffer of 0 bytes returns 0 without a memory access):
+// a load on one path only leaves a phi whose register copy waits for it.  PF = 1 with NB = 4
 // at CPL 4: C3 (1,024 x L200) A/B, pairs/s: PF 1 NB 4 698, PF 2 NB 3 677,
 // PF 1 NB 3 612, PF 4 NB 2 519 (wider groups halve the row traffic per
 // cell; the registers they take come out of the prefetch depth).
 #ifndef SK4C_PF
 #define SK4C_PF 1
 #endif
-constexpr int kS4cV = SK4C_PF + 2;
+constexpr int kS4cV = 2;
 #ifndef SK4C_NB4  // column-group width of the CPL 4 class (|y| 128..255)
 #define SK4C_NB4 4
 #endif
@@ -1057,23 +1059,17 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   cur_init(fc, w);
   int fdelay = w;
   auto fetch_next = [&](Row& r) __attribute__((always_inline)) {
-    if (fdelay > 0) {
-      --fdelay;
-      return;
-    }
-    if (fc.q.valid(n, NB)) {
-      if (fc.on && fc.s >= 1) {
-        const int nk = m - fc.s + 1;  // valid cells of the row
-        const auto ra = s4c_rowbuf(planes + (int64_t)fc.i * cp + fc.ro, nk);
-        const auto rb = s4c_rowbuf(bpy + fc.ye, nk);
+    const bool ld = fdelay <= 0 && fc.q.valid(n, NB) && fc.on && fc.s >= 1;
+    const int nk = ld ? m - fc.s + 1 : 0;  // valid cells of the row
+    const auto ra = s4c_rowbuf(planes + (ld ? (int64_t)fc.i * cp + fc.ro : 0), nk);
+    const auto rb = s4c_rowbuf(bpy + (ld ? fc.ye : 0), nk);
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          r.A[c] = s4c_rld64(ra, c, lane);
-          r.bp[c] = s4c_rld32(rb, c, lane);
-        }
-      }
-      cur_next(fc);
+    for (int c = 0; c < CPL; ++c) {
+      r.A[c] = s4c_rld64(ra, c, lane);
+      r.bp[c] = s4c_rld32(rb, c, lane);
     }
+    if (fdelay > 0) --fdelay;
+    else if (fc.q.valid(n, NB)) cur_next(fc);
   };
 
   // The round wrap: wave 0's positions are 0, W, 2W, ..., so at step u it
@@ -1093,12 +1089,14 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
 #pragma unroll
     for (int e = 0; e < SEGR; ++e) wrq[q][e] = 0.0;
   auto zload = [&](double (&wr)[SEGR]) __attribute__((always_inline)) {
-    if (!zc.on || zc.s == 0) return;
-    const int nk = m - zc.s + 1;
+    const bool ld = zc.q.valid(n, NB) && zc.on && zc.s != 0;
+    const int nk = ld ? m - zc.s + 1 : 0;
+    const int ro = ld ? zc.ro : 0;
 #pragma unroll
     for (int q = 0; q < SEGR; ++q) {
       const int sg = w + q * W, ch = sg / CPL, c = sg % CPL;
-      if (sg < NSEG) wr[q] = s4c_rld64(s4c_rowbuf(wrapb + (int64_t)ch * cp + zc.ro, nk), c, lane);
+      // (sg >= NSEG: wave w has no q-th segment -- W > NSEG / SEGR -- nothing to load)
+      wr[q] = s4c_rld64(s4c_rowbuf(wrapb + (int64_t)(ch < NB ? ch : 0) * cp + ro, sg < NSEG ? nk : 0), c % CPL, lane);
     }
   };
   auto zstore = [&](double* dst, const double (&wr)[SEGR]) __attribute__((always_inline)) {
@@ -1116,11 +1114,9 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       }
     }
   };
-  // the fence loads: one 4-byte load per step into fq, consumed PF steps
-  // later, so every step's stores complete by then (see kS4cV)
-  float fq[PF];
-#pragma unroll
-  for (int q = 0; q < PF; ++q) fq[q] = 0.0f;
+  // the fence load: one 4-byte load at the end of every step, waited for at
+  // the end of the next, so every step's stores complete by then (kS4cV)
+  float fq = 0.0f;
   const auto fence_buf = s4c_rowbuf(bpy, 1);
 
   // steps -PF .. -1: this wave's first rows (of steps 0 .. PF-1; before its
@@ -1133,9 +1129,22 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     cur_next(zc);
     zload(wrq[q]);
   }
+  fq = s4c_rld32(fence_buf, 0, lane);
 
+#ifdef SK4C_TIMING  // diagnostic build: cycles per step part, printed for two blocks
+  uint64_t tm_bar = 0, tm_fence = 0, tm_row = 0, tm_tail = 0, tm_a = 0, tm_b = 0;
+  int tm_steps = 0;
+#define S4C_TICK(v) (v = (uint64_t)clock64())
+#else
+#define S4C_TICK(v) ((void)0)
+#endif
   // every step: the barrier (this wave's row of the step is rq[0]) ...
   auto head = [&](int t) __attribute__((always_inline)) {
+#ifdef SK4C_TIMING
+    uint64_t t0, t1;
+    S4C_TICK(t0);
+    if (tm_a) tm_tail += t0 - tm_a;
+#endif
     if (t > 0) {  // (every wave takes every barrier) LDS-only: the global stores by vmcnt (kS4cV)
       asm volatile("" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1143,30 +1152,40 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
       asm volatile("" ::: "memory");
     }
-    {  // the fence load of step t - PF: this wave's stores up to then are complete
-      const float f0 = fq[0];
-#pragma unroll
-      for (int q = 0; q + 1 < PF; ++q) fq[q] = fq[q + 1];
-      asm volatile("" ::"v"(f0));
-    }
+#ifdef SK4C_TIMING
+    S4C_TICK(t1);
+#endif
+#ifdef SK4C_TIMING
+    S4C_TICK(tm_b);
+    tm_bar += t1 - t0;
+    tm_fence += tm_b - t1;
+    tm_a = tm_b;
+    ++tm_steps;
+#endif
   };
-  // ... and after the step's compute: the queue moved on, the row of step t + PF, wave 0's wrap
-  // rows (step t+1's into LDS, step t+PF+1's loaded), the fence load
-  auto tail = [&](int t) __attribute__((always_inline)) {
-#pragma unroll
-    for (int q = 0; q + 1 < PF; ++q) rq[q] = rq[q + 1];
-    fetch_next(rq[PF - 1]);
+  // ... and after the step's compute: wave 0's wrap rows of step t+1 into
+  // LDS, the wait for the previous step's fence load, the queue moved on,
+  // the row of step t + PF and wave 0's wrap rows of step t+PF+1 loaded, the
+  // fence load
+  // (FETCHED: a row step with PF = 1 issued the fetch after its prologue)
+  auto tail = [&](int t, auto fetched_tag) __attribute__((always_inline)) {
     if (yc.q.valid(n, NB)) {
       zstore(wst + (t & 1) * NB * TW, wrq[0]);
       cur_next(yc);
-#pragma unroll
-      for (int q = 0; q + 1 < PF; ++q)
-#pragma unroll
-        for (int e = 0; e < SEGR; ++e) wrq[q][e] = wrq[q + 1][e];
-      cur_next(zc);
-      zload(wrq[PF - 1]);
     }
-    fq[PF - 1] = s4c_rld32(fence_buf, 0, lane);  // (lane 0 reads bpy[0], the rest nothing)
+    asm volatile("" ::"v"(fq));  // this wave's stores of step t-1 are complete
+    if constexpr (!decltype(fetched_tag)::value) {
+#pragma unroll
+      for (int q = 0; q + 1 < PF; ++q) rq[q] = rq[q + 1];
+      fetch_next(rq[PF - 1]);
+    }
+#pragma unroll
+    for (int q = 0; q + 1 < PF; ++q)
+#pragma unroll
+      for (int e = 0; e < SEGR; ++e) wrq[q][e] = wrq[q + 1][e];
+    if (zc.q.valid(n, NB)) cur_next(zc);
+    zload(wrq[PF - 1]);
+    fq = s4c_rld32(fence_buf, 0, lane);  // (lane 0 reads bpy[0], the rest nothing)
   };
 
   double ksrc = 0.0, kacc[NB];
@@ -1186,31 +1205,29 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   // row s >= 1 of the position: NS slots hold its cells (64 (NS-1) <= m - s
   // < 64 NS), chain by chain (one uniform branch per chain on its consumer's
   // stacking); BND: a boundary chain c0 (a top-triangle position)
-  auto row = [&](int t, int s, int ro, auto bnd_tag, auto ns_tag) __attribute__((always_inline)) {
+  auto row = [&](int t, int s, int ro, auto bnd_tag, auto ns_tag, auto last_tag) __attribute__((always_inline)) {
     constexpr bool BND = decltype(bnd_tag)::value;
     constexpr int NS = decltype(ns_tag)::value;
+    // the last wave hands its B' rows on through the wrap planes, the others
+    // through their LDS links (the last wave's link has no reader)
+    constexpr bool LASTW = decltype(last_tag)::value;
     const int nk = m - s + 1;
     const double* lin = link_in + ((t - 1) & 1) * NB * TW;
     double* lout = link_out + (t & 1) * NB * TW;
-    // every wave writes its links to LDS; the last wave's (no reader) also
-    // go to the wrap planes: a buffer of 0 bytes on the other waves drops
-    // their stores (no branch per store)
-    const int nkw = w + 1 < W ? 0 : nk;
     const double gs = gpow[s];
     // per slot, shared by the chains: prob_y(k, l-1) where a source, y[l-1]
-    // (recomputed per stacking chain in the widest groups: registers)
-    constexpr bool SHARE = NB <= 3;
     double A[NS], bpd[NS];
     uint32_t yl[NS];
     const Row& X = rq[0];
 #pragma unroll
     for (int c = 0; c < NS; ++c) {
       A[c] = X.A[c];
-      if (SHARE) {
-        bpd[c] = X.bp[c] > bound ? (double)X.bp[c] : 0.0;
-        yl[c] = ysl[lane + 64 * c + s - 1];
-      }
+      bpd[c] = X.bp[c] > bound ? (double)X.bp[c] : 0.0;
+      yl[c] = ysl[lane + 64 * c + s - 1];
     }
+    // the queue's row is in A / bpd now: with PF = 1 the next row's loads go
+    // out here, into the same registers, a whole step ahead of their use
+    if constexpr (PF == 1) fetch_next(rq[0]);
     const uint32_t stk_mask = __builtin_amdgcn_readfirstlane(dc.stack);
     const int bch = BND ? __builtin_amdgcn_readfirstlane(dc.c0) : -1;
 #pragma unroll
@@ -1219,7 +1236,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       // chain's LDS reads to the top, past the register budget)
       if (NB >= 4) __builtin_amdgcn_sched_barrier(0);
       const bool bz = BND && ch == bch;  // G0(i, i) row and no G1
-      const auto rw = s4c_rowbuf(wrapb + (int64_t)ch * cp + ro, nkw);
+      const auto rw = s4c_rowbuf(wrapb + (int64_t)ch * cp + ro, LASTW ? nk : 0);
       if ((stk_mask >> ch) & 1u) {
         const uint32_t xcj = (dc.xcj >> (8 * ch)) & 0xffu;
 #pragma unroll
@@ -1238,8 +1255,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           const double ha = c + 1 < CPL ? bcast_lane0(Am2[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
           const double G3n = wave_shl1(G3c[ch][c], hg);
           const double A2 = wave_shl1(Am2[ch][c], ha);
-          const double bp_kl = SHARE ? bpd[c] : X.bp[c] > bound ? (double)X.bp[c] : 0.0;
-          const uint32_t y_l = SHARE ? yl[c] : ysl[lane + 64 * c + s - 1];
+          const double bp_kl = bpd[c];
+          const uint32_t y_l = yl[c];
           const bool mt = ((xk >> c) & 1u) && y_l == xcj && bp_kl != 0.0;
           // the source (:320-331) without its stack * bp(i-1, j-1) factor,
           // which the position's sum takes at its end
@@ -1254,8 +1271,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           G3c[ch][c] = g3;
           Am2[ch][c] = Am1[ch][c];
           Am1[ch][c] = A[c];
-          lout[ch * TW + k] = Bn;
-          s4c_rst64(rw, c, lane, Bn);
+          if (LASTW) s4c_rst64(rw, c, lane, Bn);
+          else lout[ch * TW + k] = Bn;
           A[c] = G0;
         }
       } else {
@@ -1268,8 +1285,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           double G0 = A[c] * gv;
           G0 += G1;
           const double Bn = G1 * gv;
-          lout[ch * TW + k] = Bn;
-          s4c_rst64(rw, c, lane, Bn);
+          if (LASTW) s4c_rst64(rw, c, lane, Bn);
+          else lout[ch * TW + k] = Bn;
           A[c] = G0;
         }
       }
@@ -1280,9 +1297,10 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   };
 
   int t = 0;
+  auto run = [&](auto last_tag) __attribute__((always_inline)) {
   for (; t < w && t < total; ++t) {  // before the wave's first position
     head(t);
-    tail(t);
+    tail(t, std::false_type());
   }
   // a position's rows 1 .. m in phases of NS active slots, CPL down to 1
   auto rows = [&](auto bnd_tag) __attribute__((always_inline)) {
@@ -1292,8 +1310,16 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       const int s_end = NS > 1 ? m - 64 * (NS - 1) : m;
       for (; s <= s_end; ++s, ++t) {
         head(t);
-        row(t, s, ro, bnd_tag, ns_tag);
-        tail(t);
+        row(t, s, ro, bnd_tag, ns_tag, last_tag);
+#ifdef SK4C_TIMING
+        {
+          uint64_t tr;
+          S4C_TICK(tr);
+          tm_row += tr - tm_a;
+          tm_a = tr;
+        }
+#endif
+        tail(t, std::integral_constant<bool, PF == 1>());
         ro += pad4(m + 1 - s);
       }
     };
@@ -1317,7 +1343,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     if (!dc.on) {  // a bubble
       for (int s = 0; s < R; ++s, ++t) {
         head(t);
-        tail(t);
+        tail(t, std::false_type());
       }
     } else {
       head(t);  // row 0, cells (l, l): G0 = g^(j-i), never stored; the chains' registers reset
@@ -1333,7 +1359,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           Am2[ch][c] = G2c[ch][c] = G3c[ch][c] = 0.0;
         }
       }
-      tail(t);
+      tail(t, std::false_type());
       ++t;
       if (dc.c0 >= 0) rows(std::true_type());
       else rows(std::false_type());
@@ -1347,8 +1373,16 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   }
   for (; t < total; ++t) {  // after the wave's last position
     head(t);
-    tail(t);
+    tail(t, std::false_type());
   }
+  };
+  if (w + 1 == W) run(std::true_type());
+  else run(std::false_type());
+#ifdef SK4C_TIMING
+  if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+    printf("sk4c b%d w%d steps %d bar %lu fence %lu row %lu tail %lu\n", (int)blockIdx.x, w, tm_steps,
+           (unsigned long)tm_bar, (unsigned long)tm_fence, (unsigned long)tm_row, (unsigned long)tm_tail);
+#endif
   for (int off = 32; off > 0; off >>= 1) ksrc += __shfl_xor(ksrc, off, 64);
   if (lane == 0) red[w] = ksrc;
   __syncthreads();
@@ -1359,7 +1393,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   }
 }
 
-int stem4d_col_w_max(int m) { return m - 2 * SK4C_PF - 2; }
+int stem4d_col_w_max(int m) { return m - SK4C_PF - kS4cV; }
 int stem4d_col_pf() { return SK4C_PF; }
 
 int stem4d_col_max_waves(int cpl) {

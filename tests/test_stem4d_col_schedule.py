@@ -319,16 +319,15 @@ def test_emulation_sees_a_broken_schedule():
 
 
 # the kernel's schedule (stem4d.hip sk_stem4d_col_kernel): rows PF = 1 ahead in
-# registers, no full barriers -- a global store is visible V = PF + 2 steps
-# later (the writer's in-order vmcnt wait for a load issued after it, PF
-# steps on, then a barrier; one step of margin) -- groups of at least
-# PF + V positions, wave 0's wrap rows staged PF + 1 steps ahead, and
-# W <= m - 2 PF - 2 (host: run_stem4d)
-KPF, KV, KNB = 1, 3, 4
+# registers, no full barriers -- a global store is visible V = 2 steps later
+# (the writer waits at the end of the next step for a load issued after it,
+# then a barrier) -- groups of at least PF + V positions, wave 0's wrap rows
+# staged PF + 1 steps ahead, and W <= m - PF - V (host: run_stem4d)
+KPF, KV, KNB = 1, 2, 4
 
 
-def kernel_w_max(m):
-    return max(1, m - 2 * KPF - 2)
+def kernel_w_max(m, pf=KPF):
+    return max(1, m - pf - KV)
 
 
 @pytest.mark.parametrize("n,m,W", [(9, 14, 4), (12, 17, 7), (13, 20, 10), (5, 30, 12), (17, 30, 8),
@@ -336,37 +335,36 @@ def kernel_w_max(m):
 @pytest.mark.parametrize("nb,pf", [(4, 1), (3, 1), (4, 2), (1, 4), (2, 4), (3, 4), (2, 3), (3, 2), (2, 2)])
 def test_kernel_schedule_equals_oracle(n, m, W, nb, pf):
     """(PF, NB) as the kernel's builds take them (SK4C_PF / SK4C_NB4): the
-    limits scale with PF (visibility PF + 2, groups of 2 PF + 2 positions,
-    W <= m - 2 PF - 2)."""
+    limits scale with PF (groups of PF + 2 positions, W <= m - PF - 2)."""
     x, bx, y, by = _case(n, m)
-    W = min(W, max(1, m - 2 * pf - 2))
-    got = emulate(x, bx, y, by, W, F=pf + 2, nb=nb, pf=pf, vis=pf + 2, zlead=pf + 1)
+    W = min(W, kernel_w_max(m, pf))
+    got = emulate(x, bx, y, by, W, F=KV, nb=nb, pf=pf, vis=KV, zlead=pf + 1)
     ref = _ref(x, bx, y, by)
     assert abs(got - ref) <= 1e-12 * abs(ref), (got, ref)
 
 
 def test_kernel_schedule_limits_have_teeth():
     """Two waves past the host's W limit (which keeps one wave of margin:
-    m - 2 PF - 1 is exact here), or a visibility lag longer than the schedule
+    m - PF - V + 1 is exact here), or a visibility lag longer than the schedule
     allows for, gives a wrong K."""
     x, bx, y, by = _case(17, 20)
     ref = _ref(x, bx, y, by)
     W = kernel_w_max(20)
     assert abs(emulate(x, bx, y, by, W, F=KV, nb=KNB, pf=KPF, vis=KV, zlead=KPF + 1) - ref) <= 1e-12 * ref
     bad = [emulate(x, bx, y, by, W + 2, F=KV, nb=KNB, pf=KPF, vis=KV, zlead=KPF + 1),
-           emulate(x, bx, y, by, W, F=KV + 2, nb=KNB, pf=KPF, vis=KV + 2, zlead=KPF + 1)]
+           emulate(x, bx, y, by, W, F=KV, nb=KNB, pf=KPF, vis=KV + 2, zlead=KPF + 1)]
     assert all(not abs(b - ref) <= 1e-12 * ref for b in bad), bad
 
 
 def test_library_col_shape_matches_schedule_limits():
     """The shipped library's column shape (sk_stem4d_col_shape, the bench's
     roofline input) carries the PF this file emulates, and W obeys
-    W <= m - 2 PF - 2 for the smallest stacking y of the batch."""
+    W <= m - PF - 2 for the smallest stacking y of the batch."""
     from stem_kernel_amd.kernel_matrix import stem4d_col_shape
     for lo, hi in [(200, 200), (5, 5), (12, 40), (100, 120), (10, 300)]:
         sh = stem4d_col_shape(lo, hi)
         assert sh["pf"] == KPF
-        assert 1 <= sh["waves"] <= max(1, lo - 2 * sh["pf"] - 2) or (lo - 2 * sh["pf"] - 2 < 1 and sh["waves"] == 1)
+        assert 1 <= sh["waves"] <= kernel_w_max(lo, sh["pf"])
         assert sh["waves"] <= 8
     assert stem4d_col_shape(200, 200)["nb"] == KNB
     assert stem4d_col_shape(10, 300)["nb"] == 1
