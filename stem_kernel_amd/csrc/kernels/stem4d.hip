@@ -1221,8 +1221,13 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     const Row& X = rq[0];
 #pragma unroll
     for (int c = 0; c < NS; ++c) {
-      A[c] = X.A[c];
-      bpd[c] = X.bp[c] > bound ? (double)X.bp[c] : 0.0;
+      // (explicit copies: the queue's registers end here, so the loads below
+      // can land in them; a renamed A would leave them live and the loads
+      // in other registers, copied -- and waited for -- at the loop latch)
+      asm volatile("v_mov_b64 %0, %1" : "=v"(A[c]) : "v"(X.A[c]));
+      float b;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(b) : "v"(X.bp[c]));
+      bpd[c] = b > bound ? (double)b : 0.0;
       yl[c] = ysl[lane + 64 * c + s - 1];
     }
     // the queue's row is in A / bpd now: with PF = 1 the next row's loads go

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r05n: fetch issued after the row prologue (PF 1), y tables shared: 4-D tests, C3, step-part cycles
+# r05n: column kernel variants: 4-D tests, C3, step-part cycles
 set -o pipefail
 TAG=${1:-r05n}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_stem4d.py tests/test_large_configs.py -m gpu -x -v --timeout 300 --timeout-method thread -k "stem4d" > $OUT/pytest_4d.log 2>&1 || { tail -30 $OUT/pytest_4d.log; exit 1; }
