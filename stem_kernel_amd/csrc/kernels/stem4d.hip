@@ -38,6 +38,18 @@ __device__ __forceinline__ double wave_shl1(double v, double high) {
   return __hiloint2double(rhi, rlo);
 }
 
+// lane l receives lane l+1's value of v, lane 63 lane 0's of `next` (the
+// slot after v's): lane 63's value comes by DPP wave_rol:1 of `next` and
+// stays where the wave_shl:1 of v has no source -- four DPP moves, no trip
+// through SGPRs (wave_shl1 with bcast_lane0(next) as `high`: six VALU)
+__device__ __forceinline__ double wave_shl1_next(double v, double next) {
+  const int nlo = __builtin_amdgcn_mov_dpp(__double2loint(next), 0x134, 0xf, 0xf, false);
+  const int nhi = __builtin_amdgcn_mov_dpp(__double2hiint(next), 0x134, 0xf, 0xf, false);
+  const int rlo = __builtin_amdgcn_update_dpp(nlo, __double2loint(v), 0x130, 0xf, 0xf, false);
+  const int rhi = __builtin_amdgcn_update_dpp(nhi, __double2hiint(v), 0x130, 0xf, 0xf, false);
+  return __hiloint2double(rhi, rlo);
+}
+
 __device__ __forceinline__ int pad4(int v) { return (v + 3) & ~3; }
 
 // read-only, wave-uniform global data through the constant address space
@@ -1256,10 +1268,10 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           // (k+1, l-1) (row s-2): the next lane's, or the next slot's lane 0
           // (slot c+1 not yet updated this row; past the row's slots, lanes
           // of no valid cell)
-          const double hg = c + 1 < CPL ? bcast_lane0(G3c[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
-          const double ha = c + 1 < CPL ? bcast_lane0(Am2[ch][c + 1 < CPL ? c + 1 : c]) : 0.0;
-          const double G3n = wave_shl1(G3c[ch][c], hg);
-          const double A2 = wave_shl1(Am2[ch][c], ha);
+          const double G3n = c + 1 < CPL ? wave_shl1_next(G3c[ch][c], G3c[ch][c + 1 < CPL ? c + 1 : c])
+                                         : wave_shl1(G3c[ch][c], 0.0);
+          const double A2 = c + 1 < CPL ? wave_shl1_next(Am2[ch][c], Am2[ch][c + 1 < CPL ? c + 1 : c])
+                                        : wave_shl1(Am2[ch][c], 0.0);
           const double bp_kl = bpd[c];
           const uint32_t y_l = yl[c];
           const bool mt = ((xk >> c) & 1u) && y_l == xcj && bp_kl != 0.0;
