@@ -67,15 +67,19 @@ PEAK_FP64_TFS = 78.6    # FP64 vector
 # the written Gram (in the plain sum the stem term is ~1e-32 of the string
 # term at L=200).  Same two DPs, plus a log epilogue in sk_combine_kernel.
 CONFIGS = {
-    "ns": dict(kernel="ss", cls="LSuStemStrKernel", n=4096, L=200, slices=48, cid=2, cpu_pairs=12288),
+    # NS: a step is 1/16 of the Gram (524k pairs): 206.2k / 206.1k pairs/s
+    # against 203.7k / 204.0k with 1/24 and 201.2k / 201.5k with 1/48 on one
+    # box (r05w: the class launches' fill and last round over more pairs);
+    # the whole Gram in one call (sk_gram_sharded, bench --full) 204.1k (r05r)
+    "ns": dict(kernel="ss", cls="LSuStemStrKernel", n=4096, L=200, slices=16, cid=2, cpu_pairs=12288),
     # C2's whole Gram is 32,896 pairs (0.2 s): a step is the whole Gram, the
     # unit the reference computes per call (kernel_matrix.cpp:485-575), not a
     # slice whose launch fill and tail would dominate ("whole": steps repeat it)
     "c2": dict(kernel="ss", n=256, L=150, slices=1, whole=True, cid=1, cpu_pairs=12288),
     # C3: 1,023 pairs per step, one workgroup per pair (LDS: one per CU), so
     # four rounds of 256 CUs: 591.8 / 755.2 / 759.5 pairs/s for 384 / 768 /
-    # 1,023 pairs on one box (r05j; 384 leaves half the CUs idle in its
-    # second round)
+    # 1,023 pairs on one box (r05j, an earlier column kernel; 384 leaves half
+    # the CUs idle in its second round)
     "c3": dict(kernel="stem4d", n=1024, L=200, slices=513, cid=2, cpu_pairs=32),
     # async: step t+1 planned while step t runs (sk_set_async): C4 +3.6 % (its
     # 7 ms steps had 0.6-0.9 ms host gaps); the DAG configs gain <1 % and
