@@ -79,6 +79,13 @@ variant:
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/host/svm_predict.o $(BUILD)/var/$(NAME)/sk_api.o $(BUILD)/var/$(NAME)/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/kernels/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 .PHONY: variant
 
+# fold kernel experiment build: make variantf NAME=x DEFS="-DSK_FOLD_TIMING" -> build/libsk_x.so
+variantf:
+	@mkdir -p $(BUILD)/var/$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/fold.hip -o $(BUILD)/var/$(NAME)/fold.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/host/svm_predict.o $(BUILD)/sk_api.o $(BUILD)/kernels/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/kernels/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/var/$(NAME)/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+.PHONY: variantf
+
 # 4-D kernel experiment build: make variant4 NAME=x DEFS="-DSK4_MINB=4" -> build/libsk_x.so
 variant4:
 	@mkdir -p $(BUILD)/var/$(NAME)

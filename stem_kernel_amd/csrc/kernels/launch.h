@@ -289,11 +289,19 @@ struct FoldLaunch {
   double log_sc = 0.0;            // ln of the per-nucleotide scale
   int32_t no_gu = 0, no_closing_gu = 0;
   const uint8_t* lp = nullptr;    // --noLonelyPairs pair filter (nullptr: off)
-  double* work = nullptr;
+  int32_t n_tab = 0, n_tab_pad = 0;  // table length (doubles), rounded up to 2 (LDS copy)
+  int32_t ring_n = 0;               // set by launch_fold: ring row length (0: no ring)
+  double* work = nullptr;           // per sequence 6 n^2 + 2 (n + 1) doubles (fold_work_doubles)
   double* out = nullptr;
   double* log_z = nullptr;        // per sequence of the launch (nullptr: not wanted)
 };
-hipError_t launch_fold(const FoldLaunch& P, int n_seqs, hipStream_t st);
+// the fold kernel keeps the interior-loop window of the inside / outside
+// tables in LDS for sequences up to this length (33 n doubles)
+constexpr int kFoldRingMaxN = 248;
+bool fold_ring(int max_n);
+size_t fold_lds_bytes(const FoldLaunch& P, int max_n);
+inline size_t fold_work_doubles(size_t n) { return 6 * n * n + 2 * (n + 1); }
+hipError_t launch_fold(const FoldLaunch& P, int n_seqs, int max_n, hipStream_t st);
 
 enum CombineMode : int32_t {
   kCombineStem = 0,      // K = stem

@@ -3787,6 +3787,8 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
   sk::FoldLaunch L;
   std::vector<double> tab;
   fold_tables(max_len, L, tab);
+  L.n_tab = (int32_t)tab.size();
+  L.n_tab_pad = (L.n_tab + 1) & ~1;
   L.no_gu = (flags & SK_FOLD_NO_GU) ? 1 : 0;
   L.no_closing_gu = (flags & SK_FOLD_NO_CLOSING_GU) ? 1 : 0;
   size_t free_b = 0, total_b = 0;
@@ -3801,9 +3803,10 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
     std::vector<uint8_t> lp;  // --noLonelyPairs tables
     size_t work = 0, outn = 0;
     int32_t b1 = b0;
+    int bmax = 0;
     for (; b1 < n; ++b1) {
       const size_t nn = (size_t)len[b1];
-      const size_t w = 10 * nn * nn + 2 * (nn + 1);
+      const size_t w = sk::fold_work_doubles(nn);
       if (!sq.empty() && (double)(work + w) * 8.0 > budget) break;
       sk::FoldSeq f;
       f.seq_off = (int64_t)codes.size();
@@ -3818,6 +3821,7 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
       }
       work += w;
       outn += nn > 1 ? nn * (nn - 1) / 2 : 0;
+      bmax = std::max(bmax, (int)nn);
       sq.push_back(f);
     }
     const int nb = b1 - b0;
@@ -3849,7 +3853,7 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
     L.work = ctx->scratch;
     L.out = d_out;
     L.log_z = d_lz;
-    SK_HIP(ctx, sk::launch_fold(L, nb, S));
+    SK_HIP(ctx, sk::launch_fold(L, nb, bmax, S));
     std::vector<double> lz(nb);
     if (outn) SK_HIP(ctx, hipMemcpyAsync(out + out_host, d_out, outn * 8, hipMemcpyDeviceToHost, S));
     SK_HIP(ctx, hipMemcpyAsync(lz.data(), d_lz, nb * 8, hipMemcpyDeviceToHost, S));
