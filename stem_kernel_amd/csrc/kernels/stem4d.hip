@@ -1244,7 +1244,9 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     }
     // the queue's row is in A / bpd now: with PF = 1 the next row's loads go
     // out here, into the same registers, a whole step ahead of their use
-    if constexpr (PF == 1) fetch_next(rq[0]);
+    // (not in the widest rows, where the registers they hold through the row
+    // are the kernel's peak: there the tail issues them)
+    if constexpr (PF == 1 && (NS < CPL || CPL < 4)) fetch_next(rq[0]);
     const uint32_t stk_mask = __builtin_amdgcn_readfirstlane(dc.stack);
     const int bch = BND ? __builtin_amdgcn_readfirstlane(dc.c0) : -1;
 #pragma unroll
@@ -1336,7 +1338,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           tm_a = tr;
         }
 #endif
-        tail(t, std::integral_constant<bool, PF == 1>());
+        tail(t, std::integral_constant<bool, PF == 1 && (NS < CPL || CPL < 4)>());
         ro += pad4(m + 1 - s);
       }
     };
