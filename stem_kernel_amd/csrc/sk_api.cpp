@@ -1861,9 +1861,10 @@ static int stem4d_dataset_tables(sk_context* ctx, sk_dataset* ds, const sk_kerne
     bpall.insert(bpall.end(), bp.begin(), bp.end());
     chall.insert(chall.end(), chr.begin(), chr.end());
   }
+  if (T.bp) SK_HIP(ctx, hipDeviceSynchronize());  // launches still reading the old tables
   T.bp = nullptr;
   T.ch = nullptr;
-  T.buf.release();  // (hipFree waits for the launches that read the old tables)
+  T.buf.release();
   SK_HIP(ctx, upload(T.buf, bpall, &T.bp));
   SK_HIP(ctx, upload(T.buf, chall, &T.ch));
   T.device = ctx->device;
