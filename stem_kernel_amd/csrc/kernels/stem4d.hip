@@ -869,6 +869,9 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 #define SK4C_PF 1
 #endif
 constexpr int kS4cV = 2;
+#ifndef SK4C_STAGE_IN_ROW  // row steps stage wave 0's wrap rows inside their first chain
+#define SK4C_STAGE_IN_ROW 1
+#endif
 #ifndef SK4C_NB4  // column-group width of the CPL 4 class (|y| 128..255)
 #define SK4C_NB4 4
 #endif
@@ -1180,23 +1183,45 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   // the row of step t + PF and wave 0's wrap rows of step t+PF+1 loaded, the
   // fence load
   // (FETCHED: a row step with PF = 1 issued the fetch after its prologue)
-  auto tail = [&](int t, auto fetched_tag) __attribute__((always_inline)) {
+  // (STAGED: a row step ran the staging part -- wave 0's wrap rows and the
+  // fence wait -- inside its first chain, where its scalar work interleaves
+  // with the chain's vector work: in the tail all waves reach it together,
+  // and the CU's one scalar unit serialises them)
+  auto stage = [&](int t) __attribute__((always_inline)) {
     if (yc.q.valid(n, NB)) {
       zstore(wst + (t & 1) * NB * TW, wrq[0]);
       cur_next(yc);
     }
     asm volatile("" ::"v"(fq));  // this wave's stores of step t-1 are complete
-    if constexpr (!decltype(fetched_tag)::value) {
-#pragma unroll
-      for (int q = 0; q + 1 < PF; ++q) rq[q] = rq[q + 1];
-      fetch_next(rq[PF - 1]);
-    }
 #pragma unroll
     for (int q = 0; q + 1 < PF; ++q)
 #pragma unroll
       for (int e = 0; e < SEGR; ++e) wrq[q][e] = wrq[q + 1][e];
     if (zc.q.valid(n, NB)) cur_next(zc);
     zload(wrq[PF - 1]);
+  };
+  auto tail = [&](int t, auto fetched_tag, auto staged_tag) __attribute__((always_inline)) {
+    constexpr bool STAGED = decltype(staged_tag)::value;
+    if constexpr (!STAGED) {
+      if (yc.q.valid(n, NB)) {
+        zstore(wst + (t & 1) * NB * TW, wrq[0]);
+        cur_next(yc);
+      }
+      asm volatile("" ::"v"(fq));  // this wave's stores of step t-1 are complete
+    }
+    if constexpr (!decltype(fetched_tag)::value) {
+#pragma unroll
+      for (int q = 0; q + 1 < PF; ++q) rq[q] = rq[q + 1];
+      fetch_next(rq[PF - 1]);
+    }
+    if constexpr (!STAGED) {
+#pragma unroll
+      for (int q = 0; q + 1 < PF; ++q)
+#pragma unroll
+        for (int e = 0; e < SEGR; ++e) wrq[q][e] = wrq[q + 1][e];
+      if (zc.q.valid(n, NB)) cur_next(zc);
+      zload(wrq[PF - 1]);
+    }
     fq = s4c_rld32(fence_buf, 0, lane);  // (lane 0 reads bpy[0], the rest nothing)
   };
 
@@ -1254,6 +1279,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       // (one chain at a time: the scheduler would otherwise hoist every
       // chain's LDS reads to the top, past the register budget)
       if (NB >= 4) __builtin_amdgcn_sched_barrier(0);
+      if (SK4C_STAGE_IN_ROW && ch == 0) stage(t);
       const bool bz = BND && ch == bch;  // G0(i, i) row and no G1
       const auto rw = s4c_rowbuf(wrapb + (int64_t)ch * cp + ro, LASTW ? nk : 0);
       if ((stk_mask >> ch) & 1u) {
@@ -1319,7 +1345,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   auto run = [&](auto last_tag) __attribute__((always_inline)) {
   for (; t < w && t < total; ++t) {  // before the wave's first position
     head(t);
-    tail(t, std::false_type());
+    tail(t, std::false_type(), std::false_type());
   }
   // a position's rows 1 .. m in phases of NS active slots, CPL down to 1
   auto rows = [&](auto bnd_tag) __attribute__((always_inline)) {
@@ -1338,7 +1364,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           tm_a = tr;
         }
 #endif
-        tail(t, std::integral_constant<bool, PF == 1 && (NS < CPL || CPL < 4)>());
+        tail(t, std::integral_constant<bool, PF == 1 && (NS < CPL || CPL < 4)>(),
+             std::integral_constant<bool, SK4C_STAGE_IN_ROW != 0>());
         ro += pad4(m + 1 - s);
       }
     };
@@ -1362,7 +1389,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     if (!dc.on) {  // a bubble
       for (int s = 0; s < R; ++s, ++t) {
         head(t);
-        tail(t, std::false_type());
+        tail(t, std::false_type(), std::false_type());
       }
     } else {
       head(t);  // row 0, cells (l, l): G0 = g^(j-i), never stored; the chains' registers reset
@@ -1378,7 +1405,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           Am2[ch][c] = G2c[ch][c] = G3c[ch][c] = 0.0;
         }
       }
-      tail(t, std::false_type());
+      tail(t, std::false_type(), std::false_type());
       ++t;
       if (dc.c0 >= 0) rows(std::true_type());
       else rows(std::false_type());
@@ -1392,7 +1419,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   }
   for (; t < total; ++t) {  // after the wave's last position
     head(t);
-    tail(t, std::false_type());
+    tail(t, std::false_type(), std::false_type());
   }
   };
   if (w + 1 == W) run(std::true_type());
