@@ -148,6 +148,25 @@ def test_stem4d_resident_tables_two_datasets(gpu_ctx):
         assert rel_err(got, ref) < TOL
 
 
+@pytest.mark.gpu
+def test_stem4d_col_cpl8_matches_oracle(gpu_ctx):
+    """The column kernel's widest class (CPL 8: 256 <= |y| < 512, one k
+    tile, NB 1) against the oracle: short x, long y (the oracle's cost is
+    |x|^2 |y|^2 / 4 cells), y's of different lengths in one batch (W from the
+    shortest)."""
+    xs = ska.random_sequences(2, 24, 0x5EED0061) + ["GGGCGCAAGCCU"]
+    ys = ska.random_sequences(1, 300, 0x5EED0062) + ska.random_sequences(1, 457, 0x5EED0063)
+    seqs = xs + ys
+    ds, _ = make_examples(seqs)
+    kern = ska.StemKernel4D(bp_model=2, bp_bound=0.3)
+    x = np.array([0, 1, 2, 0, 2], np.int32)
+    y = np.array([3, 3, 4, 4, 3], np.int32)
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    assert gpu_ctx.last_classes()["stem4d_col"] == [8]
+    ref = _oracle(seqs, kern, list(zip(x, y)))
+    assert rel_err(got, ref) < TOL
+
+
 def test_oracle_band_wide_equals_full_dp():
     """partial_dp with a band wider than both sequences computes every cell."""
     s = ska.random_sequences(3, 24, 21) + ska.random_sequences(1, 17, 22)
