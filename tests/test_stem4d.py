@@ -167,6 +167,24 @@ def test_stem4d_col_cpl8_matches_oracle(gpu_ctx):
     assert rel_err(got, ref) < TOL
 
 
+@pytest.mark.gpu
+def test_stem4d_short_y_limits(gpu_ctx):
+    """y lengths 2 .. 8 around the column kernel's limit W <= m - PF - 2: the
+    shortest go to the span kernel in batches of their own (run_stem4d), the
+    next run one to a few waves; every pair against the oracle."""
+    ys = ["GC", "GCU", "GGCC", "GAUCA", "GGAUCC", "GGGAUCC", "GCGAAAGC"]
+    xs = ska.random_sequences(3, 16, 0x5EED0071) + ["GGGGAAACCCC"]
+    seqs = xs + ys
+    ds, _ = make_examples(seqs)
+    kern = ska.StemKernel4D(bp_model=2, bp_bound=0.3)
+    pairs = [(a, len(xs) + b) for a in range(len(xs)) for b in range(len(ys))]
+    x = np.array([p[0] for p in pairs], np.int32)
+    y = np.array([p[1] for p in pairs], np.int32)
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    ref = _oracle(seqs, kern, pairs)
+    assert rel_err(got, ref) < TOL
+
+
 def test_oracle_band_wide_equals_full_dp():
     """partial_dp with a band wider than both sequences computes every cell."""
     s = ska.random_sequences(3, 24, 21) + ska.random_sequences(1, 17, 22)
