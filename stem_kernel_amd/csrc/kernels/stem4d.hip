@@ -830,41 +830,46 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 // pair (prob(i-1, j-1) <= bound) has G3 = G2 = 0 in every cell, so its chain
 // costs one FMA and one multiply per cell (stem_kernel.cpp:320-334).
 // Schedule (tests/test_stem4d_col_schedule.py emulates it step by step
-// against the oracle): group g holds c_g = max(j_hi, F + PF) positions (its
+// against the oracle): group g holds c_g = max(j_hi, PF + V) positions (its
 // planes, then bubbles); position p is wave p % W's plane of round p / W,
 // row s at step T(p) + s, T(p) = (p / W) R + p % W, R = m + 1 rows, one
-// workgroup barrier per step.  With R >= W + F + PF (the host's W), T is
-// increasing with T(p2) - T(p1) >= p2 - p1, so:
+// LDS-only workgroup barrier per step (lgkmcnt: only the LDS link rows must
+// be visible across it).  With W <= m - PF - V (the host's W; m - PF - V + 1
+// is exact in the emulator) T is increasing with T(p2) - T(p1) >= p2 - p1, so:
 //  * B' of row s is written by wave w-1 at step t-1 and read by wave w at
-//    step t (LDS slot t & 1), or, at the wrap, >= F + PF steps later;
+//    step t (LDS slot t & 1), or, at the wrap, >= PF + V steps later;
 //  * the A row that position (g, i) fetches PF rows ahead was written by
-//    position (g-1, i), >= c_{g-1} >= F + PF positions earlier;
+//    position (g-1, i), >= c_{g-1} >= PF + V positions earlier;
 //  * row 0 is never stored: G0(i, j, l, l) = g^(j-i), the repeated products
 //    of gap_powers, as the chain G0(i+1, j, l, l) g forms it (:313-317).
-// Barriers: between steps only the LDS B' rows must be visible, so a step
-// starts with an LDS-only barrier (lgkmcnt); every F-th is a full one (a
-// workgroup release of global memory), so a global store of step u is seen
-// from the first multiple of F above u on -- hence the F + PF lags.
+// Global visibility without full barriers: every step ends with a vector
+// load issued after its stores (the fence load), and the next step waits for
+// it (vmcnt counts loads and stores together, in issue order), so a store of
+// step u is complete when its wave ends step u + 1 and seen by the other
+// waves after the barrier of step u + 2: V = 2.
+// Wave 0's round-wrap rows (one plane per chain in HBM) are staged by all
+// waves: each loads its share of the (chain, slot) segments PF + 1 steps
+// ahead and writes it into an LDS staging slot the step before wave 0 reads
+// it -- in a row step inside the first chain, where the scalar work
+// interleaves with vector work (in the tail all waves reached it together and
+// the CU's one scalar unit serialised them).
 // The K chain is summed (sk_stem4d_gsum_kernel): each lane sums its sources
 // over every chain of every position, the waves' sums are added in wave
 // order.  Lanes past a row's end compute values that are never stored (the
 // range-checked buffers end at the row) nor read by a valid cell of a later
 // row (a cell reads k and k+1 of earlier rows, both valid there), and add
 // nothing to K (their bp loads return 0, and bound >= 0).
-// Rows fetched ahead (PF, in registers) and the visibility lag of a global
-// store (V steps).  There are no full barriers: every step ends with a
-// vector load issued after its stores (the fence load), and the next step's
-// tail waits for it (vmcnt counts loads and stores together, in issue order),
-// so a store of step u is complete when its wave ends step u + 1 and seen by
-// the other waves after the barrier of step u + 2: V = 2.  Hence groups of at
-// least PF + V positions and W <= m - PF - V (run_stem4d), which
-// tests/test_stem4d_col_schedule.py emulates step by step (m - PF - V + 1 is
-// exact there).  Every load of a step is issued whether its row exists or
-// not (a range-checked buffer of 0 bytes returns 0 without a memory access):
-// a load on one path only leaves a phi whose register copy waits for it.  PF = 1 with NB = 4
-// at CPL 4: C3 (1,024 x L200) A/B, pairs/s: PF 1 NB 4 698, PF 2 NB 3 677,
-// PF 1 NB 3 612, PF 4 NB 2 519 (wider groups halve the row traffic per
-// cell; the registers they take come out of the prefetch depth).
+// Every load of a step is issued whether its row exists or not (a
+// range-checked buffer of 0 bytes returns 0 without a memory access): a load
+// on one path only leaves a phi whose register copy waits for it, right where
+// the copy sits.  The next row is fetched (PF = 1) right after a row's
+// prologue, into the registers it just left -- but in the widest rows (NS =
+// CPL = 4) in the tail, where the early fetch held the kernel's peak
+// registers.  PF = 1 with NB = 4 at CPL 4 from the C3 (1,024 x L200) A/B,
+// pairs/s: PF 1 NB 4 698, PF 2 NB 3 677, PF 1 NB 3 612, PF 4 NB 2 519 on the
+// kernel of then (wider groups halve the row traffic per cell; the registers
+// they take come out of the prefetch depth); NB 3 1,106 against NB 4 1,306
+// on the final one.
 #ifndef SK4C_PF
 #define SK4C_PF 1
 #endif
