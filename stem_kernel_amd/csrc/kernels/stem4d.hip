@@ -1247,7 +1247,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   // row s >= 1 of the position: NS slots hold its cells (64 (NS-1) <= m - s
   // < 64 NS), chain by chain (one uniform branch per chain on its consumer's
   // stacking); BND: a boundary chain c0 (a top-triangle position)
-  auto row = [&](int t, int s, int ro, auto bnd_tag, auto ns_tag, auto last_tag) __attribute__((always_inline)) {
+  auto row = [&](int t, int s, int ro, int ye, const double* pbase, auto bnd_tag, auto ns_tag, auto last_tag)
+                 __attribute__((always_inline)) {
     constexpr bool BND = decltype(bnd_tag)::value;
     constexpr int NS = decltype(ns_tag)::value;
     // the last wave hands its B' rows on through the wrap planes, the others
@@ -1276,7 +1277,21 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     // out here, into the same registers, a whole step ahead of their use
     // (not in the widest rows, where the registers they hold through the row
     // are the kernel's peak: there the tail issues them)
-    if constexpr (PF == 1 && (NS < CPL || CPL < 4)) fetch_next(rq[0]);
+    // (the row is this position's s + 1, when s < m: its offsets follow from
+    // this row's, the plane's base is the position's -- no cursor arithmetic;
+    // the fetch cursor moves on all the same, for the steps that use it)
+    if constexpr (PF == 1 && (NS < CPL || CPL < 4)) {
+      const bool ld = s < m;
+      const int nk = ld ? m - s : 0;
+      const auto ra = s4c_rowbuf(pbase + (ld ? ro + pad4(m + 1 - s) : 0), nk);
+      const auto rb = s4c_rowbuf(bpy + (ld ? ye + m + 1 - s : 0), nk);
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        rq[0].A[c] = s4c_rld64(ra, c, lane);
+        rq[0].bp[c] = s4c_rld32(rb, c, lane);
+      }
+      cur_next(fc);
+    }
     const uint32_t stk_mask = __builtin_amdgcn_readfirstlane(dc.stack);
     const int bch = BND ? __builtin_amdgcn_readfirstlane(dc.c0) : -1;
 #pragma unroll
@@ -1354,13 +1369,14 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   }
   // a position's rows 1 .. m in phases of NS active slots, CPL down to 1
   auto rows = [&](auto bnd_tag) __attribute__((always_inline)) {
-    int s = 1, ro = pad4(m + 1);
+    int s = 1, ro = pad4(m + 1), ye = 0;
+    const double* pbase = planes + (int64_t)dc.i * cp;
     auto phase = [&](auto ns_tag) __attribute__((always_inline)) {
       constexpr int NS = decltype(ns_tag)::value;
       const int s_end = NS > 1 ? m - 64 * (NS - 1) : m;
       for (; s <= s_end; ++s, ++t) {
         head(t);
-        row(t, s, ro, bnd_tag, ns_tag, last_tag);
+        row(t, s, ro, ye, pbase, bnd_tag, ns_tag, last_tag);
 #ifdef SK4C_TIMING
         {
           uint64_t tr;
@@ -1372,6 +1388,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
         tail(t, std::integral_constant<bool, PF == 1 && (NS < CPL || CPL < 4)>(),
              std::integral_constant<bool, SK4C_STAGE_IN_ROW != 0>());
         ro += pad4(m + 1 - s);
+        ye += m + 1 - s;
       }
     };
     if constexpr (CPL >= 8) {
