@@ -1279,7 +1279,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     // are the kernel's peak: there the tail issues them)
     // (the row is this position's s + 1, when s < m: its offsets follow from
     // this row's, the plane's base is the position's -- no cursor arithmetic;
-    // the fetch cursor moves on all the same, for the steps that use it)
+    // the fetch cursor stands still, and the position's end sets it again)
     if constexpr (PF == 1 && (NS < CPL || CPL < 4)) {
       const bool ld = s < m;
       const int nk = ld ? m - s : 0;
@@ -1290,7 +1290,6 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
         rq[0].A[c] = s4c_rld64(ra, c, lane);
         rq[0].bp[c] = s4c_rld32(rb, c, lane);
       }
-      cur_next(fc);
     }
     const uint32_t stk_mask = __builtin_amdgcn_readfirstlane(dc.stack);
     const int bch = BND ? __builtin_amdgcn_readfirstlane(dc.c0) : -1;
@@ -1435,6 +1434,17 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       for (int ch = 0; ch < NB; ++ch) {  // the position's sources: times stack * bp(i-1, j-1)
         ksrc += kacc[ch] * (P.stack * (double)dc.bpc[ch]);
         kacc[ch] = 0.0;
+      }
+      // the fetch cursor resumes at the next position's row 1, which that
+      // position's first step fetches (the row steps fetched without it)
+      if constexpr (PF == 1) {
+        fc.q = cur;
+        fc.q.advance(W, n, NB, FP);
+        fc.i = __builtin_amdgcn_readfirstlane(pos_of(fc.q, fc.on));
+        fc.s = 1;
+        fc.ro = pad4(m + 1);
+        fc.ye = 0;
+        fdelay = 0;
       }
     }
     cur.advance(W, n, NB, FP);
