@@ -1098,7 +1098,8 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   // segments (chain, slot) w, w + W, ... of wave 0's rows of step u are
   // loaded at step u - PF - 1, written to wst[(u - 1) & 1] at step u-1 (the
   // slot a link of step u-1 takes) and read by wave 0 at step u after the
-  // barrier.  zc: the rows of the last staging load, yc: of the next store.
+  // barrier.  zc: the rows of the last staging load, yc: of the next store
+  // (with PF = 1 the same rows: zc serves both, and yc is dead).
   Cur zc, yc;
   cur_init(zc, 0);
   cur_init(yc, 0);
@@ -1119,7 +1120,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       wr[q] = s4c_rld64(s4c_rowbuf(wrapb + (int64_t)(ch < NB ? ch : 0) * cp + ro, sg < NSEG ? nk : 0), c % CPL, lane);
     }
   };
-  auto zstore = [&](double* dst, const double (&wr)[SEGR]) __attribute__((always_inline)) {
+  auto zstore = [&](double* dst, const double (&wr)[SEGR], const Cur& yc) __attribute__((always_inline)) {
     if (!yc.on || yc.s == 0) return;
 #pragma unroll
     for (int q = 0; q < SEGR; ++q) {
@@ -1193,8 +1194,10 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   // with the chain's vector work: in the tail all waves reach it together,
   // and the CU's one scalar unit serialises them)
   auto stage = [&](int t) __attribute__((always_inline)) {
-    if (yc.q.valid(n, NB)) {
-      zstore(wst + (t & 1) * NB * TW, wrq[0]);
+    if constexpr (PF == 1) {
+      if (zc.q.valid(n, NB)) zstore(wst + (t & 1) * NB * TW, wrq[0], zc);
+    } else if (yc.q.valid(n, NB)) {
+      zstore(wst + (t & 1) * NB * TW, wrq[0], yc);
       cur_next(yc);
     }
     asm volatile("" ::"v"(fq));  // this wave's stores of step t-1 are complete
@@ -1208,8 +1211,10 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   auto tail = [&](int t, auto fetched_tag, auto staged_tag) __attribute__((always_inline)) {
     constexpr bool STAGED = decltype(staged_tag)::value;
     if constexpr (!STAGED) {
-      if (yc.q.valid(n, NB)) {
-        zstore(wst + (t & 1) * NB * TW, wrq[0]);
+      if constexpr (PF == 1) {
+        if (zc.q.valid(n, NB)) zstore(wst + (t & 1) * NB * TW, wrq[0], zc);
+      } else if (yc.q.valid(n, NB)) {
+        zstore(wst + (t & 1) * NB * TW, wrq[0], yc);
         cur_next(yc);
       }
       asm volatile("" ::"v"(fq));  // this wave's stores of step t-1 are complete
