@@ -38,6 +38,14 @@ __device__ __forceinline__ double wave_shl1(double v, double high) {
   return __hiloint2double(rhi, rlo);
 }
 
+// lane l receives lane l+1's value of v, lane 63 zero (DPP bound_ctrl): two
+// moves, for a slot whose lane 63 holds no valid cell
+__device__ __forceinline__ double wave_shl1_z(double v) {
+  const int rlo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
+  const int rhi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
+  return __hiloint2double(rhi, rlo);
+}
+
 // lane l receives lane l+1's value of v, lane 63 lane 0's of `next` (the
 // slot after v's): lane 63's value comes by DPP wave_rol:1 of `next` and
 // stays where the wave_shl:1 of v has no source -- four DPP moves, no trip
@@ -1250,7 +1258,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   Plane dc;
 
   // row s >= 1 of the position: NS slots hold its cells (64 (NS-1) <= m - s
-  // < 64 NS), chain by chain (one uniform branch per chain on its consumer's
+  // + 1 < 64 NS), chain by chain (one uniform branch per chain on its consumer's
   // stacking); BND: a boundary chain c0 (a top-triangle position)
   auto row = [&](int t, int s, int ro, int ye, const double* pbase, auto bnd_tag, auto ns_tag, auto last_tag)
                  __attribute__((always_inline)) {
@@ -1318,12 +1326,13 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           G0 += G1;
           // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
           // (k+1, l-1) (row s-2): the next lane's, or the next slot's lane 0
-          // (slot c+1 not yet updated this row; past the row's slots, lanes
-          // of no valid cell)
-          const double G3n = c + 1 < CPL ? wave_shl1_next(G3c[ch][c], G3c[ch][c + 1 < CPL ? c + 1 : c])
-                                         : wave_shl1(G3c[ch][c], 0.0);
-          const double A2 = c + 1 < CPL ? wave_shl1_next(Am2[ch][c], Am2[ch][c + 1 < CPL ? c + 1 : c])
-                                        : wave_shl1(Am2[ch][c], 0.0);
+          // (slot c+1 not yet updated this row); the phase's last slot has
+          // no valid cell in lane 63 (a phase's rows hold < 64 NS cells), so
+          // nothing comes from the slot after it
+          const double G3n = c + 1 < NS ? wave_shl1_next(G3c[ch][c], G3c[ch][c + 1 < CPL ? c + 1 : c])
+                                        : wave_shl1_z(G3c[ch][c]);
+          const double A2 = c + 1 < NS ? wave_shl1_next(Am2[ch][c], Am2[ch][c + 1 < CPL ? c + 1 : c])
+                                       : wave_shl1_z(Am2[ch][c]);
           const double bp_kl = bpd[c];
           const uint32_t y_l = yl[c];
           const bool mt = ((xk >> c) & 1u) && y_l == xcj && bp_kl != 0.0;
@@ -1371,13 +1380,15 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     head(t);
     tail(t, std::false_type(), std::false_type());
   }
-  // a position's rows 1 .. m in phases of NS active slots, CPL down to 1
+  // a position's rows 1 .. m in phases of NS active slots, CPL down to 1:
+  // phase NS takes the rows of 64 (NS-1) .. 64 NS - 1 cells (m - s + 1), so
+  // lane 63 of its last slot never holds a valid cell (m < 64 CPL)
   auto rows = [&](auto bnd_tag) __attribute__((always_inline)) {
     int s = 1, ro = pad4(m + 1), ye = 0;
     const double* pbase = planes + (int64_t)dc.i * cp;
     auto phase = [&](auto ns_tag) __attribute__((always_inline)) {
       constexpr int NS = decltype(ns_tag)::value;
-      const int s_end = NS > 1 ? m - 64 * (NS - 1) : m;
+      const int s_end = NS > 1 ? m + 1 - 64 * (NS - 1) : m;
       for (; s <= s_end; ++s, ++t) {
         head(t);
         row(t, s, ro, ye, pbase, bnd_tag, ns_tag, last_tag);
