@@ -1306,6 +1306,19 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     }
     const uint32_t stk_mask = __builtin_amdgcn_readfirstlane(dc.stack);
     const int bch = BND ? __builtin_amdgcn_readfirstlane(dc.c0) : -1;
+    // the B' rows from the neighbour (G1), every chain's at once: a chain
+    // whose consumer does not stack (most of them) is a few VALU after its
+    // read, so reads issued chain by chain leave one LDS round trip per
+    // chain exposed.  Not in the widest phase, whose registers are the
+    // kernel's peak (there each chain reads its own)
+    constexpr bool HOIST = NB >= 2 && NB * NS <= 12 && (NS < CPL || CPL <= 2);
+    double G1h[NB][HOIST ? NS : 1];
+    if constexpr (HOIST) {
+#pragma unroll
+      for (int ch = 0; ch < NB; ++ch)
+#pragma unroll
+        for (int c = 0; c < NS; ++c) G1h[ch][c] = lin[ch * TW + lane + 64 * c];
+    }
 #pragma unroll
     for (int ch = 0; ch < NB; ++ch) {
       // (one chain at a time: the scheduler would otherwise hoist every
@@ -1321,7 +1334,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           const int k = lane + 64 * c;
           double G1 = 0.0;
           if (bz) A[c] = gs;
-          else G1 = lin[ch * TW + k];
+          else G1 = HOIST ? G1h[ch][HOIST ? c : 0] : lin[ch * TW + k];
           double G0 = A[c] * gv;
           G0 += G1;
           // the consumer's G3 at (k+1, l) (row s-1) and G0(i, j-1) at
@@ -1359,7 +1372,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
           const int k = lane + 64 * c;
           double G1 = 0.0;
           if (bz) A[c] = gs;
-          else G1 = lin[ch * TW + k];
+          else G1 = HOIST ? G1h[ch][HOIST ? c : 0] : lin[ch * TW + k];
           double G0 = A[c] * gv;
           G0 += G1;
           const double Bn = G1 * gv;
