@@ -1327,7 +1327,48 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       if (SK4C_STAGE_IN_ROW && ch == 0) stage(t);
       const bool bz = BND && ch == bch;  // G0(i, i) row and no G1
       const auto rw = s4c_rowbuf(wrapb + (int64_t)ch * cp + ro, LASTW ? nk : 0);
-      if ((stk_mask >> ch) & 1u) {
+      if constexpr (HOIST) {
+        // the part every chain runs, then the stacking consumer's terms in
+        // one branch without an else (a non-stacking chain: G0, B' and the
+        // store; an if / else costs two branches and its phi copies)
+        double G0v[NS], Bnv[NS];
+#pragma unroll
+        for (int c = 0; c < NS; ++c) {
+          double G1 = 0.0;
+          if (bz) A[c] = gs;
+          else G1 = G1h[ch][HOIST ? c : 0];
+          G0v[c] = A[c] * gv + G1;
+          Bnv[c] = G1 * gv;
+        }
+        if ((stk_mask >> ch) & 1u) {
+          const uint32_t xcj = (dc.xcj >> (8 * ch)) & 0xffu;
+#pragma unroll
+          for (int c = 0; c < NS; ++c) {
+            const double G3n = c + 1 < NS ? wave_shl1_next(G3c[ch][c], G3c[ch][c + 1 < CPL ? c + 1 : c])
+                                          : wave_shl1_z(G3c[ch][c]);
+            const double A2 = c + 1 < NS ? wave_shl1_next(Am2[ch][c], Am2[ch][c + 1 < CPL ? c + 1 : c])
+                                         : wave_shl1_z(Am2[ch][c]);
+            const double bp_kl = bpd[c];
+            const bool mt = ((xk >> c) & 1u) && yl[c] == xcj && bp_kl != 0.0;
+            kacc[ch] += A2 * bp_kl * (mt ? 1.0 : subv);
+            double g3 = G3n * gv;
+            g3 += mt ? A2 : 0.0;
+            double g2 = G2c[ch][c] * gv;
+            g2 += g3;
+            Bnv[c] += g2;
+            G2c[ch][c] = g2;
+            G3c[ch][c] = g3;
+            Am2[ch][c] = Am1[ch][c];
+            Am1[ch][c] = A[c];
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < NS; ++c) {
+          if (LASTW) s4c_rst64(rw, c, lane, Bnv[c]);
+          else lout[ch * TW + lane + 64 * c] = Bnv[c];
+          A[c] = G0v[c];
+        }
+      } else if ((stk_mask >> ch) & 1u) {
         const uint32_t xcj = (dc.xcj >> (8 * ch)) & 0xffu;
 #pragma unroll
         for (int c = 0; c < NS; ++c) {
