@@ -938,6 +938,29 @@ __device__ __forceinline__ float s4c_rld32(__amdgpu_buffer_rsrc_t r, int c, int 
 __device__ __forceinline__ void s4c_rst64(__amdgpu_buffer_rsrc_t r, int c, int lane, double v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, v), r, (lane + 64 * c) * 8, 0, 0);
 }
+// the same row as a window [off, off + nk) of a buffer whose base does not
+// move from row to row: the range check covers voffset + soffset (gfx950,
+// tools/calib/buf_soffset.hip), so records = off + nk and soffset = off
+// bound the row exactly -- two scalar shifts per row instead of a 64-bit
+// base address and its descriptor words
+struct S4cWin {
+  __amdgpu_buffer_rsrc_t r;
+  int so;
+};
+template <class T>
+__device__ __forceinline__ S4cWin s4c_win(const T* base, int off, int nk) {
+  return {s4c_rsrc(base, __builtin_amdgcn_readfirstlane((off + nk) * (int)sizeof(T))),
+          __builtin_amdgcn_readfirstlane(off * (int)sizeof(T))};
+}
+__device__ __forceinline__ double s4c_rld64(S4cWin w, int c, int lane) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(w.r, (lane + 64 * c) * 8, w.so, 0));
+}
+__device__ __forceinline__ float s4c_rld32(S4cWin w, int c, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(w.r, (lane + 64 * c) * 4, w.so, 0));
+}
+__device__ __forceinline__ void s4c_rst64(S4cWin w, int c, int lane, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(s4c_u32x2, v), w.r, (lane + 64 * c) * 8, w.so, 0);
+}
 
 template <int CPL>
 __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kernel(Stem4dLaunch P) {
@@ -1125,9 +1148,11 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     for (int q = 0; q < SEGR; ++q) {
       const int sg = w + q * W, ch = sg / CPL, c = sg % CPL;
       // (sg >= NSEG: wave w has no q-th segment -- W > NSEG / SEGR -- nothing to load)
-      wr[q] = s4c_rld64(s4c_rowbuf(wrapb + (int64_t)(ch < NB ? ch : 0) * cp + ro, sg < NSEG ? nk : 0), c % CPL, lane);
+      wr[q] = s4c_rld64(s4c_win(wrapb + (int64_t)(ch < NB ? ch : 0) * cp, ro, sg < NSEG ? nk : 0), c % CPL, lane);
     }
   };
+  // (segments past this wave's SEGR: only with few waves; one flag)
+  const bool zrest = __builtin_amdgcn_readfirstlane(w + SEGR * W < NSEG ? 1 : 0) != 0;
   auto zstore = [&](double* dst, const double (&wr)[SEGR], const Cur& yc) __attribute__((always_inline)) {
     if (!yc.on || yc.s == 0) return;
 #pragma unroll
@@ -1135,11 +1160,11 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       const int sg = w + q * W, ch = sg / CPL, c = sg % CPL;
       if (sg < NSEG) dst[ch * TW + 64 * c + lane] = wr[q];
     }
-    if (SEGR * W < NSEG) {  // few waves (short y): the rest loaded here
+    if (zrest) {  // few waves (short y): the rest loaded here
       const int nk = m - yc.s + 1;
       for (int sg = w + SEGR * W; sg < NSEG; sg += W) {
         const int ch = sg / CPL, c = sg % CPL;
-        dst[ch * TW + 64 * c + lane] = s4c_rld64(s4c_rowbuf(wrapb + (int64_t)ch * cp + yc.ro, nk), c, lane);
+        dst[ch * TW + 64 * c + lane] = s4c_rld64(s4c_win(wrapb + (int64_t)ch * cp, yc.ro, nk), c, lane);
       }
     }
   };
@@ -1294,10 +1319,10 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
     // this row's, the plane's base is the position's -- no cursor arithmetic;
     // the fetch cursor stands still, and the position's end sets it again)
     if constexpr (PF == 1 && (NS < CPL || CPL < 4)) {
-      const bool ld = s < m;
-      const int nk = ld ? m - s : 0;
-      const auto ra = s4c_rowbuf(pbase + (ld ? ro + pad4(m + 1 - s) : 0), nk);
-      const auto rb = s4c_rowbuf(bpy + (ld ? ye + m + 1 - s : 0), nk);
+      // (at s = m the window is empty: nothing is read)
+      const int nk = m - s;
+      const auto ra = s4c_win(pbase, ro + pad4(m + 1 - s), nk);
+      const auto rb = s4c_win(bpy, ye + m + 1 - s, nk);
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         rq[0].A[c] = s4c_rld64(ra, c, lane);
@@ -1326,7 +1351,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
       if (NB >= 4) __builtin_amdgcn_sched_barrier(0);
       if (SK4C_STAGE_IN_ROW && ch == 0) stage(t);
       const bool bz = BND && ch == bch;  // G0(i, i) row and no G1
-      const auto rw = s4c_rowbuf(wrapb + (int64_t)ch * cp + ro, LASTW ? nk : 0);
+      const auto rw = s4c_win(wrapb + (int64_t)ch * cp, ro, LASTW ? nk : 0);
       if constexpr (HOIST) {
         // the part every chain runs, then the stacking consumer's terms in
         // one branch without an else (a non-stacking chain: G0, B' and the
@@ -1423,7 +1448,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
         }
       }
     }
-    const auto rg = s4c_rowbuf(planes + (int64_t)dc.i * cp + ro, nk);
+    const auto rg = s4c_win(pbase, ro, nk);
 #pragma unroll
     for (int c = 0; c < NS; ++c) s4c_rst64(rg, c, lane, A[c]);  // the last chain's G0 (i, j_hi)
   };
