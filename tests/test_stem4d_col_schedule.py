@@ -368,3 +368,35 @@ def test_library_col_shape_matches_schedule_limits():
         assert sh["waves"] <= 8
     assert stem4d_col_shape(200, 200)["nb"] == KNB
     assert stem4d_col_shape(10, 300)["nb"] == 1
+
+
+def _col_cpl(m):
+    # the column kernel's class for |y| = m (sk_api.cpp: |y| < 64, 128, 256, 512)
+    return next(c for c in (1, 2, 4, 8) if m < 64 * c)
+
+
+def _phases(m, cpl):
+    # stem4d.hip rows(): phase NS runs s .. s_end(NS), s_end = m + 1 - 64 (NS - 1)
+    # for NS > 1 and m for NS = 1, from CPL down to 1 (row s holds m - s + 1 cells)
+    out, s = [], 1
+    for ns in [c for c in (8, 7, 6, 5, 4, 3, 2, 1) if c <= cpl]:
+        s_end = m + 1 - 64 * (ns - 1) if ns > 1 else m
+        while s <= s_end:
+            out.append((s, ns))
+            s += 1
+    return out
+
+
+def test_phase_rows_leave_lane_63_of_the_last_slot_empty():
+    """Every row 1..m runs in exactly one phase; phase NS's rows hold
+    64 (NS-1) .. 64 NS - 1 cells (NS slots suffice, and lane 63 of the last
+    slot is never a valid cell, so its lane shift takes nothing from the slot
+    past it: wave_shl1_z in stem4d.hip)."""
+    for m in range(1, 512):
+        cpl = _col_cpl(m)
+        rows = _phases(m, cpl)
+        assert [s for s, _ in rows] == list(range(1, m + 1)), m
+        for s, ns in rows:
+            nk = m - s + 1
+            assert 1 <= nk <= 64 * ns - 1, (m, s, ns)
+            assert ns == 1 or nk >= 64 * (ns - 1), (m, s, ns)
