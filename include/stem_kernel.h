@@ -421,10 +421,12 @@ int sk_sync_timing(sk_context *ctx);
  * lane), shifted by 4 for the banded (partial_dp) variant and by 8 for the
  * column-pipelined full_dp kernel. */
 int sk_last_classes(const sk_context *ctx, uint32_t *stem_maxk_mask, uint32_t *stem4d_mask);
-/* Shape the column-pipelined 4-D kernel takes for a full_dp batch of y
- * examples of lengths [min_len, max_len], max_len < 512 (longer y's run the
- * k-tiled span kernel): *nb chained columns per group, *waves waves per pair,
- * *pf rows fetched ahead per wave (diagnostic; bench roofline). */
+/* Shape the column-pipelined 4-D kernel takes for a full_dp Gram batch whose
+ * x and y examples have lengths [min_len, max_len]: *nb chained columns per
+ * group, *waves waves per pair, *pf rows fetched ahead per wave (diagnostic;
+ * bench roofline).  *waves = 0 when that batch does not run on the column
+ * kernel: max_len >= 512 (k-tiled span kernel), max_len over the column
+ * kernel's x limit (2,048), or min_len too short for the column schedule. */
 int sk_stem4d_col_shape(int32_t min_len, int32_t max_len, int32_t *nb, int32_t *waves, int32_t *pf);
 /* RIBOSUM85-60 tables as compiled into the library (pinning tests). */
 void sk_ribosum_tables(float *s16, float *p256);

@@ -90,7 +90,10 @@ __device__ __forceinline__ int team_of(int ncell, int nt) {
 constexpr int kFoldRing = 33;  // 31 diagonals read + the one written, distinct slots
 
 // 512 threads (8 waves; 94 VGPRs: two workgroups per CU by LDS at L = 200)
-template <bool RING>
+// GTAB: the hairpin and scale tables (the tail of P.tab, sized by the
+// batch's longest sequence) are read from HBM, only the fixed-size head sits
+// in LDS -- long sequences, whose tables would not fit beside the codes
+template <bool RING, bool GTAB>
 __global__ void __launch_bounds__(512) sk_fold_kernel(FoldLaunch P) {
   extern __shared__ __attribute__((aligned(16))) double fsm[];
   __shared__ double red[8];
@@ -103,19 +106,20 @@ __global__ void __launch_bounds__(512) sk_fold_kernel(FoldLaunch P) {
   double *Q5 = W + 6 * N2, *H5 = Q5 + n + 1;
   // LDS: the Boltzmann tables, the ring (RING), the codes
   double* tl = fsm;
-  double* ring = tl + P.n_tab_pad;
+  const int n_lds = GTAB ? P.n_small : P.n_tab;  // table entries copied to LDS
+  double* ring = tl + ((n_lds + 1) & ~1);
   int8_t* c = reinterpret_cast<int8_t*>(ring + (RING ? kFoldRing * P.ring_n : 0));
-  for (int k = tid; k < P.n_tab; k += nt) tl[k] = P.tab[k];
+  for (int k = tid; k < n_lds; k += nt) tl[k] = P.tab[k];
   for (int k = tid; k < n; k += nt) c[k] = P.codes[sq.seq_off + k];
   __syncthreads();
   FoldTables T;
   T.st = tl + P.o_st;
-  T.hp = tl + P.o_hp;
+  T.hp = GTAB ? P.tab + P.o_hp : tl + P.o_hp;
   T.bu = tl + P.o_bu;
   T.in = tl + P.o_in;
   T.ni = tl + P.o_ni;
   T.au = tl + P.o_au;
-  T.scp = tl + P.o_scp;
+  T.scp = GTAB ? P.tab + P.o_scp : tl + P.o_scp;
   T.mlc = tl[P.o_ml];
   T.mli = tl[P.o_ml + 1];
   const double* scp = T.scp;
@@ -328,30 +332,38 @@ __global__ void __launch_bounds__(512) sk_fold_kernel(FoldLaunch P) {
 #endif
 }
 
-size_t fold_lds_bytes(const FoldLaunch& P, int max_n) {
+static size_t fold_lds_bytes_t(const FoldLaunch& P, int max_n, bool gtab) {
   const bool ring = fold_ring(max_n);
-  return ((size_t)P.n_tab_pad + (ring ? (size_t)kFoldRing * max_n : 0)) * 8 + (size_t)(max_n + 15) / 16 * 16;
+  const size_t ntab = gtab ? (size_t)((P.n_small + 1) & ~1) : (size_t)P.n_tab_pad;
+  return (ntab + (ring ? (size_t)kFoldRing * max_n : 0)) * 8 + (size_t)(max_n + 15) / 16 * 16;
+}
+
+bool fold_gtab(const FoldLaunch& P, int max_n) { return fold_lds_bytes_t(P, max_n, false) > kFoldLdsMax; }
+
+size_t fold_lds_bytes(const FoldLaunch& P, int max_n) {
+  return fold_lds_bytes_t(P, max_n, fold_gtab(P, max_n));
 }
 
 bool fold_ring(int max_n) { return max_n <= kFoldRingMaxN; }
+
+template <bool RING, bool GTAB>
+static hipError_t launch_fold_t(const FoldLaunch& P, int n_seqs, size_t lds, hipStream_t st) {
+  hipError_t e = hipFuncSetAttribute((const void*)sk_fold_kernel<RING, GTAB>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((sk_fold_kernel<RING, GTAB>), dim3(n_seqs), dim3(512), lds, st, P);
+  return hipGetLastError();
+}
 
 hipError_t launch_fold(const FoldLaunch& P0, int n_seqs, int max_n, hipStream_t st) {
   if (n_seqs <= 0) return hipSuccess;
   FoldLaunch P = P0;
   P.ring_n = fold_ring(max_n) ? max_n : 0;
   const size_t lds = fold_lds_bytes(P, max_n);
-  if (fold_ring(max_n)) {
-    hipError_t e = hipFuncSetAttribute((const void*)sk_fold_kernel<true>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(sk_fold_kernel<true>, dim3(n_seqs), dim3(512), lds, st, P);
-  } else {
-    hipError_t e = hipFuncSetAttribute((const void*)sk_fold_kernel<false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(sk_fold_kernel<false>, dim3(n_seqs), dim3(512), lds, st, P);
-  }
-  return hipGetLastError();
+  if (lds > kFoldLdsMax) return hipErrorInvalidValue;
+  if (fold_ring(max_n)) return launch_fold_t<true, false>(P, n_seqs, lds, st);  // (tables always fit)
+  return fold_gtab(P, max_n) ? launch_fold_t<false, true>(P, n_seqs, lds, st)
+                             : launch_fold_t<false, false>(P, n_seqs, lds, st);
 }
 
 }  // namespace sk

@@ -244,15 +244,17 @@ hipError_t launch_stem4d(const Stem4dLaunch& P, int cpl, hipStream_t st);
 // full_dp, column groups (stem4d.hip sk_stem4d_col_kernel): one workgroup of
 // `waves` waves per pair (pairs[0..n_pairs)); per pair n planes of
 // plane_doubles (G0) and stem4d_col_nb(cpl) B' planes (the round wrap) at
-// scratch_off; |y| < 512, and waves <= stem4d_col_w_max(m) for every pair
-// with m >= 2 (pairs with m <= 1 have K = 1 and take any waves)
+// scratch_off; |y| < 512, |x| <= stem4d_col_max_n(), and waves <=
+// stem4d_col_w_max(m) for every pair with m >= 2 (pairs with m <= 1 have K = 1
+// and take any waves); the LDS holds the batch's longest y and x
 int stem4d_col_w_max(int m);
+int stem4d_col_max_n();
 int stem4d_col_pf();  // rows fetched ahead per wave (SK4C_PF)
 int stem4d_col_nb(int cpl);
-size_t stem4d_col_lds_bytes(int cpl, int waves, int max_m);
+size_t stem4d_col_lds_bytes(int cpl, int waves, int max_m, int max_n);
 int stem4d_col_max_waves(int cpl);
 hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves, int max_m,
-                             hipStream_t st);
+                             int max_n, hipStream_t st);
 
 // PairHMM alignment constraints of a 4-D batch (-a, stem_kernel.cpp:14-81):
 // one wavefront per pair writes c_low/c_high (n+1 each at pair.band_off).
@@ -290,6 +292,7 @@ struct FoldLaunch {
   int32_t no_gu = 0, no_closing_gu = 0;
   const uint8_t* lp = nullptr;    // --noLonelyPairs pair filter (nullptr: off)
   int32_t n_tab = 0, n_tab_pad = 0;  // table length (doubles), rounded up to 2 (LDS copy)
+  int32_t n_small = 0;              // the fixed-size head of the tables (o_st .. o_ml)
   int32_t ring_n = 0;               // set by launch_fold: ring row length (0: no ring)
   double* work = nullptr;           // per sequence 6 n^2 + 2 (n + 1) doubles (fold_work_doubles)
   double* out = nullptr;
@@ -298,7 +301,12 @@ struct FoldLaunch {
 // the fold kernel keeps the interior-loop window of the inside / outside
 // tables in LDS for sequences up to this length (33 n doubles)
 constexpr int kFoldRingMaxN = 248;
+// dynamic LDS a fold launch may take (160 KB less the kernel's static block sums)
+constexpr size_t kFoldLdsMax = 163840 - 256;
 bool fold_ring(int max_n);
+// whether a launch keeps the hairpin / scale tables in HBM (they and the ring
+// and codes would not fit the LDS)
+bool fold_gtab(const FoldLaunch& P, int max_n);
 size_t fold_lds_bytes(const FoldLaunch& P, int max_n);
 inline size_t fold_work_doubles(size_t n) { return 6 * n * n + 2 * (n + 1); }
 hipError_t launch_fold(const FoldLaunch& P, int n_seqs, int max_n, hipStream_t st);

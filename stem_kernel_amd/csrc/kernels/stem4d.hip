@@ -23,6 +23,7 @@
 // Per pair, a ring of three span buffers of n+1 planes each.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "device_set.h"
@@ -882,6 +883,11 @@ __global__ void __launch_bounds__(256) SK4P_ATTR sk_stem4d_pre_kernel(Stem4dLaun
 #define SK4C_PF 1
 #endif
 constexpr int kS4cV = 2;
+// longest x of the column kernel: its x characters sit in LDS (sized per
+// launch from the batch's longest x), and with |x| <= 2,048 and |y| < 512 the
+// step count fits an int for any W >= 1 (sum of group lengths <= 2.1M
+// positions, times R <= 512); longer x go to the span kernels
+constexpr int kS4cMaxN = 2048;
 #ifndef SK4C_STAGE_IN_ROW  // row steps stage wave 0's wrap rows inside their first chain
 #define SK4C_STAGE_IN_ROW 1
 #endif
@@ -1005,7 +1011,7 @@ __global__ void __launch_bounds__(64 * s4c_max_waves<CPL>()) sk_stem4d_col_kerne
   // steps: T(last position) + R
   int np = 0;
   for (int gg = 0; gg * NB < n; ++gg) np += s4c_group_len(gg, n, NB, FP);
-  const int total = np > 0 ? ((np - 1) / W) * R + (np - 1) % W + R : 0;  // (< 2^31 for |x|, |y| < 512)
+  const int total = np > 0 ? ((np - 1) / W) * R + (np - 1) % W + R : 0;  // (< 2^31: |x| <= kS4cMaxN, |y| < 512)
 
   // Every position runs all NB chains: a group cut short by n runs virtual
   // columns past n (no stacking sources; the last group's G0 store is never
@@ -1578,16 +1584,19 @@ int stem4d_col_nb(int cpl) {
   return cpl <= 1 ? s4c_nb<1>() : cpl == 2 ? s4c_nb<2>() : cpl == 4 ? s4c_nb<4>() : s4c_nb<8>();
 }
 
-size_t stem4d_col_lds_bytes(int cpl, int waves, int m) {
+int stem4d_col_max_n() { return kS4cMaxN; }
+
+size_t stem4d_col_lds_bytes(int cpl, int waves, int m, int n) {
   const int nb = stem4d_col_nb(cpl);
   return ((size_t)(waves + 1) * 2 * nb * 64 * cpl + waves) * sizeof(double) +
-         (size_t)(64 * cpl + m + 1 + 8 + 512 + 15) / 16 * 16;  // y, x (|x| < 512)
+         (size_t)(64 * cpl + m + 1 + 8 + std::max(n, 0) + 15) / 16 * 16;  // y, x
 }
 
 hipError_t launch_stem4d_col(const Stem4dLaunch& P, int64_t n_pairs, int cpl, int waves, int max_m,
-                             hipStream_t st) {
+                             int max_n, hipStream_t st) {
   if (n_pairs == 0) return hipSuccess;
-  const size_t lds = stem4d_col_lds_bytes(cpl, waves, max_m);
+  if (max_n > kS4cMaxN || max_m + 1 > 64 * cpl) return hipErrorInvalidValue;
+  const size_t lds = stem4d_col_lds_bytes(cpl, waves, max_m, max_n);
   const dim3 grid((unsigned)n_pairs), block(64 * waves);
 #define SK_L(C)                                                                                   \
   {                                                                                               \

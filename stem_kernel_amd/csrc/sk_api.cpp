@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <numeric>
 #include <queue>
@@ -152,9 +153,23 @@ struct HostPack {
 }  // namespace
 
 // 4-D stem kernel tables of every example of a dataset, resident on the
-// device: built on the first 4-D call for a bp model and loop, rebuilt when
-// examples were added since (examples are append-only); stem4d_tables
+// device: one set per (device, bp model, loop), built on the first 4-D call
+// for it and rebuilt when examples were added since (examples are
+// append-only); stem4d_tables.  A call holds its sets through shared_ptrs, and
+// a replaced set synchronizes its own device before its buffers are freed,
+// so kernels of any context still reading it finish first.
 struct Stem4dTables {
+  Stem4dTables() = default;
+  Stem4dTables(const Stem4dTables&) = delete;
+  Stem4dTables& operator=(const Stem4dTables&) = delete;
+  ~Stem4dTables() {
+    if (device < 0 || buf.ptrs.empty()) return;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) cur = -1;
+    if (hipSetDevice(device) == hipSuccess) (void)hipDeviceSynchronize();
+    buf.release();
+    if (cur >= 0) (void)hipSetDevice(cur);
+  }
   DeviceBuffers buf;
   int device = -1, model = -1;
   unsigned loop = 0;
@@ -181,8 +196,11 @@ struct sk_dataset {
   // depend only on the dataset (immutable once uploaded) and loop_gap
   double* prep = nullptr;
   double prep_loop_gap = -1.0;
-  Stem4dTables s4;
+  // 4-D tables per (device, bp model, loop), at most kS4Sets (oldest dropped)
+  std::mutex s4_mu;
+  std::vector<std::shared_ptr<Stem4dTables>> s4;
 };
+constexpr size_t kS4Sets = 4;
 
 struct Stem4dBatch {
   sk::Stem4dPair* pairs = nullptr;
@@ -1830,11 +1848,19 @@ void stem4d_tables(const Example& X, const sk_kernel_params* kp, std::vector<flo
     }
 }
 
-static int stem4d_dataset_tables(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp) {
-  Stem4dTables& T = ds->s4;
-  if (T.bp && T.device == ctx->device && T.model == kp->bp_model && T.loop == kp->loop &&
-      T.n_ex == ds->ex.size())
+static int stem4d_dataset_tables(sk_context* ctx, sk_dataset* ds, const sk_kernel_params* kp,
+                                 std::shared_ptr<const Stem4dTables>* out) {
+  std::lock_guard<std::mutex> lk(ds->s4_mu);
+  auto same = [&](const std::shared_ptr<Stem4dTables>& t) {
+    return t->device == ctx->device && t->model == kp->bp_model && t->loop == kp->loop;
+  };
+  auto it = std::find_if(ds->s4.begin(), ds->s4.end(), same);
+  if (it != ds->s4.end() && (*it)->n_ex == ds->ex.size()) {
+    *out = *it;
     return SK_OK;
+  }
+  auto tp = std::make_shared<Stem4dTables>();
+  Stem4dTables& T = *tp;
   const size_t n = ds->ex.size();
   std::vector<float> bpall, bp;
   std::vector<uint8_t> chall, chr;
@@ -1861,16 +1887,21 @@ static int stem4d_dataset_tables(sk_context* ctx, sk_dataset* ds, const sk_kerne
     bpall.insert(bpall.end(), bp.begin(), bp.end());
     chall.insert(chall.end(), chr.begin(), chr.end());
   }
-  if (T.bp) SK_HIP(ctx, hipDeviceSynchronize());  // launches still reading the old tables
-  T.bp = nullptr;
-  T.ch = nullptr;
-  T.buf.release();
+  T.device = ctx->device;
   SK_HIP(ctx, upload(T.buf, bpall, &T.bp));
   SK_HIP(ctx, upload(T.buf, chall, &T.ch));
-  T.device = ctx->device;
   T.model = kp->bp_model;
   T.loop = kp->loop;
   T.n_ex = n;
+  // the set it replaces is freed once no call holds it (after its device
+  // synchronizes, ~Stem4dTables)
+  if (it != ds->s4.end()) {
+    *it = tp;
+  } else {
+    if (ds->s4.size() >= kS4Sets) ds->s4.erase(ds->s4.begin());
+    ds->s4.push_back(tp);
+  }
+  *out = tp;
   return SK_OK;
 }
 
@@ -1882,12 +1913,12 @@ int64_t stem4d_plane_doubles(int m) {
 
 // waves per pair of the column kernel for a batch whose y lengths lie in
 // [min_m, max_m] (min_m counts |y| >= 2 only; INT32_MAX for none)
-static int col_waves(int cpl, int min_m, int max_m) {
+static int col_waves(int cpl, int min_m, int max_m, int max_n) {
   static const int w_env = std::getenv("SK4C_W") ? std::max(1, std::atoi(std::getenv("SK4C_W"))) : 0;
   int W = std::min(w_env ? w_env : sk::stem4d_col_max_waves(cpl), sk::stem4d_col_max_waves(cpl));
   if (min_m != INT32_MAX) W = std::min(W, sk::stem4d_col_w_max(min_m));
   W = std::max(W, 1);
-  while (W > 1 && sk::stem4d_col_lds_bytes(cpl, W, max_m) > 160 * 1024) --W;
+  while (W > 1 && sk::stem4d_col_lds_bytes(cpl, W, max_m, max_n) > 160 * 1024) --W;
   return W;
 }
 
@@ -1907,11 +1938,13 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // full_dp operation for operation.
   const bool ali_phmm = ali && kp->ali_zerop_fixed;
   // per-example tables, resident per dataset (built on first use)
-  int rc = stem4d_dataset_tables(ctx, xs_, kp);
+  std::shared_ptr<const Stem4dTables> tx, ty;
+  int rc = stem4d_dataset_tables(ctx, xs_, kp, &tx);
   if (rc) return rc;
-  if (ys_ != xs_ && (rc = stem4d_dataset_tables(ctx, ys_, kp))) return rc;
-  const Stem4dTables& TX = xs_->s4;
-  const Stem4dTables& TY = ys_->s4;
+  if (ys_ == xs_) ty = tx;
+  else if ((rc = stem4d_dataset_tables(ctx, ys_, kp, &ty))) return rc;
+  const Stem4dTables& TX = *tx;
+  const Stem4dTables& TY = *ty;
   auto usable = [&](const Stem4dTables& T, int e) -> int {
     if (T.why[e] == 1) return fail(ctx, SK_ERR_INVALID, "4-D stem kernel takes single sequences");
     if (T.why[e] == 2) return fail(ctx, SK_ERR_INVALID, "4-D stem kernel with bp_model 0 needs base pairs");
@@ -1963,9 +1996,12 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // go to the span kernel in batches of their own)
   const bool colk_call = gsum && !ktiles && !std::getenv("SK4_SPAN") && !std::getenv("SK4_NO_PRE");
   const int col_nb = colk_call ? sk::stem4d_col_nb(cpl) : 0;
+  // (|x| <= stem4d_col_max_n(): the kernel holds x in LDS and counts its
+  // steps in an int; longer x take the span kernel)
   auto col_ok = [&](int64_t q) {
     const int m = ys_->ex[y[q]].len;
-    return colk_call && (m <= 1 || sk::stem4d_col_w_max(m) >= 1);
+    return colk_call && xs_->ex[x[q]].len <= sk::stem4d_col_max_n() &&
+           (m <= 1 || sk::stem4d_col_w_max(m) >= 1);
   };
   // batches of one kernel: the column kernel's pairs first, then longest x first
   std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
@@ -2017,7 +2053,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       int min_m = INT32_MAX;
       for (const auto& p : prs)
         if (p.m >= 2) min_m = std::min(min_m, p.m);
-      const int W = col_waves(cpl, min_m, max_m);
+      const int W = col_waves(cpl, min_m, max_m, maxn);
       rc = ensure_scratch(ctx, ring_bytes + 64);
       if (rc) return rc;
       if (Bt.cap_pairs < prs.size()) {
@@ -2046,7 +2082,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
       L.gsum = 3;
       SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
       SK_HIP(ctx, sk::lev_mark(ctx, S));
-      SK_HIP(ctx, sk::launch_stem4d_col(L, (int64_t)prs.size(), cpl, W, max_m, S));
+      SK_HIP(ctx, sk::launch_stem4d_col(L, (int64_t)prs.size(), cpl, W, max_m, maxn, S));
       SK_HIP(ctx, sk::lev_mark(ctx, S));
       ctx->last_s4d_classes |= 1u << ((cpl == 1 ? 0 : cpl == 2 ? 1 : cpl == 4 ? 2 : 3) + 8);
       ++launches;
@@ -3695,7 +3731,11 @@ int sk_fold_synthetic(const char* seq, int32_t n, int32_t no_gu, double* out) {
 namespace {
 
 // Boltzmann factor tables of fold.hip (host/fold_params.h), laid out in one
-// buffer; max_len bounds the hairpin and scale tables.
+// buffer: the fixed-size tables first (o_st .. o_ml, n_small doubles), then
+// the two whose length follows the batch's longest sequence max_len (hairpin,
+// scale powers), so a launch whose tables outgrow the LDS keeps the first
+// part in LDS and reads the tail from HBM (fold.hip GTAB).  Entry k of every
+// table is the same double whatever max_len is.
 void fold_tables(int max_len, sk::FoldLaunch& L, std::vector<double>& t) {
   using namespace sk::foldp;
   t.clear();
@@ -3703,16 +3743,6 @@ void fold_tables(int max_len, sk::FoldLaunch& L, std::vector<double>& t) {
   L.o_st = (int32_t)t.size();
   for (int a = 0; a < 7; ++a)
     for (int b = 0; b < 7; ++b) t.push_back(a && b ? bz(stack37[a][b]) : 0.0);
-  L.o_hp = (int32_t)t.size();
-  for (int k = 0; k <= max_len + 1; ++k) {
-    if (k < 3) {
-      t.push_back(0.0);
-      continue;
-    }
-    double e = hairpin37[k <= 30 ? k : 30];
-    if (k > 30) e += lxc * std::log((double)k / 30.0);
-    t.push_back(bz(e));
-  }
   L.o_bu = (int32_t)t.size();
   for (int k = 0; k <= max_loop; ++k) t.push_back(k ? bz(bulge37[k]) : 0.0);
   L.o_in = (int32_t)t.size();
@@ -3724,9 +3754,22 @@ void fold_tables(int max_len, sk::FoldLaunch& L, std::vector<double>& t) {
   L.o_ml = (int32_t)t.size();
   t.push_back(bz(ml_closing + ml_intern));
   t.push_back(bz(ml_intern));
+  L.n_small = (int32_t)t.size();
+  L.o_hp = (int32_t)t.size();
+  for (int k = 0; k <= max_len + 1; ++k) {
+    if (k < 3) {
+      t.push_back(0.0);
+      continue;
+    }
+    double e = hairpin37[k <= 30 ? k : 30];
+    if (k > 30) e += lxc * std::log((double)k / 30.0);
+    t.push_back(bz(e));
+  }
   L.o_scp = (int32_t)t.size();
   for (int k = 0; k <= max_len + 2; ++k) t.push_back(std::exp(log_sc * k));
   L.log_sc = log_sc;
+  L.n_tab = (int32_t)t.size();
+  L.n_tab_pad = (L.n_tab + 1) & ~1;
 }
 
 int8_t fold_code(char ch) {
@@ -3787,9 +3830,6 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
   }
   sk::FoldLaunch L;
   std::vector<double> tab;
-  fold_tables(max_len, L, tab);
-  L.n_tab = (int32_t)tab.size();
-  L.n_tab_pad = (L.n_tab + 1) & ~1;
   L.no_gu = (flags & SK_FOLD_NO_GU) ? 1 : 0;
   L.no_closing_gu = (flags & SK_FOLD_NO_CLOSING_GU) ? 1 : 0;
   size_t free_b = 0, total_b = 0;
@@ -3826,6 +3866,9 @@ int sk_fold_mccaskill(sk_context* ctx, int32_t n, const char* const* seqs, int32
       sq.push_back(f);
     }
     const int nb = b1 - b0;
+    fold_tables(bmax, L, tab);  // sized by this batch's longest sequence
+    if (sk::fold_lds_bytes(L, bmax) > sk::kFoldLdsMax)
+      return fail(ctx, SK_ERR_UNSUPPORTED, "fold: sequence too long for the fold kernel's LDS");
     size_t need = sq.size() * sizeof(sk::FoldSeq) + codes.size() + lp.size() + tab.size() * 8 +
                   (outn + nb) * 8 + 7 * 256;
     int rc = ensure_work(ctx, need);
@@ -3995,8 +4038,14 @@ int sk_last_launch_ms(const sk_context* ctx, double* ms_sum, int32_t* n_launches
 int sk_stem4d_col_shape(int32_t min_len, int32_t max_len, int32_t* nb, int32_t* waves, int32_t* pf) {
   if (max_len < 0 || min_len > max_len) return SK_ERR_INVALID;
   const int cpl = sk::stem4d_cpl(max_len);
+  // the shape of the launch that actually runs (a Gram: x and y lengths in
+  // [min_len, max_len]); waves = 0 where the column kernel does not run --
+  // |y| >= 512 (k tiles), |x| past its LDS / step-count limit, or a y too
+  // short for the column schedule (those pairs take the span kernel)
+  const bool runs = max_len + 1 <= 64 * cpl && max_len <= sk::stem4d_col_max_n() &&
+                    (min_len <= 1 || sk::stem4d_col_w_max(min_len) >= 1);
   if (nb) *nb = sk::stem4d_col_nb(cpl);
-  if (waves) *waves = col_waves(cpl, min_len >= 2 ? min_len : INT32_MAX, max_len);
+  if (waves) *waves = runs ? col_waves(cpl, min_len >= 2 ? min_len : INT32_MAX, max_len, max_len) : 0;
   if (pf) *pf = sk::stem4d_col_pf();
   return SK_OK;
 }

@@ -136,3 +136,21 @@ def test_gpu_fold_no_lonely_pairs(gpu_ctx, no_gu):
             b, pb, _ = po.fold_enum(s, no_gu, False, no_lp=True)
             assert abs(z - b) < 1e-12 * max(1.0, abs(b)) and np.max(np.abs(p - pb), initial=0.0) < 1e-12
     assert any(np.max(np.abs(p - q)) > 1e-6 for p, q in zip(got[4:], plain[4:]))
+
+
+@pytest.mark.gpu
+def test_gpu_fold_tables_sized_per_batch(gpu_ctx):
+    """the Boltzmann tables are sized by each launch's longest
+    sequence (sk_fold_mccaskill builds them per batch), so short sequences
+    fold the same -- on the LDS-ring path -- alone and in a call with a
+    1,200-nt sequence (no ring; its hairpin / scale tables 19 KB longer); the
+    long one against the oracle's ln Z."""
+    rng = np.random.default_rng(77)
+    short = [_rand_seq(rng, L) for L in (12, 60, 150)]
+    long_ = _rand_seq(rng, 1200)
+    a, za = gpu_ctx.fold(short, log_z=True)
+    b, zb = gpu_ctx.fold(short + [long_], log_z=True)
+    for k in range(len(short)):
+        assert np.max(np.abs(a[k] - b[k]), initial=0.0) < 1e-13 and abs(za[k] - zb[k]) <= 1e-13 * abs(za[k])
+    ref_z, _ = po.fold_mccaskill(long_, 0, 0)
+    assert abs(zb[-1] - ref_z) <= 1e-12 * abs(ref_z)

@@ -182,8 +182,15 @@ def test_stem4d_at_config_size(gpu_ctx):
     for k in range(len(xs)):  # one call per pair: a call's class follows its longest y
         got = gpu_ctx.pairs(ds, ska.StemKernel4D(band=int(band[k])), [idx[xs[k]]], [idx[ys[k]]])
         assert rel_err(got, S4D["value"][k:k + 1]) < TOL, k
-        seen |= set(gpu_ctx.last_classes()["stem4d"])
-    assert {(4, False), (8, False), (4, True)} <= seen
+        cls = gpu_ctx.last_classes()
+        seen |= set(cls["stem4d"])
+        if int(band[k]) == 0 and len(ys[k]) < 512 and len(xs[k]) <= 2048:
+            # the default full_dp kernel is the column-group kernel: it, and
+            # only it, ran on this unbanded config-size pair
+            cpl = next(c for c in (1, 2, 4, 8) if len(ys[k]) < 64 * c)
+            assert cls["stem4d_col"] == [cpl] and cls["stem4d"] == [(cpl, False)], (k, cls)
+            seen.add(("col", cpl))
+    assert {(4, False), (8, False), (4, True), ("col", 4), ("col", 8)} <= seen
 
 
 @pytest.mark.gpu

@@ -58,3 +58,43 @@ def test_stem4d_long_mixed_call(gpu_ctx, long_set):
     got = gpu_ctx.pairs(ds, ska.StemKernel4D(), [idx[a] for _, (a, _, _) in cs],
                         [idx[b] for _, (_, b, _) in cs])
     assert rel_err(got, LONG["value"][[k for k, _ in cs]]) < TOL
+
+
+LONGX = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "longx_4d.npz"))
+
+
+def _cases_x():
+    return [(str(a), str(b)) for a, b in zip(LONGX["x"], LONGX["y"])]
+
+
+def test_longx_fold_bytes_pinned():
+    h = hashlib.sha256()
+    for a, b in _cases_x():
+        for t in (a, b):
+            h.update(np.ascontiguousarray(ska.fold(t.lower()), np.float64).tobytes())
+    assert h.hexdigest() == str(LONGX["sha"])
+    assert max(len(a) for a, _ in _cases_x()) > 2048  # one pair past the column kernel's x limit
+    assert any(512 < len(a) <= 2048 for a, _ in _cases_x())
+
+
+@pytest.mark.gpu
+def test_stem4d_long_x_short_y(gpu_ctx):
+    """Long x against short y: the column kernel's x characters
+    sit in LDS sized from the batch's longest x, so |x| 640 / 700 / 1,200
+    against |y| 40-100 run on it (before, a fixed 512-byte region dropped the
+    tail of x); |x| = 2,100 is past its limit and runs the span kernel.  One
+    call per pair and one call for all; every value against the oracle's."""
+    seqs = sorted({s for c in _cases_x() for s in c})
+    ds = ska.Dataset.from_sequences(seqs, bpp=[ska.fold(s.lower()) for s in seqs])
+    idx = {s: i for i, s in enumerate(seqs)}
+    for k, (a, b) in enumerate(_cases_x()):
+        got = gpu_ctx.pairs(ds, ska.StemKernel4D(), [idx[a]], [idx[b]])
+        assert rel_err(got, LONGX["value"][k:k + 1]) < TOL, (k, got, LONGX["value"][k])
+        cls = gpu_ctx.last_classes()
+        if len(a) <= 2048:  # (stem4d lists the column kernel's classes too)
+            assert cls["stem4d_col"] and cls["stem4d"] == [(c, False) for c in cls["stem4d_col"]], (k, cls)
+        else:
+            assert cls["stem4d"] and not cls["stem4d_col"], (k, cls)
+    cs = _cases_x()
+    got = gpu_ctx.pairs(ds, ska.StemKernel4D(), [idx[a] for a, _ in cs], [idx[b] for _, b in cs])
+    assert rel_err(got, LONGX["value"]) < TOL
