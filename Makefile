@@ -24,7 +24,7 @@ HDRS := $(wildcard $(ROOT)stem_kernel_amd/csrc/*/*.h) $(ROOT)include/stem_kernel
 HOST_OBJ := $(patsubst $(ROOT)stem_kernel_amd/csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC) $(API_SRC))
 HIP_OBJ := $(patsubst $(ROOT)stem_kernel_amd/csrc/%.hip,$(BUILD)/%.o,$(HIP_SRC))
 
-all: lib cli oracle
+all: lib cli oracle exp
 
 lib: $(LIB)
 
@@ -92,3 +92,17 @@ variant4:
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -x hip -c $(ROOT)stem_kernel_amd/csrc/kernels/stem4d.hip -o $(BUILD)/var/$(NAME)/stem4d.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(BUILD)/libsk_$(NAME).so $(BUILD)/host/synth.o $(BUILD)/host/example_build.o $(BUILD)/host/readers.o $(BUILD)/host/shard.o $(BUILD)/host/svm_predict.o $(BUILD)/sk_api.o $(BUILD)/kernels/dag_stem.o $(BUILD)/kernels/profile_string.o $(BUILD)/kernels/bpla.o $(BUILD)/var/$(NAME)/stem4d.o $(BUILD)/kernels/phmm.o $(BUILD)/kernels/bpla_grad.o $(BUILD)/kernels/dag_stem_big.o $(BUILD)/kernels/fold.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 .PHONY: variant4
+
+# experiments build: the shipped sources with the A/B switches compiled in
+# (SK_KNOB reads the environment; sk_experiments() = 1) -> build/libstem_kernel_amd_exp.so,
+# loaded by the GPU tests that compare kernel variants (tests/explib.py)
+EXP_LIB := $(ROOT)build/libstem_kernel_amd_exp.so
+EXP_OBJ := $(patsubst $(ROOT)stem_kernel_amd/csrc/%.cpp,$(BUILD)/exp/%.o,$(HOST_SRC) $(API_SRC))
+exp: $(EXP_LIB)
+$(BUILD)/exp/%.o: $(ROOT)stem_kernel_amd/csrc/%.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(CXXFLAGS) -DSK_EXPERIMENTS -D__HIP_PLATFORM_AMD__ -c $< -o $@
+$(BUILD)/exp/host/synth.o: CXXFLAGS += -ffp-contract=off
+$(EXP_LIB): $(EXP_OBJ) $(HIP_OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+.PHONY: exp

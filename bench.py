@@ -297,21 +297,25 @@ def roofline(config, kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, ce
     """The dominant kernel's roofline.
 
     HBM-bound kernels (DAG stem, 4-D stem): the headline `achieved` is the
-    MEASURED HBM bytes per launch (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, per
-    cell, scaled to this run's cells) over the launches' span per launch (the
-    launches run on several streams and overlap: span / launches), so `frac`
-    cannot pass 1.  `algorithmic_per_launch` is the implemented algorithm's
-    compulsory bytes (DAG: the gamma schedule's stored rows written and read
-    back once, `dag_row_bytes`; 4-D: 16/NB + 16/W B per cell), a lower bound
-    of the measured bytes; `algorithmic_frac` puts it over the same span.  The
+    implemented algorithm's COMPULSORY bytes per launch
+    (`algorithmic_per_launch`: DAG, the gamma schedule's stored rows written
+    and read back once, `dag_row_bytes`; 4-D column kernel, 16/NB + 16/W B per
+    cell) over the launches' span per launch (the launches run on several
+    streams and overlap: span / launches), so `frac` is the compulsory-traffic
+    fraction of the 8 TB/s peak.  The counter figure stands beside it:
+    `traffic` (rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch, per cell from
+    the committed profile, scaled to this run's cells) and `traffic_frac`
+    (traffic over the same span) -- L2-to-fabric bytes, Infinity-Cache (MALL)
+    hits included (MI355X_MICROARCH.md; tools/calib/fetch_calib.hip's
+    re-read case), so an upper bound of the HBM bytes, not HBM bytes.  The
     DAG kernel also reports every row transfer its schedule issues
     (`schedule_bytes_per_launch`) and SURVEY §8d's model bytes
     (`survey_model_bytes_per_launch`, no fraction: the path-sum, gamma and phi
     reformulation never moves them).  A profile measured on other kernel
-    sources is `stale`: then `traffic` is null and `frac` falls back to the
-    algorithmic bytes over the average launch duration (`basis` says which).
-    FP64 kernels (BPLA): algorithmic flops per launch over the average launch
-    duration."""
+    sources is `stale`: its `traffic` is then null.  `frac_per_avg_launch`
+    puts the compulsory bytes over the average launch duration instead of the
+    span.  FP64 kernels (BPLA): algorithmic flops per launch over the average
+    launch duration."""
     bound, unit, peak, model, alg, extra = algorithmic(kind, shapes, xs, ys, rt)
     n_launch = max(1, n_launch)
     avg_s = sum_ms / n_launch * 1e-3
@@ -335,17 +339,18 @@ def roofline(config, kind, length, shapes, xs, ys, span_ms, sum_ms, n_launch, ce
     for k, v in extra.items():
         r[k + "_per_launch"] = v / n_launch
     if bound == "hbm":
-        r["algorithmic_frac"] = alg_pl / eff_s / scale / peak if eff_s > 0 else None
+        r["achieved"] = alg_pl / eff_s / scale if eff_s > 0 else 0.0
+        r["basis"] = "compulsory (algorithmic) bytes per launch / (launches' span / launches)"
+        r["frac_per_avg_launch"] = alg_pl / avg_s / scale / peak if avg_s > 0 else None
         if traffic is not None and fresh and eff_s > 0:
-            r["achieved"] = traffic / eff_s / scale
-            r["basis"] = ("measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, " + rel +
-                          ") / (launches' span / launches)")
             r["traffic"] = traffic
+            r["traffic_frac"] = traffic / eff_s / scale / peak
+            r["traffic_basis"] = ("2 x FETCH_SIZE + WRITE_SIZE per launch (" + rel + ") / (launches' span / "
+                                  "launches): L2-to-fabric bytes, Infinity-Cache (MALL) hits included -- an "
+                                  "upper bound of the HBM bytes")
         else:
-            r["achieved"] = alg_pl / avg_s / scale if avg_s > 0 else 0.0
-            r["basis"] = ("algorithmic bytes per launch / average launch duration (no fresh "
-                          "measured traffic: " + ("stale profile" if pm is not None else "no profile") + ")")
             r["traffic"] = None
+            r["traffic_frac"] = None
             if traffic is not None:
                 r["traffic_stale_value"] = traffic
         r["traffic_per_cell"] = pm.get("hbm_bytes_per_cell") if pm else None

@@ -431,6 +431,10 @@ int sk_stem4d_col_shape(int32_t min_len, int32_t max_len, int32_t *nb, int32_t *
 /* RIBOSUM85-60 tables as compiled into the library (pinning tests). */
 void sk_ribosum_tables(float *s16, float *p256);
 int sk_char2rna(int c);
+/* 1 in the experiments build (make exp: build/libstem_kernel_amd_exp.so, which
+ * reads the A/B switches INTEGRATION.md lists from the environment), 0 in the
+ * shipped library (no switches compiled in). */
+int sk_experiments(void);
 
 #ifdef __cplusplus
 }

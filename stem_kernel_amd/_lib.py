@@ -104,6 +104,7 @@ SIGNATURES = {
     "sk_stem4d_col_shape": (C.c_int, [C.c_int32, C.c_int32, _I32P, _I32P, _I32P]),
     "sk_ribosum_tables": (None, [_F32P, _F32P]),
     "sk_char2rna": (C.c_int, [C.c_int]),
+    "sk_experiments": (C.c_int, []),
     "sk_bpla_gradients": (C.c_int, [_P, _P, _P, C.POINTER(KernelParams), _I32P, _I32P, C.c_int64,
                                     _F64P, _F64P]),
     "sk_seqfile_read": (C.c_int, [C.c_char_p, C.c_int32, C.POINTER(_P)]),

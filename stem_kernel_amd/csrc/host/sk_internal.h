@@ -5,6 +5,18 @@
 #include <string>
 #include <vector>
 
+// Experiment switches (A/B variants of equal results, tuning knobs): read
+// from the environment only in the experiments build (make exp ->
+// build/libstem_kernel_amd_exp.so, -DSK_EXPERIMENTS); the shipped library
+// compiles them out -- SK_KNOB is a null pointer and the switch's name is not
+// in the binary -- so it reads only diagnostics and thread-count variables.
+#ifdef SK_EXPERIMENTS
+#include <cstdlib>
+#define SK_KNOB(name) (std::getenv(name))
+#else
+#define SK_KNOB(name) ((const char*)nullptr)
+#endif
+
 namespace sk {
 
 // ---------------------------------------------------------------------------

@@ -313,11 +313,17 @@ __device__ __forceinline__ double row_ld(__amdgpu_buffer_rsrc_t r, int lane, int
 #ifndef SK_HALF_D  // phase D likewise
 #define SK_HALF_D 64
 #endif
+#ifndef SK_M16_HALFA  // the 12-wave MAXK 16 class loads A in halves
+#define SK_M16_HALFA 1
+#endif
+#ifndef SK_M16_HALFD  // ... and reads D's G1 in halves
+#define SK_M16_HALFD 1
+#endif
 template <int MAXK>
 __device__ __forceinline__ void add_rows2(double (&S)[MAXK], __amdgpu_buffer_rsrc_t r0,
                                           __amdgpu_buffer_rsrc_t r1, double eg0, double eg1,
                                           int lane) {
-  constexpr int H = (MAXK > SK_HALF_A || m16_wide<MAXK>()) ? MAXK / 2 : MAXK;
+  constexpr int H = (MAXK > SK_HALF_A || (m16_wide<MAXK>() && SK_M16_HALFA)) ? MAXK / 2 : MAXK;
 #pragma unroll
   for (int h0 = 0; h0 < MAXK; h0 += H) {
     double a[H], b[H];
@@ -876,7 +882,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // per-thread program order makes it visible: no fence.  A row nobody
     // reads (a root) is not stored; it is no child of the next row either.
     // (the widest classes read G1 back in two halves: fewer live registers)
-    constexpr int HD = (MAXK > SK_HALF_D || m16_wide<MAXK>()) ? MAXK / 2 : MAXK;
+    constexpr int HD = (MAXK > SK_HALF_D || (m16_wide<MAXK>() && SK_M16_HALFD)) ? MAXK / 2 : MAXK;
     if (pslot == 0xffffu) {
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) S[k] = egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);

@@ -608,7 +608,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
   auto tnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double tp0 = tnow();
   // SK_SWEEP_LANES=0: sweep chunks in schedule order (A/B diagnostics)
-  const char* lanes_env = std::getenv("SK_SWEEP_LANES");
+  const char* lanes_env = SK_KNOB("SK_SWEEP_LANES");
   const bool sweep_lanes_greedy = !lanes_env || std::atoi(lanes_env) != 0;
   P = HostPack();
   const int n = (int)ds->ex.size();
@@ -680,14 +680,14 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
   }
   std::sort(P.gam_key.begin(), P.gam_key.end());
   P.gam_key.erase(std::unique(P.gam_key.begin(), P.gam_key.end()), P.gam_key.end());
-  const bool gam_on = !P.gam_key.empty() && P.gam_key.size() <= 512 && !std::getenv("SK_NO_GAMMA");
+  const bool gam_on = !P.gam_key.empty() && P.gam_key.size() <= 512 && !SK_KNOB("SK_NO_GAMMA");
   if (!gam_on) P.gam_key.clear();
   auto gamma_idx = [&](uint32_t key) {
     return (uint32_t)(std::lower_bound(P.gam_key.begin(), P.gam_key.end(), key) - P.gam_key.begin());
   };
   std::sort(phi_raw.begin(), phi_raw.end());
   phi_raw.erase(std::unique(phi_raw.begin(), phi_raw.end()), phi_raw.end());
-  const bool phi_on = gam_on && !phi_raw.empty() && phi_raw.size() < 0x4000 && !std::getenv("SK_NO_PHI");
+  const bool phi_on = gam_on && !phi_raw.empty() && phi_raw.size() < 0x4000 && !SK_KNOB("SK_NO_PHI");
   if (phi_on)
     for (uint64_t k : phi_raw) {
       P.phi_al.push_back((uint32_t)k);
@@ -1063,7 +1063,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
             }
           }
         }
-        if (std::getenv("SK_REF_ORDER")) {
+        if (SK_KNOB("SK_REF_ORDER")) {
           for (int v = 0; v < nn; ++v)
             if (level[v] >= 0) order.push_back(v);
         } else {
@@ -1105,7 +1105,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
             if (pos[v] < nn && (first_parent[c] == nn || pos[v] < pos[first_parent[c]])) first_parent[c] = v;
           }
         std::vector<std::vector<int>> before(nn + 1);
-        const bool move = phi_on && !std::getenv("SK_PHI_POSTORDER");
+        const bool move = phi_on && !SK_KNOB("SK_PHI_POSTORDER");
         std::vector<int> o1;
         for (int v : order) {
           if (move && is_phi(X, v)) before[first_parent[v]].push_back(v);
@@ -1145,7 +1145,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
       // rows read only by the next row, among its first four children, are
       // never stored: the next row takes them from registers (slot 0xfffe)
       std::vector<uint8_t> nostore(nn, 0);
-      if (!std::getenv("SK_STORE_ALL")) {
+      if (!SK_KNOB("SK_STORE_ALL")) {
         std::vector<int> npar(nn, 0), emitted;
         for (int v = 0; v < nn; ++v)
           for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) ++npar[X.edge_to[k]];
@@ -1579,7 +1579,7 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   const HostPack& PY = ys_->pack;
   // per-example lengths and flags once (the pair loops below touch only
   // these small arrays, not the examples)
-  const bool general_only = std::getenv("SK_BPLA_GENERAL") != nullptr;  // A/B switch
+  const bool general_only = SK_KNOB("SK_BPLA_GENERAL") != nullptr;  // A/B switch
   auto ex_info = [&](const sk_dataset* d, const HostPack& H, std::vector<int32_t>& len,
                      std::vector<uint8_t>& ok, std::vector<uint8_t>& dy) {
     const size_t m = d->ex.size();
@@ -1621,12 +1621,12 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
   std::vector<int32_t> px, py;
   std::vector<int64_t> oidx;
   constexpr int kItemWaves = 8;
-  static const int item_max = std::getenv("SK_BPLA_ITEM") ? std::max(1, std::atoi(std::getenv("SK_BPLA_ITEM")))
+  static const int item_max = SK_KNOB("SK_BPLA_ITEM") ? std::max(1, std::atoi(SK_KNOB("SK_BPLA_ITEM")))
                                                           : 16 * sk::kBplaItemsWavesMax;
   std::vector<int2> items;
   {
     const bool group = n_fast >= 4 * kItemWaves * std::max<int64_t>(distinct, 1) &&
-                       !std::getenv("SK_BPLA_NO_ITEMS");
+                       !SK_KNOB("SK_BPLA_NO_ITEMS");
     const bool permute = n_fast != n || group;
     if (permute && n_fast) {
       px.resize((size_t)n);
@@ -1757,7 +1757,7 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
       // pairs a wave streams back to back (SK_BPLA_CHUNK: 1..kBplaChunkMax)
       // (0: per item, as many as give each wave one chunk)
       F.chunk = 8;  // C4, items of 192 pairs: 7.99 ms per launch against 8.58 (4) and 8.97 (16)
-      if (const char* e = std::getenv("SK_BPLA_CHUNK")) F.chunk = std::atoi(e);
+      if (const char* e = SK_KNOB("SK_BPLA_CHUNK")) F.chunk = std::atoi(e);
       F.chunk = std::min(std::max(F.chunk, 0), sk::kBplaChunkMax);
       // waves per workgroup and workgroups per CU (SK_BPLA_IWAVES /
       // SK_BPLA_IWG: geometry experiments; the VGPR budget caps the waves
@@ -1767,8 +1767,8 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
       // waves), halved while its LDS does not fit, the CU's 16 waves then
       // made up by more workgroups.
       static const int iw =
-          std::getenv("SK_BPLA_IWAVES") ? std::atoi(std::getenv("SK_BPLA_IWAVES")) : sk::kBplaItemsWavesMax;
-      static const int iwg = std::getenv("SK_BPLA_IWG") ? std::atoi(std::getenv("SK_BPLA_IWG")) : 0;
+          SK_KNOB("SK_BPLA_IWAVES") ? std::atoi(SK_KNOB("SK_BPLA_IWAVES")) : sk::kBplaItemsWavesMax;
+      static const int iwg = SK_KNOB("SK_BPLA_IWG") ? std::atoi(SK_KNOB("SK_BPLA_IWG")) : 0;
       w = std::min(std::max(iw, 1), sk::kBplaItemsWavesMax);
       while (w > 1 && sk::bpla_items_lds_bytes(F.lds_max_len, w) > 163840) w /= 2;
       const size_t l = sk::bpla_items_lds_bytes(F.lds_max_len, w);
@@ -1781,7 +1781,7 @@ int run_bpla(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel_
       // as many waves per CU as the per-wave LDS allows (<= 16), in
       // workgroups of up to 4
       static const int wcap =
-          std::getenv("SK_BPLA_WAVES") ? std::atoi(std::getenv("SK_BPLA_WAVES")) : 16;
+          SK_KNOB("SK_BPLA_WAVES") ? std::atoi(SK_KNOB("SK_BPLA_WAVES")) : 16;
       const int per_cu_w =
           (int)std::max<size_t>(1, std::min<size_t>((size_t)wcap, (163840 - 2 * sk::kBplaExpLds) / wl));
       w = std::min(4, per_cu_w);
@@ -1914,7 +1914,7 @@ int64_t stem4d_plane_doubles(int m) {
 // waves per pair of the column kernel for a batch whose y lengths lie in
 // [min_m, max_m] (min_m counts |y| >= 2 only; INT32_MAX for none)
 static int col_waves(int cpl, int min_m, int max_m, int max_n) {
-  static const int w_env = std::getenv("SK4C_W") ? std::max(1, std::atoi(std::getenv("SK4C_W"))) : 0;
+  static const int w_env = SK_KNOB("SK4C_W") ? std::max(1, std::atoi(SK_KNOB("SK4C_W"))) : 0;
   int W = std::min(w_env ? w_env : sk::stem4d_col_max_waves(cpl), sk::stem4d_col_max_waves(cpl));
   if (min_m != INT32_MAX) W = std::min(W, sk::stem4d_col_w_max(min_m));
   W = std::max(W, 1);
@@ -1986,7 +1986,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // and PairHMM-constrained partial_dp keep the four-state planes (their
   // boundary approximations read K0 / K1 off the band)
   const bool banded = ali_phmm || (!ali && kp->len_band > 0);
-  const bool gsum = !banded && !std::getenv("SK4_NO_GSUM");
+  const bool gsum = !banded && !SK_KNOB("SK4_NO_GSUM");
   const size_t nst = gsum ? 2 : 4;
   // full_dp with one k tile: the column-group kernel (one workgroup per pair,
   // B' handed on through LDS, NB columns chained per position;
@@ -1994,7 +1994,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
   // pre-combined span kernel instead, SK4_NO_PRE=1 the K-sum span kernel
   // (pairs whose y is too short for the column schedule, 2 <= m < 2 PF + 3,
   // go to the span kernel in batches of their own)
-  const bool colk_call = gsum && !ktiles && !std::getenv("SK4_SPAN") && !std::getenv("SK4_NO_PRE");
+  const bool colk_call = gsum && !ktiles && !SK_KNOB("SK4_SPAN") && !SK_KNOB("SK4_NO_PRE");
   const int col_nb = colk_call ? sk::stem4d_col_nb(cpl) : 0;
   // (|x| <= stem4d_col_max_n(): the kernel holds x in LDS and counts its
   // steps in an int; longer x take the span kernel)
@@ -2123,8 +2123,8 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     // dealt to nh parts whose launches run on their own streams (main, class,
     // side, aux), so each span's tail overlaps the other parts' launches (the
     // boundary columns of k tiles are per launch item: one stream then)
-    int nh = std::getenv("SK4_STREAMS") ? std::atoi(std::getenv("SK4_STREAMS")) : 4;
-    if (std::getenv("SK_SERIAL_CLASSES") || ktiles) nh = 1;
+    int nh = SK_KNOB("SK4_STREAMS") ? std::atoi(SK_KNOB("SK4_STREAMS")) : 4;
+    if (SK_KNOB("SK_SERIAL_CLASSES") || ktiles) nh = 1;
     nh = std::max(1, std::min({nh, 4, (int)prs.size()}));
     const hipStream_t hs[4] = {S, ctx->cls, ctx->side, ctx->aux};
     std::vector<int2> items;
@@ -2189,7 +2189,7 @@ int run_stem4d(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kerne
     L.kbound_stride = kb_stride;
     // one k tile: each plane's stacking chain produced one span early by the
     // plane that streams its G0 rows (stem4d.hip sk_stem4d_pre_kernel)
-    const bool no_pre = std::getenv("SK4_NO_PRE") != nullptr;  // per call (A/B tests)
+    const bool no_pre = SK_KNOB("SK4_NO_PRE") != nullptr;  // per call (A/B tests)
     L.gsum = gsum ? (!ktiles && !no_pre ? 2 : 1) : 0;
     SK_HIP(ctx, hipEventRecord(ctx->ev0, S));
     if (ali_phmm) {
@@ -2343,7 +2343,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     // y examples beyond the register classes (or forced there by the
     // diagnostic SK_FORCE_BIG_Y=1) go to sk_dag_stem_big_kernel
     const bool force_big = [] {
-      const char* e = std::getenv("SK_FORCE_BIG_Y");
+      const char* e = SK_KNOB("SK_FORCE_BIG_Y");
       return e && std::atoi(e) != 0;
     }();
     std::vector<uint8_t> ybig(ny, 0);
@@ -2408,7 +2408,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       if (best == 0) return fail(ctx, SK_ERR_UNSUPPORTED, "y example too large for LDS");
 #ifdef SK_STAMPS
       // diagnostics: SK_FORCE_WAVES=w,p -> w waves per workgroup, p workgroups per CU
-      if (const char* fw = std::getenv("SK_FORCE_WAVES")) {
+      if (const char* fw = SK_KNOB("SK_FORCE_WAVES")) {
         int w = 0, pc = 0;
         if (std::sscanf(fw, "%d,%d", &w, &pc) == 2 && w >= 1 && w <= C.nwaves && pc >= 1) {
           C.nwaves = w;
@@ -2437,7 +2437,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
         return cnt[a + 1] - cnt[a] > cnt[b + 1] - cnt[b];
       });
       double gss_k = 1.5;  // tuning knob: SK_GSS_K (items per workgroup at the start)
-      if (const char* e = std::getenv("SK_GSS_K")) gss_k = std::max(0.25, std::atof(e));
+      if (const char* e = SK_KNOB("SK_GSS_K")) gss_k = std::max(0.25, std::atof(e));
       const double share = 1.0 / (gss_k * (double)C.grid);
       double remaining = class_cost;
       C.item_off = items.size();
@@ -2512,7 +2512,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   int64_t n_soh = 0, n_sfast = 0;  // one-hot pairs; fast pairs (one-hot included)
   // (the fast kernels' per-wave LDS rows must fit a CU: else the general one)
   const int str_lds_len = (std::max(PY.max_len, 64) + 1) & ~1;
-  if (str && kp->kind != SK_NAIVE_STR && !std::getenv("SK_STR_GENERAL") &&
+  if (str && kp->kind != SK_NAIVE_STR && !SK_KNOB("SK_STR_GENERAL") &&
       sk::str_fast_wave_lds_bytes(str_lds_len, false) + sk::kStrFastLds0 <= 163840) {
     auto cat = [&](int64_t k) {
       const int a = x[k], b = y[k];
@@ -2644,7 +2644,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     }
     // class c runs on the main stream (c even) or the class stream (c odd):
     // one scratch region per stream, serving its classes in turn
-    const bool two_streams = classes.size() > 1 && !std::getenv("SK_SERIAL_CLASSES");
+    const bool two_streams = classes.size() > 1 && !SK_KNOB("SK_SERIAL_CLASSES");
     size_t scratch_need = 0, scratch_x = 0;
     for (size_t c = 0; c < classes.size(); ++c) {
       const StemClass& C = classes[c];
@@ -2919,7 +2919,7 @@ int bpla_gradients(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_k
   const HostPack& PY = ys_->pack;
   std::vector<int32_t> wx, wy, gx, gy;
   std::vector<int64_t> wo, go;
-  const bool general_only = std::getenv("SK_BPLA_GENERAL") != nullptr;  // A/B switch
+  const bool general_only = SK_KNOB("SK_BPLA_GENERAL") != nullptr;  // A/B switch
   for (int64_t k = 0; k < n; ++k) {
     if (!general_only && PX.ex_dyadic[x[k]] && PY.ex_dyadic[y[k]]) {
       wx.push_back(x[k]);
@@ -4063,5 +4063,13 @@ void sk_ribosum_tables(float* s16, float* p256) {
 }
 
 int sk_char2rna(int c) { return sk::char2rna(c); }
+
+int sk_experiments(void) {
+#ifdef SK_EXPERIMENTS
+  return 1;
+#else
+  return 0;
+#endif
+}
 
 }  // extern "C"

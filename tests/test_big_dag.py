@@ -86,6 +86,7 @@ def test_long_gap_edge(gpu_ctx, big_set):
 
 
 @pytest.mark.gpu
+@pytest.mark.explib
 @pytest.mark.parametrize("name", ["ns_L200", "wide_L380_420"])
 def test_forced_big_kernel_at_register_sizes(gpu_ctx, monkeypatch, name):
     dag = np.load(os.path.join(GOLDEN, "large_dag.npz"))

@@ -115,9 +115,9 @@ def test_bpla_y_grouped_items(gpu_ctx, bpla_set, noBP, SW, monkeypatch):
     """Many pairs per y: the fast pairs go to the y-grouped kernel (a
     workgroup stages one y for its waves, each wave streams a chunk of
     pairs back to back); the non-dyadic ones (the 3-row alignment) stay on
-    the general kernel.  The oracle's values for every chunk size, and the
-    same as one pair per wave (bit for bit for the max-plus SW modes; the
-    exp sums only change order)."""
+    the general kernel.  The oracle's values (the chunk sizes and one pair
+    per wave: test_bpla_chunk_sizes_agree, experiments build; bit for bit for
+    the max-plus SW modes, the exp sums only change order)."""
     ds, om = bpla_set
     n = len(om)
     kern = ska.BPLAKernel(noBP=noBP, SW=SW)
@@ -128,6 +128,24 @@ def test_bpla_y_grouped_items(gpu_ctx, bpla_set, noBP, SW, monkeypatch):
     ref = {p: po.kernel_value(kern.params.kind, om[p[0]], om[p[1]], kern.params) for p in uniq}
     want = [ref[p] for p in zip(x.tolist(), y.tolist())]
     assert rel_err(got, want) < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.explib
+@pytest.mark.parametrize("noBP,SW", MODES)
+def test_bpla_chunk_sizes_agree(gpu_ctx, bpla_set, monkeypatch, noBP, SW):
+    """Chunks of 1, 3 and 8 pairs and single-pair launches (experiments
+    build: SK_BPLA_CHUNK, SK_BPLA_NO_ITEMS) against the oracle and the
+    default chunking."""
+    ds, om = bpla_set
+    n = len(om)
+    kern = ska.BPLAKernel(noBP=noBP, SW=SW)
+    x = np.tile(np.arange(n, dtype=np.int32), 24)
+    y = np.repeat(np.array([0, 11, 12], np.int32), x.size // 3 + 1)[: x.size]
+    got = gpu_ctx.pairs(ds, kern, x, y)
+    uniq = sorted(set(zip(x.tolist(), y.tolist())))
+    ref = {p: po.kernel_value(kern.params.kind, om[p[0]], om[p[1]], kern.params) for p in uniq}
+    want = [ref[p] for p in zip(x.tolist(), y.tolist())]
     for chunk in ("1", "3", "8"):
         monkeypatch.setenv("SK_BPLA_CHUNK", chunk)
         assert rel_err(gpu_ctx.pairs(ds, kern, x, y), want) < TOL

@@ -116,12 +116,7 @@ def test_bpla_gradients_tiny_and_ragged(gpu_ctx):
         assert np.all(np.abs(grad[p] - rg[p]) <= 1e-6 * np.abs(rg[p]) + floor), (x[p], y[p], grad[p], rg[p])
 
 
-@pytest.mark.gpu
-def test_bpla_gradients_c4_size_wave_kernel(gpu_ctx, monkeypatch):
-    """C4's 4-row alignments (L 190-210, dyadic profiles: the wave-per-pair
-    kernel with several strips) against the oracle, and the wave kernel
-    against the thread-per-pair kernel (SK_BPLA_GENERAL) on every ordered
-    pair of the set."""
+def _c4_set():
     import os
     g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large_bpla.npz"))
     rows = [str(r) for r in g["rows"]]
@@ -131,15 +126,33 @@ def test_bpla_gradients_c4_size_wave_kernel(gpu_ctx, monkeypatch):
         k += nr
     alns = alns[:4]
     ds, om = make_examples(alns)
-    kern = ska.BPLAKernel(alpha=3.0, beta=0.15)
     n = len(alns)
     x, y = (a.ravel().astype(np.int32) for a in np.meshgrid(np.arange(n), np.arange(n), indexing="ij"))
+    return ds, om, x, y
+
+
+@pytest.mark.gpu
+def test_bpla_gradients_c4_size_wave_kernel(gpu_ctx):
+    """C4's 4-row alignments (L 190-210, dyadic profiles: the wave-per-pair
+    kernel with several strips) against the oracle."""
+    ds, om, x, y = _c4_set()
+    kern = ska.BPLAKernel(alpha=3.0, beta=0.15)
     val, grad = gpu_ctx.bpla_gradients(ds, kern, x, y)
     sel = [0, 1, 6, 11, 15]
     rv, rg = _ref(om, kern, [(int(x[p]), int(y[p])) for p in sel])
     assert rel_err(val[sel], rv) < 1e-6
     for q in range(4):
         assert rel_err(grad[sel, q], rg[:, q]) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.explib
+def test_bpla_gradients_wave_equals_thread_kernel(gpu_ctx, monkeypatch):
+    """The wave kernel against the thread-per-pair kernel (experiments build:
+    SK_BPLA_GENERAL) on every ordered pair of the C4-size set."""
+    ds, om, x, y = _c4_set()
+    kern = ska.BPLAKernel(alpha=3.0, beta=0.15)
+    val, grad = gpu_ctx.bpla_gradients(ds, kern, x, y)
     monkeypatch.setenv("SK_BPLA_GENERAL", "1")
     gv, gg = gpu_ctx.bpla_gradients(ds, kern, x, y)
     assert rel_err(val, gv) < 1e-9

@@ -6,8 +6,9 @@ schedules with both (default), without phi rows (SK_NO_PHI), without
 either (SK_NO_GAMMA), with every read row stored (SK_STORE_ALL: by default a
 row read only by the next one stays in registers) and in the reference
 numbering (SK_REF_ORDER: by default a depth-first order; all four read when a
-dataset is packed) agree to rounding,
-and all match the oracle, on inputs that mix the cases: single sequences,
+dataset is packed, in the experiments build only: test_gamma_switches_agree
+runs under tests/test_explib.py) agree to rounding,
+and the default matches the oracle, on inputs that mix the cases: single sequences,
 gapless alignments (several bp-frequency entries per node: the general
 seeds), gapped alignments (no Gamma / Phi for that y), length bands and
 separate row / column sets."""
@@ -45,16 +46,10 @@ def _gram(ctx, items, kern, switch=None):
 
 
 @pytest.mark.parametrize("band", [0, 4])
-def test_gamma_on_off_and_oracle(gpu_ctx, band):
+def test_gamma_oracle(gpu_ctx, band):
     items = _inputs(0x6A44A + band)
     kern = ska.SuStemKernel(loop_gap=0.4, len_band=band)
     on, om = _gram(gpu_ctx, items, kern)
-    no_phi, _ = _gram(gpu_ctx, items, kern, "SK_NO_PHI")
-    off, _ = _gram(gpu_ctx, items, kern, "SK_NO_GAMMA")
-    stored, _ = _gram(gpu_ctx, items, kern, "SK_STORE_ALL")
-    ref_order, _ = _gram(gpu_ctx, items, kern, "SK_REF_ORDER")
-    assert rel_err(on, off) < 1e-12 and rel_err(no_phi, off) < 1e-12 and rel_err(on, stored) < 1e-14
-    assert rel_err(on, ref_order) < 1e-12
     lm = gpu_ctx.last_launch_ms()
     assert lm["launches"] >= 1 and lm["ms_sum"] > 0.0
     n = len(items)
@@ -62,6 +57,23 @@ def test_gamma_on_off_and_oracle(gpu_ctx, band):
                     for i in range(n)])
     up = np.triu_indices(n)
     assert rel_err(on[up], ref[up]) < 1e-6
+
+
+@pytest.mark.explib
+@pytest.mark.parametrize("band", [0, 4])
+def test_gamma_switches_agree(gpu_ctx, band):
+    """The schedules agree to rounding (experiments build: SK_NO_PHI,
+    SK_NO_GAMMA, SK_STORE_ALL, SK_REF_ORDER are read when a dataset is
+    packed)."""
+    items = _inputs(0x6A44A + band)
+    kern = ska.SuStemKernel(loop_gap=0.4, len_band=band)
+    on, _ = _gram(gpu_ctx, items, kern)
+    no_phi, _ = _gram(gpu_ctx, items, kern, "SK_NO_PHI")
+    off, _ = _gram(gpu_ctx, items, kern, "SK_NO_GAMMA")
+    stored, _ = _gram(gpu_ctx, items, kern, "SK_STORE_ALL")
+    ref_order, _ = _gram(gpu_ctx, items, kern, "SK_REF_ORDER")
+    assert rel_err(on, off) < 1e-12 and rel_err(no_phi, off) < 1e-12 and rel_err(on, stored) < 1e-14
+    assert rel_err(on, ref_order) < 1e-12
 
 
 def test_gamma_row_and_column_sets(gpu_ctx):

@@ -83,6 +83,24 @@ def test_stem4d_gram_matches_oracle(gpu_ctx, model, bound):
 
 
 @pytest.mark.gpu
+def test_stem4d_col_default_oracle(gpu_ctx):
+    """The default full_dp kernel (the column-group kernel for |y| < 512)
+    against the oracle on short sequences, CPL 1-4, empty and one-residue
+    sequences included (the variant comparisons: the explib test below)."""
+    seqs = _seqs() + ["", "G"] + ska.random_sequences(2, 130, 0x5EED0043)
+    ds, _ = make_examples(seqs)
+    kern = ska.StemKernel4D()
+    a = gpu_ctx.gram(ds, kern)
+    assert gpu_ctx.last_classes()["stem4d_col"]
+    n = len(seqs)
+    iu = list(zip(*np.triu_indices(n)))
+    ref = _oracle(seqs, kern, iu)
+    assert rel_err(a[tuple(np.array(iu).T)], ref) < TOL
+    assert a[n - 4, n - 4] == 1.0 and np.all(a[n - 4, :] == 1.0)  # the empty sequence: K = 1
+
+
+@pytest.mark.gpu
+@pytest.mark.explib
 @pytest.mark.parametrize("mode", ["pre", "col", "ksum"])
 def test_stem4d_ksum_equals_four_state(gpu_ctx, monkeypatch, mode):
     """full_dp with the K chain summed (K0(0,n,0,m) = 1 + the sum of every
@@ -359,6 +377,7 @@ def test_stem4d_alignment_constraints_long(gpu_ctx, band):
 
 
 @pytest.mark.gpu
+@pytest.mark.explib
 @pytest.mark.parametrize("band", [0, 5])
 def test_stem4d_stream_parts_identical(gpu_ctx, band, monkeypatch):
     """A batch's pairs dealt to 1-4 parts whose span launches run on their own

@@ -23,7 +23,7 @@ def _items():
 
 
 @pytest.mark.parametrize("use_bp", [True, False])
-def test_string_fast_matches_oracle_and_general(gpu_ctx, use_bp, monkeypatch):
+def test_string_fast_matches_oracle(gpu_ctx, use_bp):
     items = _items()
     ds, om = make_examples(items, use_bp=use_bp)
     n = len(items)
@@ -33,6 +33,17 @@ def test_string_fast_matches_oracle_and_general(gpu_ctx, use_bp, monkeypatch):
                         for i in range(n)])
         up = np.triu_indices(n)
         assert rel_err(got[up], ref[up]) < 1e-6
+
+
+@pytest.mark.explib
+@pytest.mark.parametrize("use_bp", [True, False])
+def test_string_fast_equals_general(gpu_ctx, use_bp, monkeypatch):
+    """The fast paths against the general kernel on the same pairs
+    (experiments build: SK_STR_GENERAL)."""
+    items = _items()
+    ds, om = make_examples(items, use_bp=use_bp)
+    for kern in (ska.StringKernel(gap=0.8, alpha=0.2), ska.StringKernel(gap=0.7, match=1.0, mismatch=0.6)):
+        got = gpu_ctx.gram(ds, kern)
         monkeypatch.setenv("SK_STR_GENERAL", "1")
         gen = gpu_ctx.gram(ds, kern)
         monkeypatch.delenv("SK_STR_GENERAL")

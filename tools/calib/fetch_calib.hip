@@ -41,6 +41,21 @@ __global__ void read8_scatter(const double* __restrict__ a, size_t lines, size_t
   if (s == 12345.678) out[0] = s;
 }
 
+// the same coalesced 8-B read under two names, so the two passes of the
+// re-read case are told apart in the per-dispatch counter file
+__global__ void reread_1(const double* __restrict__ a, size_t n, double* out) {
+  double s = 0.0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    s += a[i];
+  if (s == 12345.678) out[0] = s;
+}
+__global__ void reread_2(const double* __restrict__ a, size_t n, double* out) {
+  double s = 0.0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    s += a[i];
+  if (s == 12345.678) out[0] = s;
+}
+
 int main() {
   const size_t bytes = (size_t)1 << 30;
   double* a = nullptr;
@@ -54,9 +69,24 @@ int main() {
   // bytes touching every line of the 1 GiB once
   hipLaunchKernelGGL(read8_scatter, dim3(4096), dim3(256), 0, 0, a, n8 / 16, (size_t)16, out);
   hipLaunchKernelGGL(read8_scatter, dim3(4096), dim3(256), 0, 0, a, n8 / 8, (size_t)8, out);
+  // re-read of a table that fits the 256 MiB Infinity Cache but not the L2
+  // (4 MiB per XCD): a 64 MiB table written, a 1 GiB stream read to evict it,
+  // then the table read twice back to back (reread_1: from HBM; reread_2:
+  // the Infinity Cache holds it) -- the DAG kernel's child rows are read
+  // 2.8 times on average.  Equal FETCH_SIZE for the two passes means the
+  // counter counts Infinity-Cache hits as fetched bytes.
+  const size_t tb = (size_t)64 << 20;
+  double* t = nullptr;
+  if (hipMalloc(&t, tb) != hipSuccess) return 1;
+  hipLaunchKernelGGL(write8, dim3(4096), dim3(256), 0, 0, t, tb / 8);
+  hipLaunchKernelGGL(read8, dim3(4096), dim3(256), 0, 0, a, n8, out);
+  hipLaunchKernelGGL(reread_1, dim3(4096), dim3(256), 0, 0, t, tb / 8, out);
+  hipLaunchKernelGGL(reread_2, dim3(4096), dim3(256), 0, 0, t, tb / 8, out);
   if (hipDeviceSynchronize() != hipSuccess) return 2;
   std::printf("moved %zu bytes per launch (write8, read8, read16); read8_scatter: one 8-B load per 128-B "
-              "line (%zu loads), then per 64-B line (%zu loads)\n", bytes, n8 / 16, n8 / 8);
+              "line (%zu loads), then per 64-B line (%zu loads); reread_1 / reread_2: a %zu-byte table "
+              "read twice after a 1 GiB eviction stream\n", bytes, n8 / 16, n8 / 8, tb);
+  (void)hipFree(t);
   (void)hipFree(a);
   (void)hipFree(out);
   return 0;

@@ -13,5 +13,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == c:
                 kb = float(r["Counter_Value"])
-                print(c, r["Kernel_Name"].split("(")[0], "KiB", kb, "ratio to 1 GiB", kb * 1024 / 2**30)
+                name = r["Kernel_Name"].split("(")[0]
+                ref = 2**26 if "reread" in name else 2**30
+                print(c, name, "KiB", kb, "ratio to", "64 MiB" if ref == 2**26 else "1 GiB", kb * 1024 / ref)
 PY
