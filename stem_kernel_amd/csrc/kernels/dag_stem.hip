@@ -196,9 +196,15 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_M16
 #define SK_M16 1
 #endif
+// The MAXK 17 class (y of 1,025-1,088 non-leaf nodes: a third of the NS
+// set, L = 200) runs the 12-wave layout of MAXK 16 instead of the 8-wave
+// MAXK 20 class (SK_K17 = 0: no such class)
+#ifndef SK_K17
+#define SK_K17 1
+#endif
 template <int MAXK>
 constexpr bool m16_wide() {
-  return MAXK == 16 && SK_M16 != 0;
+  return (MAXK == 16 || MAXK == 17) && SK_M16 != 0;
 }
 // Sweep weights per y node (gap^2 w(q), 8 B per node; the widest classes
 // w(q) itself, the float, 4 B) instead of per schedule slot (8 B per slot of
@@ -228,8 +234,9 @@ constexpr int pass_width() {
   return (MAXK >= SK_PW2_MIN || m16_wide<MAXK>()) ? 2 : SK_PW;
 }
 // host mirror of pass_width (stem_lds_bytes)
-static inline int pass_width_of(int maxk) { return (maxk >= SK_PW2_MIN || (maxk == 16 && SK_M16 != 0)) ? 2 : SK_PW; }
-static inline bool node_weights_of(int maxk) { return maxk >= SK_NODEW_MIN || (maxk == 16 && SK_M16 != 0); }
+static inline bool m16_wide_of(int maxk) { return (maxk == 16 || maxk == 17) && SK_M16 != 0; }
+static inline int pass_width_of(int maxk) { return (maxk >= SK_PW2_MIN || m16_wide_of(maxk)) ? 2 : SK_PW; }
+static inline bool node_weights_of(int maxk) { return maxk >= SK_NODEW_MIN || m16_wide_of(maxk); }
 #ifndef SK_EDG_MIN  // the narrowest class whose MATCH reads the node-major edges from L2, not LDS
 #define SK_EDG_MIN 64  // off: C5 100.7k against 102.3k pairs/s (r03 A/B; MATCH 14.4k against 9.9k cycles per row)
 #endif
@@ -323,7 +330,7 @@ template <int MAXK>
 __device__ __forceinline__ void add_rows2(double (&S)[MAXK], __amdgpu_buffer_rsrc_t r0,
                                           __amdgpu_buffer_rsrc_t r1, double eg0, double eg1,
                                           int lane) {
-  constexpr int H = (MAXK > SK_HALF_A || (m16_wide<MAXK>() && SK_M16_HALFA)) ? MAXK / 2 : MAXK;
+  constexpr int H = (MAXK > SK_HALF_A || (m16_wide<MAXK>() && SK_M16_HALFA)) ? (MAXK + 1) / 2 : MAXK;
 #pragma unroll
   for (int h0 = 0; h0 < MAXK; h0 += H) {
     double a[H], b[H];
@@ -882,7 +889,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     // per-thread program order makes it visible: no fence.  A row nobody
     // reads (a root) is not stored; it is no child of the next row either.
     // (the widest classes read G1 back in two halves: fewer live registers)
-    constexpr int HD = (MAXK > SK_HALF_D || (m16_wide<MAXK>() && SK_M16_HALFD)) ? MAXK / 2 : MAXK;
+    constexpr int HD = (MAXK > SK_HALF_D || (m16_wide<MAXK>() && SK_M16_HALFD)) ? (MAXK + 1) / 2 : MAXK;
     if (pslot == 0xffffu) {
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) S[k] = egt0 * T0[k] + (NPF >= 2 ? egt1 * T1[k] : 0.0);
@@ -950,7 +957,7 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
 
 template <int MAXK>
 struct StemWaves {
-  static constexpr int value = MAXK <= 12 ? 12 : MAXK <= 16 ? (SK_M16 ? 12 : SK_W16) : MAXK <= 20 ? SK_W20 : 8;
+  static constexpr int value = MAXK <= 12 ? 12 : MAXK <= 17 ? (SK_M16 ? 12 : SK_W16) : MAXK <= 20 ? SK_W20 : 8;
 };
 
 template <int MAXK>
@@ -1223,7 +1230,7 @@ size_t stem_lds_bytes(const StemLaunch& P, int nwaves) {
   return b;
 }
 
-#define SK_STEM_CLASSES(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32)
+#define SK_STEM_CLASSES(X) X(4) X(8) X(12) X(16) X(17) X(20) X(24) X(28) X(32)
 
 static const void* stem_kernel_ptr(int maxk) {
   switch (maxk) {
@@ -1236,7 +1243,9 @@ static const void* stem_kernel_ptr(int maxk) {
 }
 
 int stem_maxk(int max_nl) {
-  const int k = ((std::max(max_nl, 1) + 63) / 64 + 3) & ~3;
+  const int s = (std::max(max_nl, 1) + 63) / 64;  // 64-node slots per lane
+  if (SK_K17 && s == 17) return 17;
+  const int k = (s + 3) & ~3;
   return k <= 32 ? k : -1;
 }
 

@@ -2367,7 +2367,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
         big_o.push_back(k);
       }
     }
-    for (int maxk : {32, 28, 24, 20, 16, 12, 8, 4}) {
+    for (int maxk : {32, 28, 24, 20, 17, 16, 12, 8, 4}) {
       StemClass C;
       C.maxk = maxk;
       bool any = false;
@@ -2731,7 +2731,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
       SK_HIP(ctx, sk::lev_mark(ctx, on_cls ? ctx->cls : S));
       SK_HIP(ctx, sk::launch_stem(SL, C.grid, C.nwaves, on_cls ? ctx->cls : S));
       SK_HIP(ctx, sk::lev_mark(ctx, on_cls ? ctx->cls : S));
-      ctx->last_stem_classes |= 1u << (C.maxk / 4);
+      ctx->last_stem_classes |= 1u << (C.maxk % 4 ? C.maxk : C.maxk / 4);  // (MAXK 17: bit 17)
     }
     if (two_streams) {
       SK_HIP(ctx, hipEventRecord(ctx->evx, ctx->cls));

@@ -616,7 +616,9 @@ class Context:
         ran the column-pipelined full_dp kernel (also in `stem4d`, unbanded)."""
         a, b = C.c_uint32(), C.c_uint32()
         self._chk(lib().sk_last_classes(self._h, C.byref(a), C.byref(b)))
-        maxk = sorted(4 * k for k in range(32) if a.value >> k & 1)
+        # bit MAXK / 4 for the classes of multiples of 4 (0: the big-y kernel),
+        # bit 17 for the MAXK 17 class
+        maxk = sorted((4 * k if k <= 8 else k) for k in range(32) if a.value >> k & 1)
         s4d = sorted({(1 << (k & 3), bool(k & 4)) for k in range(12) if b.value >> k & 1})
         col = sorted(1 << (k & 3) for k in range(8, 12) if b.value >> k & 1)
         return dict(stem_maxk=maxk, stem4d=s4d, stem4d_col=col)

@@ -6,7 +6,8 @@ Which instantiation runs depends on the input size:
 
 * DAG stem kernel (stem_kernel_lite/stem_kernel.cpp:14-95): one register
   class per y example, MAXK = 64-node slots per lane = ceil(non-leaf
-  nodes / 64) rounded up to 4.  C2 (L=150) runs MAXK 16, NS (L=200) 16/20,
+  nodes / 64) rounded up to 4, except 17 slots (1,025-1,088 nodes: its own
+  class since r06).  C2 (L=150) runs MAXK 16, NS (L=200) 16/17/20,
   C5 (L=300) 20/24/28; the L=380/420 examples add 28/32 (2,048 nodes, the
   kernel's limit).  The profile string kernel runs 3-7 strips of 64 rows.
 * 4-D stem kernel full_dp (stem_kernel/stem_kernel.cpp:282-351): CPL = cells
@@ -23,7 +24,7 @@ Expected values come from the CPU oracle (oracle/sk_oracle.c), a line-by-line
 restatement of the reference (parity against the reference's own output is
 unpinned: it ships no fixtures and its DP does not build here).
 
-Run:  python tests/golden/make_golden_large.py      (~1-2 min on 8 cores)
+Run:  python tests/golden/make_golden_large.py [--dag-only]     (~1-2 min on 8 cores)
 """
 import hashlib
 import os
@@ -72,6 +73,16 @@ def dag_sets():
                     (L == 380 or nl > 1792):
                 wide.append(s)
     out["wide_L380_420"] = wide
+    # NS-size y of 1,089-1,280 non-leaf nodes (the MAXK 20 class, since r06's
+    # MAXK 17 class takes 1,025-1,088): the first three such examples of the
+    # NS stream past the six above
+    ns20 = []
+    for s in ska.random_sequences(64, 200, 0x5EED0002)[6:]:
+        ds = ska.Dataset.synthetic([s])
+        nl = int(np.sum(ds.dag(0)["n_edges"] > 0))
+        if 1088 < nl <= 1280 and len(ns20) < 3:
+            ns20.append(s)
+    out["ns20_L200"] = ns20
     return out
 
 
@@ -120,6 +131,8 @@ def main():
                 arrays[f"{name}_K{kind}"] = v
             print(name, n, "examples, L =", sorted({len(s) for s in seqs}), flush=True)
     np.savez_compressed(os.path.join(HERE, "large_dag.npz"), **arrays)
+    if "--dag-only" in sys.argv:
+        return
 
     # 4-D full_dp at C3's L=200 (CPL 4), CPL 8 at |y| = 260, banded partial_dp
     c3 = ska.random_sequences(3, 200, 0x5EED0002)
