@@ -416,7 +416,7 @@ int sk_sync_timing(sk_context *ctx);
  * diagnostic): *stem_maxk_mask has bit MAXK/4 set for every DAG stem register
  * class run (MAXK = 4, 8, ..., 32 64-node slots per lane; bit 17 for the MAXK 17
  * class, y examples of 1,025-1,088 non-leaf nodes) and bit 0 when the
- * big-y kernel ran (y examples over 2,048 non-leaf nodes or with a stem edge
+ * big-y kernel ran (y examples of 2,048 non-leaf nodes or more, or with a stem edge
  * gap over 1,023, which the register classes cannot hold); *stem4d_mask has
  * bit log2(CPL) set for every 4-D stem class run (CPL = 1, 2, 4, 8 cells per
  * lane), shifted by 4 for the banded (partial_dp) variant and by 8 for the

@@ -290,8 +290,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* base, i
   const uint64_t a = (uint64_t)base;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, nly * 8,
-                                           0x00020000);
+  // (the record count through readfirstlane too: a value the compiler
+  // cannot prove uniform turns every load through the descriptor into a
+  // waterfall loop)
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(nly * 8), 0x00020000);
 }
 
 // cache policy bits of the G0 row loads / stores (experiments: 2 = nt)
@@ -380,12 +383,13 @@ template <bool NW, bool NWF>
 __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int lane) {
   const lds_u32* rp = Y.sc + c0 * 64 + lane;
   const lds_f64* wp = Y.ew + (NW ? 0 : c0 * 64 + lane);
-  // NW: the slot's weight from its parent's node weight and g^gaps; a dummy
-  // (child == parent) weighs 0
+  // NW: the slot's weight from its parent's node weight and g^gaps.  A
+  // dummy record reads and writes the class's last slot (the staging's
+  // zslot: no node there -- the classes keep one slot free -- so its R
+  // entry and node weight are 0): it adds 0 * 0, no select needed
   auto nweight = [&](uint32_t rec) __attribute__((always_inline)) -> double {
     const uint32_t pa = (rec >> 11) & 0x7ff;
-    const double w = (NWF ? Y.gap2 * (double)Y.ewf[pa] : Y.ew[pa]) * Y.gp[rec >> 22];
-    return ((rec ^ (rec >> 11)) & 0x7ff) == 0u ? 0.0 : w;
+    return (NWF ? Y.gap2 * (double)Y.ewf[pa] : Y.ew[pa]) * Y.gp[rec >> 22];
   };
   // three chunk slots in rotation (the loop is unrolled by three, so no
   // loaded register is ever copied, which would force a wait for it)
@@ -1019,13 +1023,21 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
       // sweep schedule + two dummy chunks (read ahead past the end), with
       // the edge weights; dummy records have child == parent and weight 0
       const int sb = s.ex_ysc_base[y] * 64, nrec = Y.nch * 64;
-      const int nl1 = max(Y.nl, 1);
+      // dummy records (the schedule's padding and two trailing chunks read
+      // ahead) read and write a free slot past the y's nodes: the classes
+      // hold y of at most 64 MAXK - 1 nodes (stem_maxk(nl + 1)), so there is
+      // one at least, its R entry stays 0 through every sweep and its node
+      // weight is 0 -- a dummy adds 0 * 0 to it, without a select in the sweep
+      // (spread over the free slots by lane: one target for every dummy of a
+      // chunk would serialize their atomics)
+      const int nfree = max(maxnl - Y.nl, 1);
       for (int k = threadIdx.x; k < nrec + 128; k += blockDim.x) {
-        const uint32_t d = (uint32_t)((k & 63) % nl1);
-        const uint32_t r = k < nrec ? s.ysc[sb + k] : (d | (d << 11));
+        uint32_t r = k < nrec ? s.ysc[sb + k] : 0u;
         const uint32_t ch = r & 0x7ff, pa = (r >> 11) & 0x7ff;
+        const uint32_t zs = (uint32_t)(maxnl - 1 - (k & 63) % nfree);
+        if (k >= nrec || ch == pa) r = zs | (zs << 11);
         ysc[k] = r;
-        if (!NW) yew[k] = ch == pa ? 0.0 : gap2 * (double)s.yn_w[nb + pa] * gp[r >> 22];
+        if (!NW) yew[k] = (k >= nrec || ch == pa) ? 0.0 : gap2 * (double)s.yn_w[nb + pa] * gp[r >> 22];
       }
       if (node_weights_f32<MAXK>())
         for (int q = threadIdx.x; q < maxnl; q += blockDim.x) ((lds_f32*)yew)[q] = q < Y.nl ? s.yn_w[nb + q] : 0.0f;

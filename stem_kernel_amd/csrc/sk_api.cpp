@@ -105,9 +105,10 @@ struct HostPack {
   // dyadic and no empty profile column: the string kernel's fast path;
   // every column one residue: its one-hot variant
   std::vector<uint8_t> ex_str_fast, ex_onehot;
-  // y examples the register-class stem kernel cannot take (more than 2048
-  // non-leaf nodes, or a stem edge gap over 1023: its packed 11/11/10-bit
-  // records); they go to sk_dag_stem_big_kernel (level-order arrays)
+  // y examples the register-class stem kernel cannot take (2,048 non-leaf
+  // nodes or more -- each class keeps its last slot free --, or a stem edge
+  // gap over 1023: its packed 11/11/10-bit records); they go to
+  // sk_dag_stem_big_kernel (level-order arrays)
   std::vector<uint8_t> ex_big;
   std::vector<float> ex_nseqs;
   pvec<uint32_t> nd_a, nd_b, nd_c;
@@ -969,7 +970,9 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
     for (int l = 0; l < nlev; ++l) lv[l + 1] += lv[l];
     O.lvl.insert(O.lvl.end(), lv.begin(), lv.end());
     // the register-class kernel's y records: child:11 | parent:11 | gaps:10
-    const bool big = nl > 2048 || big_gap;
+    // (at most 2,047 nodes: every register class keeps its last slot free,
+    // the dummy records' target, dag_stem.hip)
+    const bool big = nl > 2047 || big_gap;
     O.ex_big.push_back(big ? 1 : 0);
 
     // (the y-role records are formed after the x-role pass: pack_y below)
@@ -2349,7 +2352,7 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     std::vector<uint8_t> ybig(ny, 0);
     for (int j = 0; j < ny; ++j) ybig[j] = force_big || PY.ex_big[j] ? 1 : 0;
     auto in_class = [&](int j, int maxk) {
-      return !ybig[j] && sk::stem_maxk(std::max(PY.ex_nl[j], 1)) == maxk;
+      return !ybig[j] && sk::stem_maxk(PY.ex_nl[j] + 1) == maxk;  // (one slot free: dag_stem.hip zslot)
     };
     {
       std::vector<int64_t> bk;  // pairs dealt cyclically to the waves: costliest first

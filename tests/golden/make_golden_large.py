@@ -8,7 +8,7 @@ Which instantiation runs depends on the input size:
   class per y example, MAXK = 64-node slots per lane = ceil(non-leaf
   nodes / 64) rounded up to 4, except 17 slots (1,025-1,088 nodes: its own
   class since r06).  C2 (L=150) runs MAXK 16, NS (L=200) 16/17/20,
-  C5 (L=300) 20/24/28; the L=380/420 examples add 28/32 (2,048 nodes, the
+  C5 (L=300) 20/24/28; the L=380/420 examples add 28/32 (2,047 nodes, the
   kernel's limit).  The profile string kernel runs 3-7 strips of 64 rows.
 * 4-D stem kernel full_dp (stem_kernel/stem_kernel.cpp:282-351): CPL = cells
   per lane = 4 for |y| < 256 (C3, L=200), 8 for 256 <= |y| < 512; banded

@@ -60,9 +60,11 @@ def _expected(name, kind):
 
 
 def _maxk(nl):
-    # dag_stem.hip stem_maxk: 64-node slots per lane, rounded up to a multiple
-    # of 4 -- except 17 slots (1,025-1,088 nodes), a class of its own
-    s = (max(nl, 1) + 63) // 64
+    # sk_api.cpp in_class = dag_stem.hip stem_maxk(nl + 1): 64-node slots per
+    # lane for the y's nodes plus one free slot (the sweep's dummy target),
+    # rounded up to a multiple of 4 -- except 17 slots (1,024-1,087 nodes), a
+    # class of its own
+    s = (nl + 1 + 63) // 64
     return 17 if s == 17 else (s + 3) // 4 * 4
 
 
