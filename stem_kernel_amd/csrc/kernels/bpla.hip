@@ -917,19 +917,21 @@ __device__ __forceinline__ void bpla_fast_chunk3(const BplaLaunch& P, int np, co
   // boundary row; rows B and C take up and diagonal from the row before)
   double sB1 = 0.0, sC1 = 0.0, sC2 = 0.0;
   auto cells = [&](const BplaPos& yc, double dS, double uM, double uX, bool c1) __attribute__((always_inline)) {
+    (void)c1;
     const double eA = expo(xA, yc);
     const double eB = expo(xB, yc);
     const double eC = expo(xC, yc);
     const double sA = aM + aX;
     const double nMA = eA * __builtin_fma(fb, dS, 1.0);
     const double nXA = cbg * uM + cbe * uX;
-    const double nYA = c1 ? 0.0 : bg * sA + be * aY;
+    // (column 1, c1: the wrap reset every left value, so these are 0 -- no select)
+    const double nYA = bg * sA + be * aY;
     const double nMB = __builtin_fma(eB, sA + aY, eB);  // diagonal: row A at j-1
     const double nXB = bg * nMA + be * nXA;
-    const double nYB = c1 ? 0.0 : bg * sB1 + be * bY;
+    const double nYB = bg * sB1 + be * bY;
     const double nMC = __builtin_fma(eC, sB1 + bY, eC);  // diagonal: row B at j-1
     const double nXC = bg * nMB + be * nXB;
-    const double nYC = c1 ? 0.0 : bg * sC1 + be * cY;
+    const double nYC = bg * sC1 + be * cY;
     aM = nMA;
     aX = nXA;
     aY = nYA;
@@ -1021,6 +1023,7 @@ __device__ __forceinline__ void bpla_fast_chunk3(const BplaLaunch& P, int np, co
       dS = 0.0;
       aM = aX = aY = 0.0;  // row A's column 0 (row B's diagonal at column 1)
       sB1 = bY = 0.0;      // row B's column 0 (row C's diagonal at column 1)
+      sC1 = cY = 0.0;      // row C's left at column 1 (cM, cX, sC2 stay: lane w+1's row above)
     }
     const int jb = w + 1;  // lane 0's column (strip s)
     const double* bj = bnd + 3 * (jb <= Ly ? jb : 0);

@@ -173,6 +173,9 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_NPF16  // rows prefetched per row in the MAXK 16 class
 #define SK_NPF16 1
 #endif
+#ifndef SK_NPF17  // ... in the MAXK 17 class
+#define SK_NPF17 1
+#endif
 #ifndef SK_PW  // MATCH pass width in 64-node groups
 #define SK_PW 3  // NS 193.7k against 192.2k pairs/s with 4 (r03, same box)
 #endif
@@ -230,12 +233,17 @@ constexpr bool node_weights_f32() {
 // MATCH pass width in 64-node groups: SK_PW, 2 in the widest classes (the
 // per-wave accumulator is 64 * PW doubles of LDS)
 template <int MAXK>
+#ifndef SK_PW17  // MATCH pass width of the MAXK 17 class
+#define SK_PW17 2
+#endif
 constexpr int pass_width() {
-  return (MAXK >= SK_PW2_MIN || m16_wide<MAXK>()) ? 2 : SK_PW;
+  return MAXK == 17 ? SK_PW17 : (MAXK >= SK_PW2_MIN || m16_wide<MAXK>()) ? 2 : SK_PW;
 }
 // host mirror of pass_width (stem_lds_bytes)
 static inline bool m16_wide_of(int maxk) { return (maxk == 16 || maxk == 17) && SK_M16 != 0; }
-static inline int pass_width_of(int maxk) { return (maxk >= SK_PW2_MIN || m16_wide_of(maxk)) ? 2 : SK_PW; }
+static inline int pass_width_of(int maxk) {
+  return maxk == 17 ? SK_PW17 : (maxk >= SK_PW2_MIN || m16_wide_of(maxk)) ? 2 : SK_PW;
+}
 static inline bool node_weights_of(int maxk) { return maxk >= SK_NODEW_MIN || m16_wide_of(maxk); }
 #ifndef SK_EDG_MIN  // the narrowest class whose MATCH reads the node-major edges from L2, not LDS
 #define SK_EDG_MIN 64  // off: C5 100.7k against 102.3k pairs/s (r03 A/B; MATCH 14.4k against 9.9k cycles per row)
@@ -816,7 +824,8 @@ __device__ double stem_pair(const StemLaunch& P, const YView& Y, lds_f64* R, lds
     //      land during the sweep; this row itself, when a child of the next,
     //      is added from registers in D.
     // rows prefetched per row: two where the register budget allows
-    constexpr int NPF = (MAXK == 16 && (SK_NPF16 == 0 || SK_M16 == 2)) ? 0
+    constexpr int NPF = MAXK == 17 ? SK_NPF17
+                        : (MAXK == 16 && (SK_NPF16 == 0 || SK_M16 == 2)) ? 0
                         : ((MAXK <= 12 && SK_NPF12 == 2) || (MAXK == 16 && SK_NPF16 == 2) ||
                            (MAXK == 20 && SK_W20 == 8 && SK_NPF20 == 2)) ? 2 : 1;
     uint32_t nxt_done = 0;
