@@ -173,8 +173,8 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef SK_NPF16  // rows prefetched per row in the MAXK 16 class
 #define SK_NPF16 1
 #endif
-#ifndef SK_NPF17  // ... in the MAXK 17 class
-#define SK_NPF17 1
+#ifndef SK_NPF17  // ... in the MAXK 17 class: none (with one, the row loop spilled; r06h: +2.5 % without)
+#define SK_NPF17 0
 #endif
 #ifndef SK_PW  // MATCH pass width in 64-node groups
 #define SK_PW 3  // NS 193.7k against 192.2k pairs/s with 4 (r03, same box)
