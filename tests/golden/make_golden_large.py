@@ -83,6 +83,15 @@ def dag_sets():
         if 1088 < nl <= 1280 and len(ns20) < 3:
             ns20.append(s)
     out["ns20_L200"] = ns20
+    # ... and of 896-958 (MAXK 16's lower end; r06k measured 12-wave classes
+    # of 13-15 slots for them, not shipped): the first two such
+    ns15 = []
+    for s in ska.random_sequences(64, 200, 0x5EED0002)[6:]:
+        ds = ska.Dataset.synthetic([s])
+        nl = int(np.sum(ds.dag(0)["n_edges"] > 0))
+        if 896 <= nl <= 958 and len(ns15) < 2:
+            ns15.append(s)
+    out["ns15_L200"] = ns15
     return out
 
 

@@ -3,7 +3,7 @@ L=300, C3 4-D L=200/260, C4 4-row alignments L 190-210), against the oracle
 fixtures of tests/golden/make_golden_large.py.
 
 The GPU tests reach every kernel instantiation the benches launch -- DAG stem
-register classes MAXK 16, 20, 24, 28 and 32, the profile string kernel's 3-7
+register classes MAXK 16, 17, 20, 24, 28 and 32, the profile string kernel's 3-7
 strips, 4-D full_dp CPL 4 and 8 and the banded CPL 4 class, BPLA's 4-strip
 alignments -- and assert through sk_last_classes that they did.  Tolerance:
 1e-6 relative (BASELINE.json north_star, double).
@@ -27,7 +27,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 DAG = np.load(os.path.join(GOLDEN, "large_dag.npz"))
 S4D = np.load(os.path.join(GOLDEN, "large_4d.npz"))
 BPLA = np.load(os.path.join(GOLDEN, "large_bpla.npz"))
-SETS = ["c2_L150", "ns_L200", "ns20_L200", "c5_L300", "wide_L380_420"]
+SETS = ["c2_L150", "ns_L200", "ns15_L200", "ns20_L200", "c5_L300", "wide_L380_420"]
 # 6, 7: the log compositions, 7 the north star's LSuStemStrKernel (the CLI's
 # --log mode): components as the fixtures' K0 (SuStemKernel()) and K2
 # (StringKernel(gap=0.8, alpha=0.2)), which are LSuStemStrKernel()'s
