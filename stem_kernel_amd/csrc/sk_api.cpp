@@ -72,6 +72,34 @@ float4 bpla_weight(const Example& X, int i) {
   return make_float4(std::sqrt(pl), std::sqrt(pr), std::sqrt(pu), 0.f);
 }
 
+// every position's bpla_weight, appended to out, in one pass over the
+// triangle's rows: the same float sums in the same order (pl[i] over j > i,
+// pr[i] over j < i, both by increasing j), O(L^2) with contiguous reads
+void bpla_weights(const Example& X, std::vector<float4>& out) {
+  const int L = X.len;
+  const size_t base = out.size();
+  out.resize(base + (size_t)std::max(L, 0));
+  if (!X.has_bp) {
+    for (int i = 0; i < L; ++i) out[base + i] = make_float4(0.f, 0.f, 1.f, 0.f);
+    return;
+  }
+  std::vector<float> pr((size_t)L, 0.0f);
+  for (int i = 0; i < L; ++i) {
+    float pl = 0.0f;
+    if (i + 1 < L) {
+      const double* row = X.bpp.data() + sk::tri_index(L, i, i + 1);
+      for (int j = i + 1; j < L; ++j) {
+        const double b = row[j - i - 1];
+        pl = (float)((double)pl + b);
+        pr[j] = (float)((double)pr[j] + b);
+      }
+    }
+    float pu = (float)(1.0 - (double)(pl + pr[i]));  // pr[i] is final: rows j < i came first
+    if (pu < 0.0f) pu = 0.0f;
+    out[base + i] = make_float4(std::sqrt(pl), std::sqrt(pr[i]), std::sqrt(pu), 0.f);
+  }
+}
+
 // Packed host image of a dataset (device_set.h layout).
 // vectors whose resize() leaves new elements uninitialised (trivial types):
 // the packed arrays are sized once and filled on host threads, which then
@@ -524,21 +552,22 @@ int fail(sk_context* ctx, int code, const std::string& msg) {
 static void assign_sweep_lanes(const std::vector<int>& take, const std::vector<uint32_t>& er, int nl,
                                uint32_t lanes[64]) {
   const int n = (int)take.size();  // <= 64: fixed arrays, no allocation per chunk
+  // edges per parent in the chunk (a per-thread count table over the 11-bit
+  // parent ids, cleared again after use)
+  thread_local uint8_t npar[2048];
   int cntp[64];
-  {
-    std::pair<uint32_t, int> pp[64];
-    for (int i = 0; i < n; ++i) pp[i] = {(er[take[i]] >> 11) & 0x7ff, i};
-    std::sort(pp, pp + n);
-    for (int a = 0; a < n;) {
-      int b = a;
-      while (b < n && pp[b].first == pp[a].first) ++b;
-      for (int t = a; t < b; ++t) cntp[pp[t].second] = b - a;
-      a = b;
-    }
-  }
+  for (int i = 0; i < n; ++i) ++npar[(er[take[i]] >> 11) & 0x7ff];
+  for (int i = 0; i < n; ++i) cntp[i] = npar[(er[take[i]] >> 11) & 0x7ff];
+  for (int i = 0; i < n; ++i) npar[(er[take[i]] >> 11) & 0x7ff] = 0;
+  // edges by that count, largest first, chunk order among equals (a
+  // counting sort: stable)
   int ord[64];
-  std::iota(ord, ord + n, 0);
-  std::stable_sort(ord, ord + n, [&](int a, int b) { return cntp[a] > cntp[b]; });
+  {
+    int cstart[66] = {0};
+    for (int i = 0; i < n; ++i) ++cstart[64 - cntp[i] + 1];
+    for (int k = 0; k < 65; ++k) cstart[k + 1] += cstart[k];
+    for (int i = 0; i < n; ++i) ord[cstart[64 - cntp[i]]++] = i;
+  }
   int fill[4] = {0, 0, 0, 0};
   int at[4][16];         // group -> parent slot load
   uint32_t rd[2][32][4];  // half -> child slot -> distinct children (up to 4 kept)
@@ -772,12 +801,14 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
         for (int i = nl - 1; i >= 0; --i)
           for (int t = cb[i]; t < cb[i + 1]; ++t) h[i] = std::max(h[i], h[epar[by_child[t]]] + 1);
         for (int f = 0; f < ne_all; ++f) rem[epar[f]]++;
-        typedef std::pair<std::pair<int, int>, int> Key;  // {{-height, child len}, edge}
-        std::priority_queue<Key, std::vector<Key>, std::greater<Key>> ready;
+        // key (-height, child len, edge) packed into one integer, smallest
+        // first: 2^20 - 1 - height:20 | len:16 | edge:28 (nl < 2^16, edges < 2^28)
+        std::priority_queue<uint64_t, std::vector<uint64_t>, std::greater<uint64_t>> ready;
         auto push_edges_of = [&](int c) {
+          const uint64_t len = P.nd_b[nb0 + srt[c]] & 0xffff;
           for (int t = cb[c]; t < cb[c + 1]; ++t) {
             const int f = by_child[t];
-            ready.push({{-h[epar[f]], (int)(P.nd_b[nb0 + srt[c]] & 0xffff)}, f});
+            ready.push(((uint64_t)((1 << 20) - 1 - h[epar[f]]) << 44) | (len << 28) | (uint64_t)f);
           }
         };
         for (int c = 0; c < nl; ++c)
@@ -791,7 +822,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
           take.clear();
           done.clear();
           while (!ready.empty() && (int)take.size() < 64) {
-            take.push_back(ready.top().second);
+            take.push_back((int)(ready.top() & 0xfffffffu));
             ready.pop();
           }
           for (int f : take) {
@@ -908,11 +939,16 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
       level[v] = lv;
       nlev = std::max(nlev, lv + 1);
     }
-    std::vector<int> order;  // non-leaf nodes by (level, reference index)
-    for (int v = 0; v < nn; ++v)
-      if (level[v] >= 0) order.push_back(v);
-    std::stable_sort(order.begin(), order.end(),
-                     [&](int a, int b) { return level[a] < level[b]; });
+    std::vector<int> order;  // non-leaf nodes by (level, reference index): a counting sort
+    {
+      std::vector<int> lstart(nlev + 1, 0);
+      for (int v = 0; v < nn; ++v)
+        if (level[v] >= 0) ++lstart[level[v] + 1];
+      for (int l = 0; l < nlev; ++l) lstart[l + 1] += lstart[l];
+      order.resize(lstart[nlev]);
+      for (int v = 0; v < nn; ++v)
+        if (level[v] >= 0) order[lstart[level[v]]++] = v;
+    }
     const int nl = (int)order.size();
     if (nl >= 0xffff) {
       O.err = "example too large: more than 65534 non-leaf DAG nodes";
@@ -921,6 +957,34 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
     }
     std::vector<int> nid(nn, -1);
     for (int k = 0; k < nl; ++k) nid[order[k]] = k;
+    // per-node gamma (bit 0) / phi (bit 1) row flags, tested once here: the
+    // passes below ask repeatedly
+    // and their (code, len) key's index (looked up once per node)
+    std::vector<uint8_t> fl(nn, 0);
+    std::vector<uint32_t> gix(nn, 0);
+    if (gam_on)
+      for (int v = 0; v < nn; ++v) fl[v] |= is_gamma(X, v) ? 1 : 0;
+    if (phi_on)
+      for (int v = 0; v < nn; ++v) fl[v] |= is_phi(X, v) ? 2 : 0;
+    for (int v = 0; v < nn; ++v)
+      if (fl[v]) gix[v] = gamma_idx(gamma_key(X, v));
+    {
+      const size_t ne_x = (size_t)X.n_edges();
+      for (auto* q : {&O.nd_a, &O.nd_b, &O.nd_c, &O.xr_node, &O.xg_node}) q->reserve(nl);
+      O.nd_w.reserve(nl);
+      O.nd_nbp.reserve(nl);
+      O.nd_P.reserve(nl);
+      O.ed.reserve(ne_x);
+      O.xr_ch.reserve(ne_x);
+      O.xrow.reserve(nl);
+      O.xgrow.reserve(nl);
+      O.xg_ch.reserve(2 * ne_x + nl);
+      O.xg_clg.reserve(2 * ne_x + nl);
+      O.xg_cpf.reserve(2 * ne_x + nl);
+      O.xg_cty.reserve(2 * ne_x + nl);
+      O.bpf_code.reserve(X.bpf_off[nn]);
+      O.bpf_p.reserve(X.bpf_off[nn]);
+    }
     // path weights: number of root->v paths (parents have larger reference ids)
     std::vector<double> Pw(nn, 0.0);
     for (uint32_t r : X.roots) Pw[r] += 1.0;
@@ -1057,10 +1121,10 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
         for (int v = 0; v < nn; ++v)
           for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) ++npar[X.edge_to[k]];
         for (int v = 0; v < nn; ++v) {
-          if (level[v] <= 0 || (phi_on && is_phi(X, v))) continue;
+          if (level[v] <= 0 || (fl[v] & 2)) continue;
           for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1] && k < X.edge_off[v] + 4; ++k) {
             const int c = X.edge_to[k];
-            if (npar[c] == 1 && level[c] >= 0 && !(gam_on && is_gamma(X, c))) {
+            if (npar[c] == 1 && level[c] >= 0 && !(fl[c] & 1)) {
               cand[v] = c;
               break;
             }
@@ -1107,31 +1171,40 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
             const int c = X.edge_to[k];
             if (pos[v] < nn && (first_parent[c] == nn || pos[v] < pos[first_parent[c]])) first_parent[c] = v;
           }
-        std::vector<std::vector<int>> before(nn + 1);
+        // the phi rows moved before each row (first parent nn: the roots'),
+        // in order, as one CSR list
         const bool move = phi_on && !SK_KNOB("SK_PHI_POSTORDER");
-        std::vector<int> o1;
+        std::vector<int> o1, boff(nn + 2, 0), bl;
+        o1.reserve(order.size());
         for (int v : order) {
-          if (move && is_phi(X, v)) before[first_parent[v]].push_back(v);
+          if (move && (fl[v] & 2)) ++boff[first_parent[v] + 1];
           else o1.push_back(v);
+        }
+        for (int i = 0; i <= nn; ++i) boff[i + 1] += boff[i];
+        bl.resize(boff[nn + 1]);
+        {
+          std::vector<int> bf(boff.begin(), boff.end() - 1);
+          for (int v : order)
+            if (move && (fl[v] & 2)) bl[bf[first_parent[v]]++] = v;
         }
         std::vector<int> o2;
         o2.reserve(order.size() + 8);
         for (int v : o1) {
-          auto& b = before[v];
-          const auto it = std::find(b.begin(), b.end(), cand[v]);
-          if (it != b.end()) {
-            std::rotate(it, it + 1, b.end());  // the candidate last
-            for (int u : b) o2.push_back(u);
-          } else if (!b.empty() && cand[v] >= 0 && !o2.empty() && o2.back() == cand[v]) {
+          const auto bb = bl.begin() + boff[v], be = bl.begin() + boff[v + 1];
+          const auto it = std::find(bb, be, cand[v]);
+          if (it != be) {
+            std::rotate(it, it + 1, be);  // the candidate last
+            o2.insert(o2.end(), bb, be);
+          } else if (bb != be && cand[v] >= 0 && !o2.empty() && o2.back() == cand[v]) {
             o2.pop_back();
-            for (int u : b) o2.push_back(u);
+            o2.insert(o2.end(), bb, be);
             o2.push_back(cand[v]);
           } else {
-            for (int u : b) o2.push_back(u);
+            o2.insert(o2.end(), bb, be);
           }
           o2.push_back(v);
         }
-        for (int u : before[nn]) o2.push_back(u);  // roots
+        o2.insert(o2.end(), bl.begin() + boff[nn], bl.begin() + boff[nn + 1]);  // roots
         order.swap(o2);
       }
       // each row's slot is freed at its last parent in this order
@@ -1153,10 +1226,10 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
         for (int v = 0; v < nn; ++v)
           for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k) ++npar[X.edge_to[k]];
         for (int v : order)
-          if (!(gam_on && is_gamma(X, v))) emitted.push_back(v);
+          if (!(fl[v] & 1)) emitted.push_back(v);
         for (size_t i = 0; i + 1 < emitted.size(); ++i) {
           const int v = emitted[i], r = emitted[i + 1];
-          if (npar[v] != 1 || level[r] <= 0 || level[v] < 0 || (phi_on && is_phi(X, r))) continue;
+          if (npar[v] != 1 || level[r] <= 0 || level[v] < 0 || (fl[r] & 2)) continue;
           for (uint32_t k = X.edge_off[r]; k < X.edge_off[r + 1] && k < X.edge_off[r] + 4; ++k)
             if (X.edge_to[k] == v) nostore[v] = 1;
         }
@@ -1164,14 +1237,14 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
       for (int v : order) {
         const uint32_t e0 = X.edge_off[v], e1 = X.edge_off[v + 1];
         const uint32_t b0 = X.bpf_off[v], b1 = X.bpf_off[v + 1];
-        if (gam_on && is_gamma(X, v)) {
-          O.gr_info.push_back(gamma_idx(gamma_key(X, v)) | (X.edge_gaps[e0] << 16));
+        if (fl[v] & 1) {
+          O.gr_info.push_back(gix[v] | (X.edge_gaps[e0] << 16));
           O.gr_pf.push_back(X.bpf_p[b0]);
           O.gr_P.push_back(Pw[v]);
           continue;
         }
         const bool loop = level[v] == 0;
-        const bool phi = phi_on && is_phi(X, v);
+        const bool phi = (fl[v] & 2) != 0;
         uint32_t nch = 0;
         if (phi) {
           // components: per child c a Phi row (type 2) and its Gamma row
@@ -1182,25 +1255,25 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
             const uint32_t kc = gamma_key(X, c);
             const uint32_t pi = phi_idx(kp, kc);
             for (int ty : {2, 4}) {
-              O.xg_ch.push_back(((ty == 2 ? 0x4000u | pi : 0x8000u | gamma_idx(kc))) | (X.edge_gaps[k] << 16));
+              O.xg_ch.push_back(((ty == 2 ? 0x4000u | pi : 0x8000u | gix[c])) | (X.edge_gaps[k] << 16));
               O.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
               O.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
               O.xg_cty.push_back((uint8_t)ty);
             }
             O.phk_idx.push_back(pi);
           }
-          O.xg_ch.push_back(0x8000u | gamma_idx(kp));
+          O.xg_ch.push_back(0x8000u | gix[v]);
           O.xg_clg.push_back(0u);
           O.xg_cpf.push_back(0.0f);
           O.xg_cty.push_back(3);
-          O.gra_gidx.push_back(gamma_idx(kp));
+          O.gra_gidx.push_back(gix[v]);
           O.gra_row.push_back((uint32_t)O.xgrow.size());  // (+ the example's xgrow base)
           nch = 2 * (e1 - e0) + 1;
         } else if (!loop) {
           for (uint32_t k = e0; k < e1; ++k) {
             const int c = X.edge_to[k];
-            if (gam_on && is_gamma(X, c)) {
-              O.xg_ch.push_back((0x8000u | gamma_idx(gamma_key(X, c))) | (X.edge_gaps[k] << 16));
+            if (fl[c] & 1) {
+              O.xg_ch.push_back((0x8000u | gix[c]) | (X.edge_gaps[k] << 16));
               O.xg_clg.push_back(X.edge_gaps[X.edge_off[c]]);
               O.xg_cpf.push_back(X.bpf_p[X.bpf_off[c]]);
               O.xg_cty.push_back(1);
@@ -1280,7 +1353,7 @@ int pack_dataset(sk_dataset* ds, std::string& err, const std::function<void()>* 
       O.pos_w.push_back(X.has_bp ? X.pos_weight[i] : 1.0f);
       O.pos_chr.push_back((uint8_t)X.rows[0][i]);
     }
-    for (int i = 0; i < X.len; ++i) O.pos_lru.push_back(bpla_weight(X, i));
+    bpla_weights(X, O.pos_lru);
     {
       bool dy = true;  // the device's dyadic_sum test (bpla.hip), in host float
       for (int i = 0; i < X.len; ++i)
