@@ -192,7 +192,8 @@ __device__ __forceinline__ void wave_sync() {
 #define SK_NODEW_MIN 20
 #endif
 // The MAXK 16 class: 1 = 12 waves (3 per SIMD at 168 VGPRs: phases A / D in
-// halves, 128-node MATCH passes, per-node sweep weights; 7 VGPRs spilled),
+// halves, 128-node MATCH passes, per-node sweep weights; r06: 32 scratch
+// bytes, item-loop values reloaded per work item, none in the row loop),
 // NS 198.1k against 190.5k pairs/s with 0 (8 waves, one prefetched child row,
 // 196 VGPRs) over two alternating rounds (r04c); 2 = 1 without the
 // prefetched row (no spills): 196.0k.
