@@ -71,7 +71,9 @@ CONFIGS = {
     # against 203.7k / 204.0k with 1/24 and 201.2k / 201.5k with 1/48 on one
     # box (r05w: the class launches' fill and last round over more pairs);
     # the whole Gram in one call (sk_gram_sharded, bench --full) 204.1k (r05r)
-    "ns": dict(kernel="ss", cls="LSuStemStrKernel", n=4096, L=200, slices=16, cid=2, cpu_pairs=12288),
+    # (asynchronous calls, below: +0.7 %, r06q)
+    "ns": dict(kernel="ss", cls="LSuStemStrKernel", n=4096, L=200, slices=16, cid=2, cpu_pairs=12288,
+               async_calls=True),
     # C2's whole Gram is 32,896 pairs (0.2 s): a step is the whole Gram, the
     # unit the reference computes per call (kernel_matrix.cpp:485-575), not a
     # slice whose launch fill and tail would dominate ("whole": steps repeat it)
@@ -82,17 +84,17 @@ CONFIGS = {
     # the CUs idle in its second round)
     "c3": dict(kernel="stem4d", n=1024, L=200, slices=513, cid=2, cpu_pairs=32),
     # async: step t+1 planned while step t runs (sk_set_async): C4 +3.6 % (its
-    # 7 ms steps had 0.6-0.9 ms host gaps); the DAG configs gain <1 % and
-    # their two concurrent class launches would then overlap fully, which
-    # doubles each launch's duration (the per-launch roofline) -- kept
-    # synchronous
+    # 7 ms steps had 0.6-0.9 ms host gaps); NS +0.7 % (214.9k / 214.9k against
+    # 213.2k / 213.4k) and C5 +0.4 % (r06q: the ≈ 25 ms gap between steps --
+    # the all-gather, then the next step's host planning -- is hidden); the
+    # roofline's time base is the launches' span either way
     # C4: a step is 1/6 of the Gram (350k pairs): 20.5-20.8M against 18.5M
     # pairs/s with 1/16 steps on one box (r04u / r04v: the launch's fill and
     # last round of items amortized over 2.7x the work)
     "c4": dict(kernel="bpla", n=2048, L=(190, 210), rows=4, slices=6, cid=3, cpu_pairs=196608, async_calls=True),
     # C5: 1/64 of the Gram per step (525k pairs; 110.2k against 109.0k pairs/s
     # with 1/128 on one box, r04w2)
-    "c5": dict(kernel="stem", n=8192, L=300, slices=64, cid=4, cpu_pairs=4096),
+    "c5": dict(kernel="stem", n=8192, L=300, slices=64, cid=4, cpu_pairs=4096, async_calls=True),
 }
 
 
