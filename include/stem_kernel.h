@@ -149,6 +149,23 @@ int sk_dataset_add_synthetic_rows(sk_dataset *ds, int32_t n, int32_t n_rows,
  * call evaluates from examples built once.  dst must not be uploaded yet. */
 int sk_dataset_add_copy(sk_dataset *dst, const sk_dataset *src, int32_t i);
 int sk_dataset_size(const sk_dataset *ds);
+/* Examples [first, first + count) as bytes -- their labels, built DAGs,
+ * profiles, weights and averaged bp matrices, every field as the dataset
+ * holds it -- into buf (cap bytes); *size = the bytes needed (buf NULL: query
+ * only; SK_ERR_RANGE when cap is short).  sk_dataset_import appends such a
+ * buffer's examples to ds (not uploaded; a malformed buffer appends nothing):
+ * ranks that each build a share of the examples and gather the shares in
+ * rank order hold a dataset that packs bit for bit as one built whole
+ * (stem_kernel_amd/shard.py build_split).  Host-side counterpart of the
+ * reference's MPI Gram, where every rank reads and builds every example
+ * (common/kernel_matrix.cpp:186-261, common/framework.h:308-353). */
+int sk_dataset_export(const sk_dataset *ds, int32_t first, int32_t count, uint8_t *buf,
+                      size_t cap, size_t *size);
+int sk_dataset_import(sk_dataset *ds, const uint8_t *buf, size_t size);
+/* Diagnostic: pack ds on the host (ds not uploaded) and return FNV-1a hashes
+ * of every packed array, y-role records and x-role / per-example arrays (the
+ * lists of tools/pack_compare.cpp). */
+int sk_dataset_pack_digest(sk_dataset *ds, uint64_t *y_hash, uint64_t *x_hash);
 /* label of example i (pointer valid while ds lives) */
 const char *sk_dataset_label(const sk_dataset *ds, int i);
 /* DAG shape of example i: nodes, edges, bp_freq entries, roots, length */

@@ -62,6 +62,10 @@ SIGNATURES = {
                                                 C.POINTER(C.c_char_p), C.c_float, C.c_int32]),
     "sk_dataset_size": (C.c_int, [_P]),
     "sk_dataset_add_copy": (C.c_int, [_P, _P, C.c_int32]),
+    "sk_dataset_export": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_void_p, C.c_size_t,
+                                    C.POINTER(C.c_size_t)]),
+    "sk_dataset_import": (C.c_int, [_P, C.c_void_p, C.c_size_t]),
+    "sk_dataset_pack_digest": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "sk_dataset_label": (C.c_char_p, [_P, C.c_int]),
     "sk_dataset_shape": (C.c_int, [_P, C.c_int, _I32P, _I32P, _I32P, _I32P, _I32P]),
     "sk_dataset_row_traffic": (C.c_int, [_P, C.c_int, _I32P, _I32P, _I32P, _I32P, _I32P, _I32P, _I32P]),

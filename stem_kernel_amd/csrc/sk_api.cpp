@@ -20,6 +20,7 @@
 #include <queue>
 #include <sstream>
 #include <thread>
+#include <type_traits>
 #include <atomic>
 #include <string>
 #include <system_error>
@@ -178,6 +179,18 @@ struct HostPack {
   int32_t max_nl = 0, max_edges = 0, max_bpf = 0, max_nlev = 0, max_len = 0, max_slots = 0;
   int32_t max_nch = 0;
 };
+// every packed array: the y-role records (SK_YBIG and their bases) and the
+// x-role / per-example arrays (SK_BIG, the ex_* vectors, the key tables) --
+// sk_dataset_pack_digest and tools/pack_compare.cpp hash them in this order
+#define SK_PACK_Y_ARRAYS(X) X(yn_a) X(yn_b) X(yn_c) X(ye2) X(ysc) X(yrec) X(yn_w) X(yn_nbp) X(yn_p0) X(yn_P) \
+  X(ycs) X(ex_ysc_base) X(ex_nch) X(ex_ycs_base)
+#define SK_PACK_X_ARRAYS(X) X(nd_a) X(nd_b) X(nd_c) X(nd_w) X(nd_nbp) X(nd_P) X(ed) X(bpf_code) X(bpf_p)     \
+  X(lvl) X(xr_ch) X(xrow) X(xr_node) X(gr_info) X(gr_pf) X(gr_P) X(xg_ch) X(xg_clg) X(xg_cpf) X(xg_cty)     \
+  X(phk_idx) X(gra_gidx) X(gra_row) X(xgrow) X(xg_node) X(pos_prof) X(pos_w) X(pos_chr) X(pos_lru)          \
+  X(ex_phi_bits) X(ex_nl) X(ex_node_base) X(ex_edge_base) X(ex_bpf_base) X(ex_lvl_base) X(ex_nlev) X(ex_len) \
+  X(ex_pos_base) X(ex_has_w) X(ex_dyadic) X(ex_str_fast) X(ex_onehot) X(ex_big) X(ex_nseqs) X(ex_nslots)    \
+  X(ex_xch_base) X(gam_key) X(ex_xg_base) X(ex_nlxg) X(ex_xgch_base) X(ex_gr_base) X(ex_gapless) X(phi_al)   \
+  X(phi_g) X(ex_gra_base) X(ex_phk_base)
 
 }  // namespace
 
@@ -3179,6 +3192,100 @@ int ctx_fail(sk_context* ctx, int code, const std::string& msg) { return fail(ct
 }  // namespace sk
 
 // =================================================================== ABI
+// ---- examples as bytes (a dataset built in rank shares, gathered) --------
+// Layout: "SKEX", version 1, count; per example its label and every Example
+// field in declaration order (PODs raw, vectors as u64 count + elements,
+// strings as u32 length + bytes), little-endian as the host.
+namespace {
+struct ExWriter {
+  uint8_t* buf;
+  size_t cap, n = 0;
+  void raw(const void* p, size_t b) {
+    if (buf && n + b <= cap) std::memcpy(buf + n, p, b);
+    n += b;
+  }
+  template <class T>
+  void pod(const T& v) { raw(&v, sizeof(T)); }
+  void str(const std::string& s) {
+    pod((uint32_t)s.size());
+    raw(s.data(), s.size());
+  }
+  template <class T>
+  void vec(const std::vector<T>& v) {
+    pod((uint64_t)v.size());
+    raw(v.data(), v.size() * sizeof(T));
+  }
+};
+struct ExReader {
+  const uint8_t* buf;
+  size_t size, n = 0;
+  bool ok = true;
+  void raw(void* p, size_t b) {
+    if (!ok || b > size - n) {
+      ok = false;
+      return;
+    }
+    std::memcpy(p, buf + n, b);
+    n += b;
+  }
+  template <class T>
+  void pod(T& v) { raw(&v, sizeof(T)); }
+  void str(std::string& s) {
+    uint32_t l = 0;
+    pod(l);
+    if (!ok || l > size - n) {
+      ok = false;
+      return;
+    }
+    s.assign(reinterpret_cast<const char*>(buf + n), l);
+    n += l;
+  }
+  template <class T>
+  void vec(std::vector<T>& v) {
+    uint64_t c = 0;
+    pod(c);
+    if (!ok || c > (size - n) / sizeof(T)) {
+      ok = false;
+      return;
+    }
+    v.resize((size_t)c);
+    raw(v.data(), (size_t)c * sizeof(T));
+  }
+};
+template <class IO, class E>
+void example_fields(IO& io, E& X) {
+  io.pod(X.len);
+  io.pod(X.n_rows);
+  io.pod(X.has_bp);
+  uint32_t nr = (uint32_t)X.rows.size();
+  io.pod(nr);
+  if constexpr (std::is_same_v<IO, ExReader>) {
+    if (!io.ok || nr > io.size - io.n) {
+      io.ok = false;
+      return;
+    }
+    X.rows.resize(nr);
+  }
+  for (auto& r : X.rows) io.str(r);
+  io.vec(X.prof5);
+  io.pod(X.n_seqs);
+  io.vec(X.pos_weight);
+  io.vec(X.bpp);
+  io.vec(X.first);
+  io.vec(X.last);
+  io.vec(X.weight);
+  io.vec(X.edge_off);
+  io.vec(X.edge_to);
+  io.vec(X.edge_gaps);
+  io.vec(X.bpf_off);
+  io.vec(X.bpf_code);
+  io.vec(X.bpf_p);
+  io.vec(X.roots);
+  io.vec(X.max_pa);
+}
+constexpr uint32_t kExMagic = 0x58454b53u;  // "SKEX"
+}  // namespace
+
 extern "C" {
 
 void sk_kernel_params_default(sk_kernel_params* p, int32_t kind) {
@@ -3349,6 +3456,79 @@ int sk_dataset_add_copy(sk_dataset* dst, const sk_dataset* src, int32_t i) {
   } catch (const std::bad_alloc&) {
     return SK_ERR_ALLOC;
   }
+  return SK_OK;
+}
+
+// ---- examples as bytes: see the helpers above extern "C"
+int sk_dataset_export(const sk_dataset* ds, int32_t first, int32_t count, uint8_t* buf, size_t cap,
+                      size_t* size) {
+  if (!ds || !size || first < 0 || count < 0 || (size_t)first + (size_t)count > ds->ex.size())
+    return SK_ERR_INVALID;
+  ExWriter w{buf, buf ? cap : 0};
+  w.pod(kExMagic);
+  w.pod((uint32_t)1);
+  w.pod((uint32_t)count);
+  for (int32_t i = first; i < first + count; ++i) {
+    w.str(ds->labels[(size_t)i]);
+    example_fields(w, const_cast<Example&>(ds->ex[(size_t)i]));
+  }
+  *size = w.n;
+  return buf && w.n > cap ? SK_ERR_RANGE : SK_OK;
+}
+
+int sk_dataset_import(sk_dataset* ds, const uint8_t* buf, size_t size) {
+  if (!ds || (!buf && size)) return SK_ERR_INVALID;
+  if (ds->uploaded) return SK_ERR_INVALID;
+  ExReader r{buf, size};
+  uint32_t magic = 0, ver = 0, count = 0;
+  r.pod(magic);
+  r.pod(ver);
+  r.pod(count);
+  if (!r.ok || magic != kExMagic || ver != 1) return SK_ERR_INVALID;
+  std::vector<Example> ex;
+  std::vector<std::string> lab;
+  try {
+    for (uint32_t i = 0; i < count && r.ok; ++i) {
+      lab.emplace_back();
+      r.str(lab.back());
+      ex.emplace_back();
+      example_fields(r, ex.back());
+    }
+  } catch (const std::bad_alloc&) {
+    return SK_ERR_ALLOC;
+  }
+  if (!r.ok || r.n != size) return SK_ERR_INVALID;  // nothing appended from a malformed buffer
+  try {
+    ds->ex.insert(ds->ex.end(), std::make_move_iterator(ex.begin()), std::make_move_iterator(ex.end()));
+    ds->labels.insert(ds->labels.end(), lab.begin(), lab.end());
+  } catch (const std::bad_alloc&) {
+    return SK_ERR_ALLOC;
+  }
+  return SK_OK;
+}
+
+int sk_dataset_pack_digest(sk_dataset* ds, uint64_t* y_hash, uint64_t* x_hash) {
+  if (!ds || !y_hash || !x_hash) return SK_ERR_INVALID;
+  if (ds->uploaded) return SK_ERR_INVALID;
+  std::string err;
+  const int rc = pack_dataset(ds, err);
+  if (rc) return rc;
+  const HostPack& P = ds->pack;
+  auto hv = [](const auto& v, uint64_t h) {
+    typedef typename std::decay_t<decltype(v)>::value_type T;
+    const unsigned char* p = reinterpret_cast<const unsigned char*>(v.data());
+    for (size_t i = 0; i < v.size() * sizeof(T); ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return h ^ v.size();
+  };
+  uint64_t hy = 1469598103934665603ull, hx = hy;
+#define SK_DG_Y(f) hy = hv(P.f, hy);
+#define SK_DG_X(f) hx = hv(P.f, hx);
+  SK_PACK_Y_ARRAYS(SK_DG_Y)
+  SK_PACK_X_ARRAYS(SK_DG_X)
+#undef SK_DG_Y
+#undef SK_DG_X
+  *y_hash = hy;
+  *x_hash = hx;
   return SK_OK;
 }
 

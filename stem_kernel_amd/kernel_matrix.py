@@ -370,6 +370,33 @@ class Dataset:
     def __len__(self):
         return lib().sk_dataset_size(self._h)
 
+    def export(self, first: int = 0, count: Optional[int] = None) -> bytearray:
+        """Examples [first, first + count) as bytes (sk_dataset_export): their
+        labels and built DAGs, profiles, weights and bp matrices."""
+        count = len(self) - first if count is None else count
+        need = C.c_size_t()
+        check(lib().sk_dataset_export(self._h, first, count, None, 0, C.byref(need)))
+        out = bytearray(need.value)  # written in place (no intermediate copy)
+        buf = (C.c_char * max(need.value, 1)).from_buffer(out) if need.value else None
+        check(lib().sk_dataset_export(self._h, first, count, buf, need.value, C.byref(need)))
+        return out
+
+    def import_bytes(self, data) -> "Dataset":
+        """Append the examples of an export() (sk_dataset_import; bytes or
+        bytearray)."""
+        n = len(data)
+        if isinstance(data, bytearray) and n:
+            data = (C.c_char * n).from_buffer(data)
+        check(lib().sk_dataset_import(self._h, data, n))
+        return self
+
+    def pack_digest(self):
+        """(y-role, x-role) hashes of the host-packed arrays
+        (sk_dataset_pack_digest; the dataset must not be uploaded)."""
+        hy, hx = C.c_uint64(), C.c_uint64()
+        check(lib().sk_dataset_pack_digest(self._h, C.byref(hy), C.byref(hx)))
+        return hy.value, hx.value
+
     def profile(self, i: int):
         """ProfileSequence columns [len][5] and n_seqs of example i."""
         L = self.shape(i)[4]

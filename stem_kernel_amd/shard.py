@@ -91,6 +91,33 @@ def distributed_gram(compute: Callable[[np.ndarray, np.ndarray], "object"], n: i
     return assemble(out.cpu().numpy().reshape(world, cap), n, world, normalize)
 
 
+def build_split(build: Callable[[int, int], "object"], n: int, group=None):
+    """Build a dataset of n examples in rank shares: rank r of the group
+    builds examples [n*r/N, n*(r+1)/N) with build(first, last) (a Dataset of
+    those examples, in order), the shares are gathered as bytes
+    (Dataset.export / sk_dataset_export) and every rank appends them in rank
+    order -- the same examples, bit for bit, as one rank building all n, so
+    the packed arrays are too (tests/test_distributed.py).  The reference's
+    MPI Gram has every rank read and build every example
+    (common/kernel_matrix.cpp:186-261)."""
+    import torch.distributed as dist
+
+    from .kernel_matrix import Dataset
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    part = build(lo, hi)
+    if len(part) != hi - lo:
+        raise ValueError(f"build({lo}, {hi}) returned {len(part)} examples")
+    parts = [None] * world
+    dist.all_gather_object(parts, part.export(), group=group)
+    out = Dataset()
+    for b in parts:
+        out.import_bytes(b)
+    return out
+
+
 def rccl_init(ctx, group=None) -> None:
     """Give `ctx` its own RCCL communicator over the ranks of a
     torch.distributed group: rank 0 draws the id (sk_comm_unique_id), the
