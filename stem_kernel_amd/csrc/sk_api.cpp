@@ -345,6 +345,10 @@ void run_slices(int n, F&& f) {
   for (int t : here) f(t);
   for (auto& x : th) x.join();
 }
+// host threads of a call's planning passes (the box gives a job 16)
+int plan_threads(int want) {
+  return std::max(1, std::min({want, 16, (int)std::max(1u, std::thread::hardware_concurrency())}));
+}
 template <class F>
 void run_pool(int n, F&& work) {
   std::vector<std::thread> th;
@@ -2410,18 +2414,24 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
     // within one y, costliest x first: the waves of a workgroup take the
     // item's pairs round-robin, so equal-cost rounds and a cheap last round
     // (one packed key per pair, ties by input order: deterministic)
+    // (the y's on host threads: each sorts its own range of byy)
     {
-      std::vector<uint64_t> key;
-      for (int j = 0; j < ny; ++j) {
-        const int64_t b = cnt[j], e = cnt[j + 1];
-        if (e - b < 2) continue;
-        key.resize(e - b);
-        for (int64_t t = b; t < e; ++t)
-          key[t - b] = ((uint64_t)(0xffffffffu - (uint32_t)PX.ex_nl[x[byy[t]]]) << 32) | (uint32_t)(t - b);
-        std::sort(key.begin(), key.end());
-        std::vector<int64_t> tmp(byy.begin() + b, byy.begin() + e);
-        for (int64_t t = b; t < e; ++t) byy[t] = tmp[(uint32_t)key[t - b]];
-      }
+      std::atomic<int> nextj{0};
+      auto work = [&]() {
+        std::vector<uint64_t> key;
+        std::vector<int64_t> tmp;
+        for (int j = nextj.fetch_add(1); j < ny; j = nextj.fetch_add(1)) {
+          const int64_t b = cnt[j], e = cnt[j + 1];
+          if (e - b < 2) continue;
+          key.resize(e - b);
+          for (int64_t t = b; t < e; ++t)
+            key[t - b] = ((uint64_t)(0xffffffffu - (uint32_t)PX.ex_nl[x[byy[t]]]) << 32) | (uint32_t)(t - b);
+          std::sort(key.begin(), key.end());
+          tmp.assign(byy.begin() + b, byy.begin() + e);
+          for (int64_t t = b; t < e; ++t) byy[t] = tmp[(uint32_t)key[t - b]];
+        }
+      };
+      run_pool(plan_threads(n / 65536 + 1), work);
     }
     ixs.resize(n);
     ioidx.resize(n);
@@ -2565,25 +2575,33 @@ int run_pairs(sk_context* ctx, sk_dataset* xs_, sk_dataset* ys_, const sk_kernel
   if (phi_on) {
     // union of the x's key bitsets, keys ordered by gamma key (the kernel
     // forms one H row per gamma key and wave)
+    // (contiguous item ranges on host threads, concatenated in item order)
     const size_t W = (PX.phi_al.size() + 63) / 64;
-    std::vector<uint64_t> acc(W);
-    std::vector<int32_t> keys;
-    item_phi_off.assign(1, 0);
-    for (size_t i = 0; i < items.size(); ++i) {
-      const int4 it = items[i];
-      if (PY.ex_gapless[it.x]) {
-        std::fill(acc.begin(), acc.end(), 0ull);
-        for (int t = it.y; t < it.y + it.z; ++t) {
-          const uint64_t* b = PX.ex_phi_bits.data() + (size_t)ixs[t] * W;
-          for (size_t w = 0; w < W; ++w) acc[w] |= b[w];
+    const size_t ni = items.size();
+    const int T = plan_threads((int)(ni / 512 + 1));
+    std::vector<std::vector<int32_t>> tkeys(T), tcnt(T);
+    run_slices(T, [&](int t) {
+      std::vector<uint64_t> acc(W);
+      for (size_t i = ni * t / T; i < ni * (t + 1) / T; ++i) {
+        const int4 it = items[i];
+        const size_t k0 = tkeys[t].size();
+        if (PY.ex_gapless[it.x]) {
+          std::fill(acc.begin(), acc.end(), 0ull);
+          for (int u = it.y; u < it.y + it.z; ++u) {
+            const uint64_t* b = PX.ex_phi_bits.data() + (size_t)ixs[u] * W;
+            for (size_t w = 0; w < W; ++w) acc[w] |= b[w];
+          }
+          // (phi keys are numbered in gamma key order: the bits come sorted)
+          for (size_t w = 0; w < W; ++w)
+            for (uint64_t m = acc[w]; m; m &= m - 1) tkeys[t].push_back((int32_t)(w * 64 + __builtin_ctzll(m)));
         }
-        keys.clear();
-        for (size_t w = 0; w < W; ++w)
-          for (uint64_t m = acc[w]; m; m &= m - 1) keys.push_back((int32_t)(w * 64 + __builtin_ctzll(m)));
-        // (phi keys are numbered in gamma key order: the bits come sorted)
-        item_phi.insert(item_phi.end(), keys.begin(), keys.end());
+        tcnt[t].push_back((int32_t)(tkeys[t].size() - k0));
       }
-      item_phi_off.push_back((int32_t)item_phi.size());
+    });
+    item_phi_off.assign(1, 0);
+    for (int t = 0; t < T; ++t) {
+      item_phi.insert(item_phi.end(), tkeys[t].begin(), tkeys[t].end());
+      for (int32_t c : tcnt[t]) item_phi_off.push_back(item_phi_off.back() + c);
     }
     if (std::getenv("SK_PHI_STATS"))
       std::fprintf(stderr, "[phi] keys=%zu items=%zu item keys=%zu pairs=%lld phi components=%zu rows=%zu\n",
