@@ -67,12 +67,13 @@ PEAK_FP64_TFS = 78.6    # FP64 vector
 # the written Gram (in the plain sum the stem term is ~1e-32 of the string
 # term at L=200).  Same two DPs, plus a log epilogue in sk_combine_kernel.
 CONFIGS = {
-    # NS: a step is 1/16 of the Gram (524k pairs): 206.2k / 206.1k pairs/s
-    # against 203.7k / 204.0k with 1/24 and 201.2k / 201.5k with 1/48 on one
-    # box (r05w: the class launches' fill and last round over more pairs);
-    # the whole Gram in one call (sk_gram_sharded, bench --full) 204.1k (r05r)
+    # NS: a step is 1/8 of the Gram (1.05M pairs, 4.8 s): 219.9k / 219.8k
+    # pairs/s against 218.4k / 218.3k with 1/16 on one box (r06u; r05w: 1/16
+    # 206.2k, 1/24 203.7k, 1/48 201.2k -- the class launches' fill and last
+    # round over more pairs); the whole Gram in one call (sk_gram_sharded,
+    # bench --full) 220.0k (r06s); 8 divides the driver's 1, 2, 4 and 8 GPUs
     # (asynchronous calls, below: +0.7 %, r06q)
-    "ns": dict(kernel="ss", cls="LSuStemStrKernel", n=4096, L=200, slices=16, cid=2, cpu_pairs=12288,
+    "ns": dict(kernel="ss", cls="LSuStemStrKernel", n=4096, L=200, slices=8, cid=2, cpu_pairs=12288,
                async_calls=True),
     # C2's whole Gram is 32,896 pairs (0.2 s): a step is the whole Gram, the
     # unit the reference computes per call (kernel_matrix.cpp:485-575), not a
