@@ -768,6 +768,14 @@ def main():
         if a.cpu_stub:
             for r in range(world):
                 slice_of(a.warmup + a.steps - 1, r)
+    if rank == 0:  # a line on stderr every minute: a long run is visibly alive
+        import threading
+
+        def heartbeat(t_start=time.perf_counter()):
+            while True:
+                time.sleep(60)
+                print(f"[bench] running, {time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+        threading.Thread(target=heartbeat, daemon=True).start()
     for w in range(a.warmup):
         run_step(w)
     eng.sync()
