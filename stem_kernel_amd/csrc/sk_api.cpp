@@ -3274,7 +3274,9 @@ template <class IO, class E>
 void example_fields(IO& io, E& X) {
   io.pod(X.len);
   io.pod(X.n_rows);
-  io.pod(X.has_bp);
+  uint8_t hb = X.has_bp ? 1 : 0;  // (a byte on the wire, not a bool's object representation)
+  io.pod(hb);
+  if constexpr (std::is_same_v<IO, ExReader>) X.has_bp = hb != 0;
   uint32_t nr = (uint32_t)X.rows.size();
   io.pod(nr);
   if constexpr (std::is_same_v<IO, ExReader>) {
@@ -3302,6 +3304,41 @@ void example_fields(IO& io, E& X) {
   io.vec(X.max_pa);
 }
 constexpr uint32_t kExMagic = 0x58454b53u;  // "SKEX"
+
+// The invariants example_build.cpp establishes and the packer and kernels
+// rely on (sizes, offsets, children numbered before parents, positions and
+// bp-frequency codes in range): an imported example must hold them all.
+bool example_valid(const Example& X) {
+  const size_t L = X.len >= 0 ? (size_t)X.len : 0;
+  if (X.len < 0 || X.n_rows < 1 || X.rows.size() != (size_t)X.n_rows) return false;
+  for (const auto& r : X.rows)
+    if (r.size() != L) return false;
+  if (X.prof5.size() != L * 5) return false;
+  const size_t nn = X.first.size();
+  if (X.last.size() != nn || X.weight.size() != nn) return false;
+  if (X.edge_off.size() != nn + 1 || X.bpf_off.size() != nn + 1 || X.edge_off[0] != 0 || X.bpf_off[0] != 0)
+    return false;
+  for (size_t v = 0; v < nn; ++v) {
+    if (X.edge_off[v + 1] < X.edge_off[v] || X.bpf_off[v + 1] < X.bpf_off[v]) return false;
+    if (X.first[v] > X.last[v] || X.last[v] >= L) return false;
+  }
+  if (X.edge_to.size() != X.edge_off[nn] || X.edge_gaps.size() != X.edge_off[nn]) return false;
+  if (X.bpf_code.size() != X.bpf_off[nn] || X.bpf_p.size() != X.bpf_off[nn]) return false;
+  for (size_t v = 0; v < nn; ++v)
+    for (uint32_t k = X.edge_off[v]; k < X.edge_off[v + 1]; ++k)
+      if (X.edge_to[k] >= v) return false;  // children before parents
+  for (uint8_t c : X.bpf_code)
+    if (c >= 16) return false;
+  for (uint32_t r : X.roots)
+    if (r >= nn) return false;
+  if (X.has_bp) {
+    if (X.bpp.size() != (L > 1 ? L * (L - 1) / 2 : 0) || X.pos_weight.size() != L || X.max_pa.size() != nn)
+      return false;
+  } else if (nn != 0) {
+    return false;
+  }
+  return true;
+}
 }  // namespace
 
 extern "C" {
@@ -3516,6 +3553,8 @@ int sk_dataset_import(sk_dataset* ds, const uint8_t* buf, size_t size) {
     return SK_ERR_ALLOC;
   }
   if (!r.ok || r.n != size) return SK_ERR_INVALID;  // nothing appended from a malformed buffer
+  for (const Example& X : ex)
+    if (!example_valid(X)) return SK_ERR_INVALID;
   try {
     ds->ex.insert(ds->ex.end(), std::make_move_iterator(ex.begin()), std::make_move_iterator(ex.end()));
     ds->labels.insert(ds->labels.end(), lab.begin(), lab.end());

@@ -73,6 +73,27 @@ def test_malformed_buffers_append_nothing(seqs):
     assert len(b) == 1
 
 
+def test_inconsistent_examples_rejected(seqs):
+    """A well-framed buffer whose example breaks the builder's invariants
+    (here: its length no longer matches its rows and profile) appends
+    nothing."""
+    a = ska.Dataset.synthetic(seqs[:2], labels=["+1", "-1"])
+    data = bytearray(a.export())
+    lab = int.from_bytes(data[12:16], "little")
+    off = 16 + lab  # example 0's len (int32) after the header and its label
+    L = int.from_bytes(data[off:off + 4], "little", signed=True)
+    assert L == len(seqs[0])
+    data[off:off + 4] = (L + 1).to_bytes(4, "little", signed=True)
+    b = ska.Dataset()
+    with pytest.raises(RuntimeError):
+        b.import_bytes(data)
+    assert len(b) == 0
+    # no bp information (MData(ma)): no DAG, still a valid example
+    ds = ska.Dataset()
+    ds.add("+1", [seqs[0]], None, use_bp=False)
+    assert len(ska.Dataset().import_bytes(ds.export())) == 1
+
+
 def test_export_bounds_and_short_buffer(seqs):
     a = ska.Dataset.synthetic(seqs[:2])
     need = C.c_size_t()
