@@ -78,7 +78,9 @@ CONFIGS = {
     # C2's whole Gram is 32,896 pairs (0.2 s): a step is the whole Gram, the
     # unit the reference computes per call (kernel_matrix.cpp:485-575), not a
     # slice whose launch fill and tail would dominate ("whole": steps repeat it)
-    "c2": dict(kernel="ss", n=256, L=150, slices=1, whole=True, cid=1, cpu_pairs=12288),
+    # (asynchronous: 261.3k / 262.1k against 259.4k / 259.6k, r06ab; C3 gains
+    # nothing from it, 1,590-1,591 either way, and stays synchronous)
+    "c2": dict(kernel="ss", n=256, L=150, slices=1, whole=True, cid=1, cpu_pairs=12288, async_calls=True),
     # C3: 1,023 pairs per step, one workgroup per pair (LDS: one per CU), so
     # four rounds of 256 CUs: 591.8 / 755.2 / 759.5 pairs/s for 384 / 768 /
     # 1,023 pairs on one box (r05j, an earlier column kernel; 384 leaves half
