@@ -3586,6 +3586,7 @@ int sk_dataset_pack_digest(sk_dataset* ds, uint64_t* y_hash, uint64_t* x_hash) {
 #undef SK_DG_X
   *y_hash = hy;
   *x_hash = hx;
+  ds->pack = HostPack();  // (the upload packs again: do not hold the arrays until then)
   return SK_OK;
 }
 
