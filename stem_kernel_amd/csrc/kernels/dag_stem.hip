@@ -393,9 +393,9 @@ __device__ __forceinline__ void iy_sweep(const YView& Y, lds_f64* R, int c0, int
   const lds_u32* rp = Y.sc + c0 * 64 + lane;
   const lds_f64* wp = Y.ew + (NW ? 0 : c0 * 64 + lane);
   // NW: the slot's weight from its parent's node weight and g^gaps.  A
-  // dummy record reads and writes the class's last slot (the staging's
-  // zslot: no node there -- the classes keep one slot free -- so its R
-  // entry and node weight are 0): it adds 0 * 0, no select needed
+  // dummy record reads and writes a free slot past the y's nodes (the
+  // staging's choice, by lane; the classes keep one slot free at least): its
+  // R entry and node weight are 0, so it adds 0 * 0 -- no select needed
   auto nweight = [&](uint32_t rec) __attribute__((always_inline)) -> double {
     const uint32_t pa = (rec >> 11) & 0x7ff;
     return (NWF ? Y.gap2 * (double)Y.ewf[pa] : Y.ew[pa]) * Y.gp[rec >> 22];
@@ -1031,7 +1031,7 @@ __global__ void __launch_bounds__(64 * StemWaves<MAXK>::value) sk_dag_stem_kerne
     {
       const int ne = s.ex_edge_base[y + 1] - eb;
       // sweep schedule + two dummy chunks (read ahead past the end), with
-      // the edge weights; dummy records have child == parent and weight 0
+      // the edge weights (weight 0 for the dummies)
       const int sb = s.ex_ysc_base[y] * 64, nrec = Y.nch * 64;
       // dummy records (the schedule's padding and two trailing chunks read
       // ahead) read and write a free slot past the y's nodes: the classes
